@@ -1,0 +1,289 @@
+"""ctypes mirror of include/apd_hip.h and a thin Python driver for libapd_hip.so.
+
+This is plumbing for tests and bench.py: the product is the C-ABI library itself. The structures
+below are byte-for-byte the C ones; `ProblemArrays` keeps the numpy buffers alive while a call is in
+flight. Loading fails loudly (ApdError) when the HIP library is missing: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "lib", "libapd_hip.so")
+
+MAX_IMAGES = 32
+ANCHOR_NUM = 9
+FIRST_INIT, REFINE_INIT, REFINE_ITER = 0, 1, 2
+WEAK, STRONG, UNKNOWN = 0, 1, 2
+
+STATUS = {0: "APD_OK", -1: "APD_EINVAL", -2: "APD_ENOMEM", -3: "APD_EDEVICE", -4: "APD_ETOOMANYVIEWS",
+          -5: "APD_ESTATE"}
+
+
+class ApdError(RuntimeError):
+    pass
+
+
+class ApdCamera(C.Structure):
+    _fields_ = [("K", C.c_float * 9), ("R", C.c_float * 9), ("t", C.c_float * 3), ("c", C.c_float * 3),
+                ("height", C.c_int32), ("width", C.c_int32), ("depth_min", C.c_float), ("depth_max", C.c_float),
+                ("interval", C.c_float), ("depth_num", C.c_float)]
+
+
+assert C.sizeof(ApdCamera) == 120
+
+
+class ApdParams(C.Structure):
+    _fields_ = [("max_iterations", C.c_int32), ("num_images", C.c_int32), ("top_k", C.c_int32),
+                ("depth_min", C.c_float), ("depth_max", C.c_float), ("geom_consistency", C.c_int32),
+                ("use_impetus", C.c_int32), ("strong_radius", C.c_int32), ("strong_increment", C.c_int32),
+                ("weak_radius", C.c_int32), ("weak_increment", C.c_int32), ("use_APD", C.c_int32),
+                ("use_sa", C.c_int32), ("weak_peak_radius", C.c_int32), ("rotate_time", C.c_int32),
+                ("ransac_threshold", C.c_float), ("geom_factor", C.c_float), ("state", C.c_int32)]
+
+
+class ApdProblem(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("num_images", C.c_int32),
+                ("images", C.POINTER(C.POINTER(C.c_float))), ("cameras", C.POINTER(ApdCamera)),
+                ("params", ApdParams), ("depths", C.POINTER(C.POINTER(C.c_float))),
+                ("init_planes", C.POINTER(C.c_float)), ("weak_info", C.POINTER(C.c_uint8)),
+                ("confidence", C.POINTER(C.c_uint8)), ("sa_mask", C.POINTER(C.c_uint8)), ("seed", C.c_uint64)]
+
+
+class ApdOutputs(C.Structure):
+    _fields_ = [("planes", C.POINTER(C.c_float)), ("weak_info", C.POINTER(C.c_uint8)),
+                ("confidence", C.POINTER(C.c_uint8)), ("costs", C.POINTER(C.c_float)),
+                ("selected_views", C.POINTER(C.c_uint32)), ("view_weights", C.POINTER(C.c_uint8)),
+                ("anchors", C.POINTER(C.c_int16)), ("weak_count", C.POINTER(C.c_int32)),
+                ("reliable_curve", C.POINTER(C.c_float))]
+
+
+class ApdTiming(C.Structure):
+    _fields_ = [("total_ms", C.c_float), ("init_ms", C.c_float), ("anchors_ms", C.c_float),
+                ("sweep_ms", C.c_float), ("post_ms", C.c_float), ("iter_ms", C.c_float * 8),
+                ("iterations", C.c_int32)]
+
+
+def default_params(num_images: int, depth_min: float, depth_max: float, **kw) -> ApdParams:
+    """PatchMatchParams defaults (main.h:80-100) with the scaled depth range (APD.cpp:554-555)."""
+    p = ApdParams(max_iterations=3, num_images=num_images, top_k=4, depth_min=depth_min, depth_max=depth_max,
+                  geom_consistency=0, use_impetus=1, strong_radius=5, strong_increment=2, weak_radius=5,
+                  weak_increment=5, use_APD=0, use_sa=1, weak_peak_radius=6, rotate_time=4,
+                  ransac_threshold=0.005, geom_factor=0.2, state=FIRST_INIT)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def _ptr(a: Optional[np.ndarray], ctype):
+    if a is None:
+        return C.POINTER(ctype)()
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+@dataclass
+class ProblemArrays:
+    """Owns every numpy buffer an ApdProblem points into."""
+    width: int
+    height: int
+    images: Sequence[np.ndarray]
+    cameras: Sequence[dict]
+    params: ApdParams
+    depths: Optional[Sequence[np.ndarray]] = None
+    init_planes: Optional[np.ndarray] = None  # HxWx4 {world normal, depth}
+    weak_info: Optional[np.ndarray] = None
+    confidence: Optional[np.ndarray] = None
+    sa_mask: Optional[np.ndarray] = None
+    seed: int = 0x5EED
+
+    def build(self) -> ApdProblem:
+        n = len(self.images)
+        self._imgs = [np.ascontiguousarray(i, np.float32) for i in self.images]
+        self._img_ptrs = (C.POINTER(C.c_float) * n)(*[_ptr(i, C.c_float) for i in self._imgs])
+        self._cams = (ApdCamera * n)()
+        for i, cv in enumerate(self.cameras):
+            cam = self._cams[i]
+            for k, v in cv.items():
+                if isinstance(v, np.ndarray):
+                    getattr(cam, k)[:] = [float(x) for x in v]
+                else:
+                    setattr(cam, k, v)
+        if self.depths is not None:
+            self._deps = [np.ascontiguousarray(d, np.float32) for d in self.depths]
+            dptrs = (C.POINTER(C.c_float) * n)(*[_ptr(d, C.c_float) for d in self._deps])
+            self._dep_ptrs = dptrs
+        else:
+            self._dep_ptrs = None
+        self._planes = None if self.init_planes is None else np.ascontiguousarray(self.init_planes, np.float32)
+        self._weak = None if self.weak_info is None else np.ascontiguousarray(self.weak_info, np.uint8)
+        self._conf = None if self.confidence is None else np.ascontiguousarray(self.confidence, np.uint8)
+        self._sa = None if self.sa_mask is None else np.ascontiguousarray(self.sa_mask, np.uint8)
+        pb = ApdProblem()
+        pb.width, pb.height, pb.num_images = self.width, self.height, n
+        pb.images = C.cast(self._img_ptrs, C.POINTER(C.POINTER(C.c_float)))
+        pb.cameras = C.cast(self._cams, C.POINTER(ApdCamera))
+        pb.params = self.params
+        pb.params.num_images = n
+        pb.depths = C.cast(self._dep_ptrs, C.POINTER(C.POINTER(C.c_float))) if self._dep_ptrs is not None \
+            else C.POINTER(C.POINTER(C.c_float))()
+        pb.init_planes = _ptr(self._planes, C.c_float)
+        pb.weak_info = _ptr(self._weak, C.c_uint8)
+        pb.confidence = _ptr(self._conf, C.c_uint8)
+        pb.sa_mask = _ptr(self._sa, C.c_uint8)
+        pb.seed = self.seed
+        self._pb = pb
+        return pb
+
+
+class Outputs:
+    """Host buffers for apd_outputs, allocated for one problem size."""
+
+    def __init__(self, width: int, height: int, num_src: int, want_curve: bool = False, max_weak: int = 0):
+        hw = width * height
+        self.planes = np.zeros((height, width, 4), np.float32)
+        self.weak_info = np.zeros((height, width), np.uint8)
+        self.confidence = np.zeros((height, width), np.uint8)
+        self.costs = np.zeros((height, width), np.float32)
+        self.selected_views = np.zeros((height, width), np.uint32)
+        self.view_weights = np.zeros((num_src, height, width), np.uint8)
+        self.anchors = np.zeros((max(max_weak, 1), ANCHOR_NUM, 2), np.int16)
+        self.weak_count = np.zeros(1, np.int32)
+        self.reliable_curve = np.zeros((hw, 61), np.float32) if want_curve else None
+
+    def struct(self) -> ApdOutputs:
+        o = ApdOutputs()
+        o.planes = _ptr(self.planes, C.c_float)
+        o.weak_info = _ptr(self.weak_info, C.c_uint8)
+        o.confidence = _ptr(self.confidence, C.c_uint8)
+        o.costs = _ptr(self.costs, C.c_float)
+        o.selected_views = _ptr(self.selected_views, C.c_uint32)
+        o.view_weights = _ptr(self.view_weights, C.c_uint8)
+        o.anchors = _ptr(self.anchors, C.c_int16)
+        o.weak_count = _ptr(self.weak_count, C.c_int32)
+        o.reliable_curve = _ptr(self.reliable_curve, C.c_float)
+        return o
+
+
+EXPORTS = ["apd_abi_version", "apd_device_count", "apd_create", "apd_destroy", "apd_last_error",
+           "apd_set_problem", "apd_run_patchmatch", "apd_stage_prepare", "apd_stage_iteration",
+           "apd_stage_finish", "apd_synchronize", "apd_get_results", "apd_get_timing", "apd_profile_reset",
+           "apd_profile_query", "apd_epilogue"]
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    if not os.path.exists(path):
+        raise ApdError(f"libapd_hip.so not built at {path}: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(path)
+    lib.apd_abi_version.restype = C.c_int32
+    lib.apd_device_count.restype = C.c_int32
+    lib.apd_create.restype = C.c_void_p
+    lib.apd_create.argtypes = [C.c_int32]
+    lib.apd_destroy.argtypes = [C.c_void_p]
+    lib.apd_last_error.restype = C.c_char_p
+    lib.apd_last_error.argtypes = [C.c_void_p]
+    for name in ["apd_run_patchmatch", "apd_stage_prepare", "apd_stage_finish", "apd_synchronize"]:
+        getattr(lib, name).restype = C.c_int32
+        getattr(lib, name).argtypes = [C.c_void_p]
+    lib.apd_set_problem.restype = C.c_int32
+    lib.apd_set_problem.argtypes = [C.c_void_p, C.POINTER(ApdProblem)]
+    lib.apd_stage_iteration.restype = C.c_int32
+    lib.apd_stage_iteration.argtypes = [C.c_void_p, C.c_int32]
+    lib.apd_get_results.restype = C.c_int32
+    lib.apd_get_results.argtypes = [C.c_void_p, C.POINTER(ApdOutputs)]
+    lib.apd_get_timing.restype = C.c_int32
+    lib.apd_get_timing.argtypes = [C.c_void_p, C.POINTER(ApdTiming)]
+    lib.apd_profile_reset.restype = C.c_int32
+    lib.apd_profile_reset.argtypes = [C.c_void_p, C.c_int32]
+    lib.apd_profile_query.restype = C.c_int32
+    lib.apd_profile_query.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                                      C.POINTER(C.c_int64)]
+    lib.apd_epilogue.restype = C.c_int32
+    lib.apd_epilogue.argtypes = [C.c_int32, C.c_int32, C.POINTER(C.c_float), C.c_float, C.c_float,
+                                 C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_uint8)]
+    return lib
+
+
+class Engine:
+    """One apd_ctx on one HIP device."""
+
+    def __init__(self, device: int = 0, lib: Optional[C.CDLL] = None):
+        self.lib = lib or load_library()
+        self.ctx = self.lib.apd_create(device)
+        if not self.ctx:
+            raise ApdError("apd_create failed: " + (self.lib.apd_last_error(None) or b"?").decode())
+
+    def _check(self, st: int, what: str):
+        if st != 0:
+            msg = (self.lib.apd_last_error(self.ctx) or b"").decode()
+            raise ApdError(f"{what} -> {STATUS.get(st, st)}: {msg}")
+
+    def set_problem(self, arrays: ProblemArrays):
+        pb = arrays.build()
+        self._arrays = arrays
+        self._check(self.lib.apd_set_problem(self.ctx, C.byref(pb)), "apd_set_problem")
+
+    def run(self):
+        self._check(self.lib.apd_run_patchmatch(self.ctx), "apd_run_patchmatch")
+
+    def prepare(self):
+        self._check(self.lib.apd_stage_prepare(self.ctx), "apd_stage_prepare")
+
+    def iteration(self, i: int):
+        self._check(self.lib.apd_stage_iteration(self.ctx, i), "apd_stage_iteration")
+
+    def finish(self):
+        self._check(self.lib.apd_stage_finish(self.ctx), "apd_stage_finish")
+
+    def synchronize(self):
+        self._check(self.lib.apd_synchronize(self.ctx), "apd_synchronize")
+
+    def results(self, out: Outputs):
+        s = out.struct()
+        self._check(self.lib.apd_get_results(self.ctx, C.byref(s)), "apd_get_results")
+        return out
+
+    def timing(self) -> ApdTiming:
+        t = ApdTiming()
+        self._check(self.lib.apd_get_timing(self.ctx, C.byref(t)), "apd_get_timing")
+        return t
+
+    def profile_reset(self, enable: bool = True):
+        self._check(self.lib.apd_profile_reset(self.ctx, int(enable)), "apd_profile_reset")
+
+    def profile_query(self):
+        ms, n, px = C.c_double(), C.c_int64(), C.c_int64()
+        self._check(self.lib.apd_profile_query(self.ctx, C.byref(ms), C.byref(n), C.byref(px)), "apd_profile_query")
+        return ms.value, n.value, px.value
+
+    def close(self):
+        if self.ctx:
+            self.lib.apd_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def scene_problem(scene, ref: int = 0, srcs: Optional[Sequence[int]] = None, params: Optional[ApdParams] = None,
+                  seed: int = 0x5EED, **kw) -> ProblemArrays:
+    """ProblemArrays for one reference view of a synth.Scene (full resolution, FIRST_INIT defaults)."""
+    from importlib import import_module
+    synth = import_module("synth")
+    if srcs is None:
+        srcs = [j for j, _ in scene.pairs[ref]]
+    ids = [ref] + list(srcs)
+    cams = [synth.camera_struct_values(scene.cameras[i], scene.width, scene.height) for i in ids]
+    c0 = scene.cameras[ref]
+    if params is None:
+        params = default_params(len(ids), float(np.float32(c0.depth_min) * np.float32(0.6)),
+                                float(np.float32(c0.depth_max) * np.float32(1.2)))
+    return ProblemArrays(scene.width, scene.height, [scene.images[i] for i in ids], cams, params, seed=seed, **kw)

@@ -1,0 +1,522 @@
+// apd_device.h — device building blocks of the MI355X PatchMatch engine (gfx950, wave64).
+//
+// Numerics contract (shared bit-for-bit with the CPU oracle, which restates it independently):
+//   * compiled with -ffp-contract=off; the only fused multiply-adds are explicit fmaf() calls;
+//   * IEEE division and sqrt (hipcc default -fhip-fp32-correctly-rounded-divide-sqrt);
+//   * exp/sin/cos are the deterministic polynomials below, not the device libm;
+//   * bilinear sampling is done in software on a "quad" layout (see sample_quad), with CUDA texture
+//     semantics restated: 1/256 fixed-point coordinate, clamp-to-edge (APD.cpp:691-706).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define APD_COST_MAX 2.0f
+#define APD_WEAK 0
+#define APD_STRONG 1
+#define APD_UNKNOWN 2
+#define APD_FLT_EPSILON 1.19209290e-07f
+#define APD_FLT_MAX 3.40282347e+38f
+
+namespace apd {
+
+// launch ordinals of the RNG contract (identical to the oracle)
+constexpr uint32_t ORD_ANCHORS = 1u;
+constexpr uint32_t ORD_INIT = 2u;
+__host__ __device__ constexpr uint32_t ord_strong(int i) { return 16u + 3u * (uint32_t)i; }
+__host__ __device__ constexpr uint32_t ord_fit(int i) { return 17u + 3u * (uint32_t)i; }
+__host__ __device__ constexpr uint32_t ord_weak(int i) { return 18u + 3u * (uint32_t)i; }
+constexpr uint32_t RNG_TAG = 0x41504421u;
+
+struct Cam {  // the float part of apd_camera / Camera (main.h:50-61)
+    float K[9], R[9], t[3], c[3];
+};
+
+struct SrcView {  // H = A - b (n^T Kr^-1)/w   (APD.cu:334-394, regrouped)
+    float A[9];
+    float b[3];
+};
+
+// Kernel arguments: scalars + device pointers. Passed by value (well under the kernarg limit).
+struct Args {
+    int W, H, HW, N, row_limit, state;
+    float dmin, dmax, gf, ransac_thr;
+    int geom, impetus, use_apd, peak_radius, rotate_time, sa_any, top_k;
+    uint32_t seed_lo, seed_hi;
+    float ikx, iky, cxk, cyk;              // Kr^-1 pieces: 1/fx, 1/fy, cx/fx, cy/fy
+    float anc_cos, anc_sin, anc_thr;       // GenAnchors per-launch constants (APD.cu:1897-1901)
+    int anc_shift;
+    size_t qstride;                        // float4 elements per source quad image ((W+1)*(H+1))
+    const float *__restrict__ ref;         // reference image, H*W
+    const float4 *__restrict__ quad;       // source images 1..N in quad layout, view v at (v-1)*qstride
+    const float *__restrict__ depth;       // [N+1][H*W] depth maps (geom / APD)
+    const SrcView *__restrict__ views;     // [N+1]
+    const Cam *__restrict__ cams;          // [N+1]
+    float4 *plane;
+    float *cost;
+    uint32_t *sel;
+    uint8_t *vw;                           // view-major [N][H*W]
+    uint8_t *weak;
+    uint8_t *conf;
+    const uint8_t *sa;
+    const int *amap;
+    short2 *anchors;                       // weak_count*9
+    uint8_t *reliable;
+    short2 *nearest;
+    float4 *fit;
+    float *curve;                          // optional H*W*61
+    const short2 *near_offsets;            // 201*201 offsets sorted by (d^2, x, y)
+};
+
+// ---------------------------------------------------------------------------------------------
+// deterministic math
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float d_expf(float x) {
+    if (x != x) return x;
+    if (x > 88.7228394f) return __int_as_float(0x7f800000);
+    if (x < -103.972084f) return 0.0f;
+    float kf = floorf(fmaf(x, 1.44269502f, 0.5f));
+    int k = (int)kf;
+    float r = fmaf(kf, -0.693145752f, x);
+    r = fmaf(kf, -1.42860677e-06f, r);
+    float p = 1.98412698e-04f;
+    p = fmaf(p, r, 1.38888889e-03f);
+    p = fmaf(p, r, 8.33333333e-03f);
+    p = fmaf(p, r, 4.16666667e-02f);
+    p = fmaf(p, r, 1.66666667e-01f);
+    p = fmaf(p, r, 0.5f);
+    p = fmaf(p, r, 1.0f);
+    p = fmaf(p, r, 1.0f);
+    int k1 = k / 2, k2 = k - k1;
+    p *= __int_as_float((k1 + 127) << 23);
+    p *= __int_as_float((k2 + 127) << 23);
+    return p;
+}
+__device__ __forceinline__ float d_sinf(float x) {
+    float s2 = x * x;
+    float p = -2.50521084e-08f;
+    p = fmaf(p, s2, 2.75573192e-06f);
+    p = fmaf(p, s2, -1.98412698e-04f);
+    p = fmaf(p, s2, 8.33333333e-03f);
+    p = fmaf(p, s2, -1.66666667e-01f);
+    return fmaf(x * s2, p, x);
+}
+__device__ __forceinline__ float d_cosf(float x) {
+    float s2 = x * x;
+    float p = 2.08767570e-09f;
+    p = fmaf(p, s2, -2.75573192e-07f);
+    p = fmaf(p, s2, 2.48015873e-05f);
+    p = fmaf(p, s2, -1.38888889e-03f);
+    p = fmaf(p, s2, 4.16666667e-02f);
+    p = fmaf(p, s2, -0.5f);
+    return fmaf(s2, p, 1.0f);
+}
+
+// ---------------------------------------------------------------------------------------------
+// RNG contract: Philox4x32-10, counter (pixel, ordinal, block, TAG), key = seed
+// (replaces curand_init(clock64(), y, x) + XORWOW, APD.cu:904-917)
+// ---------------------------------------------------------------------------------------------
+struct Rng {
+    uint32_t k0, k1, c0, c1, n;
+    uint32_t b0, b1, b2, b3;
+
+    __device__ __forceinline__ Rng(uint32_t slo, uint32_t shi, uint32_t pixel, uint32_t ordinal)
+        : k0(slo), k1(shi), c0(pixel), c1(ordinal), n(0), b0(0), b1(0), b2(0), b3(0) {}
+
+    __device__ __forceinline__ void refill() {
+        uint32_t x0 = c0, x1 = c1, x2 = n >> 2, x3 = RNG_TAG;
+        uint32_t key0 = k0, key1 = k1;
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            uint32_t lo0 = 0xD2511F53u * x0, hi0 = __umulhi(0xD2511F53u, x0);
+            uint32_t lo1 = 0xCD9E8D57u * x2, hi1 = __umulhi(0xCD9E8D57u, x2);
+            uint32_t n0 = hi1 ^ x1 ^ key0, n2 = hi0 ^ x3 ^ key1;
+            x0 = n0; x1 = lo1; x2 = n2; x3 = lo0;
+            key0 += 0x9E3779B9u; key1 += 0xBB67AE85u;
+        }
+        b0 = x0; b1 = x1; b2 = x2; b3 = x3;
+    }
+    // curand()
+    __device__ __forceinline__ uint32_t u32() {
+        uint32_t j = n & 3u;
+        if (j == 0) refill();
+        n++;
+        return j == 0 ? b0 : (j == 1 ? b1 : (j == 2 ? b2 : b3));
+    }
+    // curand_uniform(): (0,1]
+    __device__ __forceinline__ float uniform() { return (float)((u32() >> 8) + 1u) * 5.96046448e-08f; }
+};
+
+// ---------------------------------------------------------------------------------------------
+// geometry (APD.cu:157-313, 405-423, 831-863) — same operation order as the oracle
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void normalize3(float4 &v) {
+    float ns = v.x * v.x + v.y * v.y + v.z * v.z;
+    float inv = 1.0f / sqrtf(ns);
+    v.x *= inv; v.y *= inv; v.z *= inv;
+}
+__device__ __forceinline__ void normalize2(float &x, float &y) {
+    float ns = x * x + y * y;
+    float inv = 1.0f / sqrtf(ns);
+    x *= inv; y *= inv;
+}
+__device__ __forceinline__ void get3d(const Cam &c, float px, float py, float depth, float X[3]) {
+    X[0] = depth * (px - c.K[2]) / c.K[0];
+    X[1] = depth * (py - c.K[5]) / c.K[4];
+    X[2] = depth;
+}
+__device__ __forceinline__ float4 view_dir(const Cam &c, int px, int py, float depth) {
+    float X[3];
+    get3d(c, (float)px, (float)py, depth, X);
+    float norm = sqrtf(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
+    return make_float4(X[0] / norm, X[1] / norm, X[2] / norm, 0.0f);
+}
+__device__ __forceinline__ float dist2origin(const Cam &c, int px, int py, float depth, float4 n) {
+    float X[3];
+    get3d(c, (float)px, (float)py, depth, X);
+    return -(n.x * X[0] + n.y * X[1] + n.z * X[2]);
+}
+__device__ __forceinline__ float depth_from_plane(const Cam &c, float4 pl, int px, int py) {
+    return -pl.w * c.K[0] /
+           (((float)px - c.K[2]) * pl.x + (c.K[0] / c.K[4]) * ((float)py - c.K[5]) * pl.y + c.K[0] * pl.z);
+}
+__device__ __forceinline__ float4 random_normal(const Cam &c, int px, int py, Rng &g, float depth) {
+    float q1 = 1.0f, q2 = 1.0f, s = 2.0f;
+    while (s >= 1.0f) {
+        q1 = 2.0f * g.uniform() - 1.0f;
+        q2 = 2.0f * g.uniform() - 1.0f;
+        s = q1 * q1 + q2 * q2;
+    }
+    float sq = sqrtf(1.0f - s);
+    float4 n = make_float4(2.0f * q1 * sq, 2.0f * q2 * sq, 1.0f - 2.0f * s, 0.0f);
+    float4 vd = view_dir(c, px, py, depth);
+    float dot = n.x * vd.x + n.y * vd.y + n.z * vd.z;
+    if (dot > 0.0f) { n.x = -n.x; n.y = -n.y; n.z = -n.z; }
+    normalize3(n);
+    return n;
+}
+__device__ __forceinline__ float4 perturbed_normal(const Cam &c, int px, int py, float4 n, Rng &g, float pert) {
+    float4 vd = view_dir(c, px, py, 1.0f);
+    float a1 = (g.uniform() - 0.5f) * pert;
+    float a2 = (g.uniform() - 0.5f) * pert;
+    float a3 = (g.uniform() - 0.5f) * pert;
+    float s1 = d_sinf(a1), s2 = d_sinf(a2), s3 = d_sinf(a3);
+    float c1 = d_cosf(a1), c2 = d_cosf(a2), c3 = d_cosf(a3);
+    float R0 = c2 * c3;
+    float R1 = c3 * s1 * s2 - c1 * s3;
+    float R2 = s1 * s3 + c1 * c3 * s2;
+    float R3 = c2 * s3;
+    float R4 = c1 * c3 + s1 * s2 * s3;
+    float R5 = c1 * s2 * s3 - c3 * s1;
+    float R6 = -s2;
+    float R7 = c2 * s1;
+    float R8 = c1 * c2;
+    float4 p = make_float4(R0 * n.x + R1 * n.y + R2 * n.z, R3 * n.x + R4 * n.y + R5 * n.z,
+                           R6 * n.x + R7 * n.y + R8 * n.z, n.w);
+    if (p.x * vd.x + p.y * vd.y + p.z * vd.z >= 0.0f) p = n;
+    normalize3(p);
+    return p;
+}
+__device__ __forceinline__ float4 to_world(const Cam &c, float4 p) {
+    return make_float4(c.R[0] * p.x + c.R[3] * p.y + c.R[6] * p.z, c.R[1] * p.x + c.R[4] * p.y + c.R[7] * p.z,
+                       c.R[2] * p.x + c.R[5] * p.y + c.R[8] * p.z, p.w);
+}
+__device__ __forceinline__ float4 to_ref(const Cam &c, float4 p) {
+    return make_float4(c.R[0] * p.x + c.R[1] * p.y + c.R[2] * p.z, c.R[3] * p.x + c.R[4] * p.y + c.R[5] * p.z,
+                       c.R[6] * p.x + c.R[7] * p.y + c.R[8] * p.z, p.w);
+}
+__device__ __forceinline__ void world_point(const Cam &c, float x, float y, float depth, float P[3]) {
+    float X0 = depth * (x - c.K[2]) / c.K[0];
+    float X1 = depth * (y - c.K[5]) / c.K[4];
+    float X2 = depth;
+    float t0 = c.R[0] * X0 + c.R[3] * X1 + c.R[6] * X2;
+    float t1 = c.R[1] * X0 + c.R[4] * X1 + c.R[7] * X2;
+    float t2 = c.R[2] * X0 + c.R[5] * X1 + c.R[8] * X2;
+    P[0] = t0 + c.c[0]; P[1] = t1 + c.c[1]; P[2] = t2 + c.c[2];
+}
+__device__ __forceinline__ void project_cam(const float P[3], const Cam &c, float &px, float &py, float &d) {
+    float t0 = c.R[0] * P[0] + c.R[1] * P[1] + c.R[2] * P[2] + c.t[0];
+    float t1 = c.R[3] * P[0] + c.R[4] * P[1] + c.R[5] * P[2] + c.t[1];
+    float t2 = c.R[6] * P[0] + c.R[7] * P[1] + c.R[8] * P[2] + c.t[2];
+    float dd = c.K[6] * t0 + c.K[7] * t1 + c.K[8] * t2;
+    px = (c.K[0] * t0 + c.K[1] * t1 + c.K[2] * t2) / dd;
+    py = (c.K[3] * t0 + c.K[4] * t1 + c.K[5] * t2) / dd;
+    d = dd;
+}
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ int trunc_clamp(float x, int n) {
+    x = fminf(fmaxf(x, -1.0f), (float)n);
+    return clampi((int)x, 0, n - 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// homography + projection
+// ---------------------------------------------------------------------------------------------
+struct Hom { float h[9]; };
+
+__device__ __forceinline__ Hom homography(const Args &a, int s, float4 pl) {
+    float m0 = pl.x * a.ikx;
+    float m1 = pl.y * a.iky;
+    float m2 = fmaf(-pl.y, a.cyk, fmaf(-pl.x, a.cxk, pl.z));
+    float iw = 1.0f / pl.w;
+    m0 *= iw; m1 *= iw; m2 *= iw;
+    const SrcView &V = a.views[s];
+    Hom H;
+    H.h[0] = fmaf(-V.b[0], m0, V.A[0]); H.h[1] = fmaf(-V.b[0], m1, V.A[1]); H.h[2] = fmaf(-V.b[0], m2, V.A[2]);
+    H.h[3] = fmaf(-V.b[1], m0, V.A[3]); H.h[4] = fmaf(-V.b[1], m1, V.A[4]); H.h[5] = fmaf(-V.b[1], m2, V.A[5]);
+    H.h[6] = fmaf(-V.b[2], m0, V.A[6]); H.h[7] = fmaf(-V.b[2], m1, V.A[7]); H.h[8] = fmaf(-V.b[2], m2, V.A[8]);
+    return H;
+}
+__device__ __forceinline__ void project(const Hom &H, float x, float y, float &ox, float &oy) {
+    float X = fmaf(H.h[1], y, fmaf(H.h[0], x, H.h[2]));
+    float Y = fmaf(H.h[4], y, fmaf(H.h[3], x, H.h[5]));
+    float Z = fmaf(H.h[7], y, fmaf(H.h[6], x, H.h[8]));
+    float iz = 1.0f / Z;
+    ox = X * iz;
+    oy = Y * iz;
+}
+
+// ---------------------------------------------------------------------------------------------
+// texture sampling
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float tex_ref(const Args &a, int x, int y) {
+    return a.ref[clampi(y, 0, a.H - 1) * a.W + clampi(x, 0, a.W - 1)];
+}
+// Quad layout: Q[(iy+1)*(W+1) + (ix+1)] = {T(ix,iy), T(ix+1,iy), T(ix,iy+1), T(ix+1,iy+1)} with
+// clamp-to-edge, for ix in [-1, W-1], iy in [-1, H-1] — one 16-byte gather per bilinear sample.
+__device__ __forceinline__ float sample_quad(const float4 *__restrict__ Q, int W, int H, float x, float y) {
+    x = fminf(fmaxf(x, -1.0f), (float)W);
+    y = fminf(fmaxf(y, -1.0f), (float)H);
+    int qx = (int)fmaf(x, 256.0f, 512.5f) - 512;
+    int qy = (int)fmaf(y, 256.0f, 512.5f) - 512;
+    int ix = min(((qx + 512) >> 8) - 2, W - 1);
+    int iy = min(((qy + 512) >> 8) - 2, H - 1);
+    float ax = (float)(qx & 255) * 0.00390625f;
+    float ay = (float)(qy & 255) * 0.00390625f;
+    float4 q = Q[(iy + 1) * (W + 1) + (ix + 1)];
+    float top = fmaf(ax, q.y - q.x, q.x);
+    float bot = fmaf(ax, q.w - q.z, q.z);
+    return fmaf(ay, bot - top, top);
+}
+
+__device__ __forceinline__ float ncc_finalize(float sr, float srr, float ss, float sss, float srs, float wsum) {
+    float inv = 1.0f / wsum;
+    sr *= inv; srr *= inv; ss *= inv; sss *= inv; srs *= inv;
+    float var_ref = fmaf(-sr, sr, srr);
+    float var_src = fmaf(-ss, ss, sss);
+    if (var_ref < 1e-5f || var_src < 1e-5f) return APD_COST_MAX;
+    float covar = fmaf(-sr, ss, srs);
+    float vrs = sqrtf(var_ref * var_src);
+    return fmaxf(0.0f, fminf(APD_COST_MAX, 1.0f - covar / vrs));
+}
+
+// Reference-side window of ComputeBilateralNCCOld (6x6, radius 5, step 2): fixed per pixel, so it is
+// gathered once per pixel and kept in VGPRs across all 14*N NCC evaluations of a sweep.
+struct RefWin {
+    float r[36];
+    float mean, var;   // sum_ref/36 and sum_ref_ref/36 - mean^2, same op order as the oracle
+};
+__device__ __forceinline__ void build_refwin(const Args &a, int px, int py, RefWin &w) {
+    float sr = 0.0f, srr = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            float r = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
+            w.r[i * 6 + j] = r;
+            sr += r;
+            srr = fmaf(r, r, srr);
+        }
+    }
+    const float inv = 1.0f / 36.0f;
+    sr *= inv;
+    srr *= inv;
+    w.mean = sr;
+    w.var = fmaf(-sr, sr, srr);
+}
+
+// SA quadrant branch of ComputeBilateralNCCOld (APD.cu:664-719); rarely taken, kept out of line.
+__device__ __noinline__ float ncc_old_sa(const Args &a, int px, int py, int s, const Hom &H, uint8_t cid) {
+    const int sign[8] = {1, 1, -1, -1, 1, -1, -1, 1};
+    const int off[18] = {1, 1, 3, 1, 1, 3, 1, 5, 3, 3, 5, 1, 5, 3, 3, 5, 5, 5};
+    const float4 *Q = a.quad + (size_t)(s - 1) * a.qstride;
+    float sr = 0.0f, srr = 0.0f, ss = 0.0f, sss = 0.0f, srs = 0.0f, wsum = 0.0f;
+    for (int q = 0; q < 4; ++q) {
+        for (int j = 0; j < 9; ++j) {
+            int rx = px + off[2 * j] * sign[2 * q];
+            int ry = py + off[2 * j + 1] * sign[2 * q + 1];
+            if (rx < 0 || rx >= a.W || ry < 0 || ry >= a.H) continue;
+            if (a.sa[ry * a.W + rx] != cid) break;
+            float r = tex_ref(a, rx, ry);
+            float sx, sy;
+            project(H, (float)rx, (float)ry, sx, sy);
+            float v = sample_quad(Q, a.W, a.H, sx, sy);
+            sr += r; srr = fmaf(r, r, srr);
+            ss += v; sss = fmaf(v, v, sss);
+            srs = fmaf(r, v, srs);
+            wsum += 1.0f;
+        }
+    }
+    return ncc_finalize(sr, srr, ss, sss, srs, wsum);
+}
+
+// ComputeBilateralNCCOld (APD.cu:596-721) for source view s (1..N), plane in the ref frame.
+__device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, float4 pl, const RefWin &rw) {
+    const int W = a.W, H = a.H;
+    Hom Hm = homography(a, s, pl);
+    float ptx, pty;
+    project(Hm, (float)px, (float)py, ptx, pty);
+    if (ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f) return APD_COST_MAX;
+    if (a.sa_any) {
+        int pidx = clampi((int)fmaf(pty, (float)W, ptx), 0, a.HW - 1);
+        if (a.sa[pidx] != 0) return ncc_old_sa(a, px, py, s, Hm, a.sa[py * W + px]);
+    }
+    const float4 *__restrict__ Q = a.quad + (size_t)(s - 1) * a.qstride;
+    float ss = 0.0f, sss = 0.0f, srs = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const float x = (float)(px - 5 + 2 * i);
+        const float cx = fmaf(Hm.h[0], x, Hm.h[2]);
+        const float cy = fmaf(Hm.h[3], x, Hm.h[5]);
+        const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const float y = (float)(py - 5 + 2 * j);
+            float X = fmaf(Hm.h[1], y, cx);
+            float Y = fmaf(Hm.h[4], y, cy);
+            float Z = fmaf(Hm.h[7], y, cz);
+            float iz = 1.0f / Z;
+            float v = sample_quad(Q, W, H, X * iz, Y * iz);
+            float r = rw.r[i * 6 + j];
+            ss += v;
+            sss = fmaf(v, v, sss);
+            srs = fmaf(r, v, srs);
+        }
+    }
+    const float inv = 1.0f / 36.0f;
+    ss *= inv; sss *= inv; srs *= inv;
+    float var_src = fmaf(-ss, ss, sss);
+    if (rw.var < 1e-5f || var_src < 1e-5f) return APD_COST_MAX;
+    float covar = fmaf(-rw.mean, ss, srs);
+    float vrs = sqrtf(rw.var * var_src);
+    return fmaxf(0.0f, fminf(APD_COST_MAX, 1.0f - covar / vrs));
+}
+
+// sa label at a possibly out-of-image linear index (same rule as the oracle's sa_at)
+__device__ __forceinline__ int sa_at(const Args &a, int x, int y) {
+    long idx = (long)y * a.W + x;
+    if (idx < 0 || idx >= a.HW) return -1;
+    return a.sa[idx];
+}
+
+// ComputeBilateralNCCNew + Softmax focal weighting (APD.cu:448-593, 431-446)
+__device__ __noinline__ float ncc_new(const Args &a, int px, int py, int s, float4 pl) {
+    const int W = a.W, H = a.H;
+    const int center = px + py * W;
+    const int cid = a.sa_any ? a.sa[center] : 0;
+    const bool use_sa = cid != 0;
+    Hom Hm = homography(a, s, pl);
+    float ptx, pty;
+    project(Hm, (float)px, (float)py, ptx, pty);
+    if (ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f) return APD_COST_MAX;
+    if (a.weak[center] != APD_WEAK) return 0.0f;
+    const float4 *__restrict__ Q = a.quad + (size_t)(s - 1) * a.qstride;
+    const short2 *anc = a.anchors + (size_t)a.amap[center] * 9;
+    float sc[9];
+    int ns = 0;
+    float center_cost = 0.0f, strong_weight = 0.0f;
+    for (int k = 0; k < 9; ++k) {
+        short2 ap = anc[k];
+        int ax = ap.x, ay = ap.y;
+        if (ax == -1 || ay == -1) continue;
+        if (use_sa && sa_at(a, ax, ay) != cid) continue;
+        float asx, asy;
+        project(Hm, (float)ax, (float)ay, asx, asy);
+        if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) {
+            if (k != 0) {
+                if ((a.sel[ax + ay * W] >> (s - 1)) & 1u) {
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) if (t == ns) sc[t] = APD_COST_MAX;
+                    ns++;
+                    strong_weight += 1.0f;
+                }
+                continue;
+            }
+            return APD_COST_MAX;
+        }
+        const int inc = (k == 0) ? 2 : 5;
+        float sr = 0.0f, srr = 0.0f, ss = 0.0f, sss = 0.0f, srs = 0.0f, wsum = 0.0f;
+        for (int i = -5; i <= 5; i += inc) {
+            const float x = (float)(ax + i);
+            const float cx = fmaf(Hm.h[0], x, Hm.h[2]);
+            const float cy = fmaf(Hm.h[3], x, Hm.h[5]);
+            const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
+            for (int j = -5; j <= 5; j += inc) {
+                int rx = ax + i, ry = ay + j;
+                if (use_sa && sa_at(a, rx, ry) != cid) continue;
+                float r = tex_ref(a, rx, ry);
+                const float y = (float)ry;
+                float X = fmaf(Hm.h[1], y, cx);
+                float Y = fmaf(Hm.h[4], y, cy);
+                float Z = fmaf(Hm.h[7], y, cz);
+                float iz = 1.0f / Z;
+                float v = sample_quad(Q, W, H, X * iz, Y * iz);
+                sr += r; srr = fmaf(r, r, srr);
+                ss += v; sss = fmaf(v, v, sss);
+                srs = fmaf(r, v, srs);
+                wsum += 1.0f;
+            }
+        }
+        if (wsum == 0.0f) continue;
+        float c = ncc_finalize(sr, srr, ss, sss, srs, wsum);
+        if (k == 0) {
+            center_cost = c;
+        } else {
+#pragma unroll
+            for (int t = 0; t < 9; ++t) if (t == ns) sc[t] = c;
+            ns++;
+            strong_weight += 1.0f;
+        }
+    }
+    if (strong_weight <= 1e-6f) return center_cost;
+    // Softmax over the anchor costs, then the focal-weighted mean (APD.cu:576-586)
+    float mx = -1e10f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) if (t < ns && sc[t] > mx) mx = sc[t];
+    float e[9];
+    float sum = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        if (t < ns) { e[t] = d_expf(sc[t] - mx); sum += e[t]; }
+    }
+    float acc = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        if (t < ns) { float w = e[t] / sum; acc = fmaf(w, sc[t], acc); }
+    }
+    acc = (acc > APD_COST_MAX) ? APD_COST_MAX : acc;
+    return (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
+}
+
+// ComputeGeomConsistencyCost (APD.cu:865-902)
+__device__ __forceinline__ float geom_cost(const Args &a, int px, int py, int s, float4 pl) {
+    const Cam &rc = a.cams[0];
+    const Cam &sc = a.cams[s];
+    float depth = depth_from_plane(rc, pl, px, py);
+    float P[3];
+    world_point(rc, (float)px, (float)py, depth, P);
+    float sx, sy, sd;
+    project_cam(P, sc, sx, sy, sd);
+    float src_depth = a.depth[(size_t)s * a.HW + trunc_clamp(sy, a.H) * a.W + trunc_clamp(sx, a.W)];
+    if (src_depth == 0.0f) return 3.0f;
+    float Q[3];
+    world_point(sc, sx, sy, src_depth, Q);
+    float bx, by, rd;
+    project_cam(Q, rc, bx, by, rd);
+    float dx = (float)px - bx, dy = (float)py - by;
+    float e = sqrtf(dx * dx + dy * dy);
+    return fminf(3.0f, e);
+}
+
+}  // namespace apd

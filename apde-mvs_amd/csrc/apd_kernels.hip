@@ -1,0 +1,1748 @@
+// apd_kernels.hip — MI355X (gfx950) PatchMatch depth kernels and the C-ABI of libapd_hip.so.
+//
+// Work decomposition:
+//   * "view-group" kernels (RandomInitialization, the Strong/Weak checkerboard sweeps, DepthToWeak,
+//     LocalRefine): one 64-lane wavefront holds floor(64/N) pixels x N source views; lane = (pixel,
+//     source view). Each lane evaluates the NCC of ITS view for every plane hypothesis of its pixel,
+//     so the per-thread cost matrix of the reference (cost_array[8][32], APD.cu:1120, ~1 KB of
+//     scratch) becomes 8 VGPRs, and the cross-view steps (view sampling CDF, weighted cost sums)
+//     become in-order __shfl reductions over the N lanes of the pixel (bit-identical to the
+//     reference's sequential sums).
+//   * pixel kernels (anchors, RANSAC fit, filter, confidence, ...): one lane per pixel.
+//   * checkerboard colours and the WEAK / non-WEAK split are compacted into pixel lists on device, so
+//     no wavefront is spent on pixels another kernel owns.
+// All launches go to the ctx stream; there is no host synchronisation inside the sweep loop.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/apd_hip.h"
+#include "apd_device.h"
+
+using namespace apd;
+
+#define WAVE 64
+#define BLOCK 256
+
+// ---------------------------------------------------------------------------------------------
+// view-group lane mapping
+// ---------------------------------------------------------------------------------------------
+struct Group {
+    int v;        // source view index 0..N-1 of this lane (src image v+1)
+    int base;     // first lane of this pixel's group
+    int slot;     // pixel slot within the wave
+    bool valid;   // lane owns a real pixel (writes allowed)
+    int li;       // list index
+    unsigned long long gmask;
+};
+
+__device__ __forceinline__ Group make_group(int N, int count, int wave) {
+    Group G;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int P = WAVE / N;
+    int g = lane / N;
+    const bool lane_ok = g < P;
+    int v = lane - g * N;
+    if (!lane_ok) { g = 0; v = (lane - P * N) % N; }  // spare lanes mirror group 0, never write
+    G.v = v;
+    G.base = g * N;
+    G.slot = g;
+    G.li = wave * P + g;
+    G.valid = lane_ok && G.li < count;
+    if (G.li >= count) G.li = count - 1;
+    G.gmask = (N >= 64) ? ~0ull : ((1ull << N) - 1ull);
+    return G;
+}
+__device__ __forceinline__ uint32_t group_bits(bool pred, const Group &G) {
+    unsigned long long m = __ballot(pred);
+    return (uint32_t)((m >> G.base) & G.gmask);
+}
+
+// ---------------------------------------------------------------------------------------------
+// setup kernels
+// ---------------------------------------------------------------------------------------------
+// Source images -> quad gather layout (one float4 = the 2x2 bilinear footprint, clamp-to-edge).
+__global__ __launch_bounds__(BLOCK) void k_build_quads(const float *__restrict__ imgs, float4 *__restrict__ quad,
+                                                     int W, int H, int N, size_t qstride) {
+    const size_t per = (size_t)(W + 1) * (H + 1);
+    const size_t total = per * N;
+    for (size_t i = blockIdx.x * (size_t)BLOCK + threadIdx.x; i < total; i += (size_t)gridDim.x * BLOCK) {
+        const int v = (int)(i / per);
+        const size_t r = i - (size_t)v * per;
+        const int iy = (int)(r / (W + 1)) - 1;
+        const int ix = (int)(r % (W + 1)) - 1;
+        const float *T = imgs + (size_t)(v + 1) * W * H;
+        const int x0 = clampi(ix, 0, W - 1), x1 = clampi(ix + 1, 0, W - 1);
+        const int y0 = clampi(iy, 0, H - 1), y1 = clampi(iy + 1, 0, H - 1);
+        quad[(size_t)v * qstride + r] =
+            make_float4(T[y0 * W + x0], T[y0 * W + x1], T[y1 * W + x0], T[y1 * W + x1]);
+    }
+}
+
+// Ordered compaction, one workgroup per image row.
+//   mode 0: colour `colour`, weak != WEAK, y < row_limit   (Strong sweep / filter pixel set)
+//   mode 1: colour `colour`, weak == WEAK, y < row_limit   (Weak sweep pixel set)
+//   mode 2: every pixel with weak == WEAK -> anchors_map (running row-major index, APD.cpp:627-640)
+__device__ __forceinline__ bool list_pred(const Args &a, int mode, int colour, int x, int y) {
+    const uint8_t w = a.weak[y * a.W + x];
+    if (mode == 2) return w == APD_WEAK;
+    if (y >= a.row_limit || ((x + y) & 1) != colour) return false;
+    return mode == 0 ? (w != APD_WEAK) : (w == APD_WEAK);
+}
+__global__ __launch_bounds__(BLOCK) void k_list_count(Args a, int mode, int colour, int *__restrict__ row_counts) {
+    const int y = blockIdx.x;
+    __shared__ int wsum[BLOCK / WAVE];
+    int cnt = 0;
+    for (int x = threadIdx.x; x < a.W; x += BLOCK) cnt += list_pred(a, mode, colour, x, y) ? 1 : 0;
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) row_counts[y] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+__global__ __launch_bounds__(1024) void k_list_scan(const int *__restrict__ row_counts, int H, int *__restrict__ row_off,
+                                                  int *__restrict__ total) {
+    __shared__ int part[1024];
+    const int per = (H + 1023) / 1024;
+    const int r0 = threadIdx.x * per;
+    int s = 0;
+    for (int r = r0; r < min(r0 + per, H); ++r) s += row_counts[r];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        int t = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += t;
+        __syncthreads();
+    }
+    int off = part[threadIdx.x] - s;
+    for (int r = r0; r < min(r0 + per, H); ++r) { row_off[r] = off; off += row_counts[r]; }
+    if (threadIdx.x == 1023) *total = part[1023];
+}
+__global__ __launch_bounds__(BLOCK) void k_list_fill(Args a, int mode, int colour, const int *__restrict__ row_off,
+                                                   int *__restrict__ out) {
+    const int y = blockIdx.x;
+    __shared__ int wcnt[BLOCK / WAVE];
+    int off = row_off[y];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int x0 = 0; x0 < a.W; x0 += BLOCK) {
+        const int x = x0 + threadIdx.x;
+        const bool p = x < a.W && list_pred(a, mode, colour, x, y);
+        const unsigned long long m = __ballot(p);
+        const int pre = __popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) wcnt[wv] = __popcll(m);
+        __syncthreads();
+        int wo = 0;
+        for (int k = 0; k < wv; ++k) wo += wcnt[k];
+        const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        if (mode == 2) {
+            if (x < a.W) out[y * a.W + x] = p ? off + wo + pre : -1;
+        } else if (p) {
+            out[off + wo + pre] = y * a.W + x;
+        }
+        off += tot;
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// APD anchor kernels (pixel kernels)
+// ---------------------------------------------------------------------------------------------
+// FindNearestStrongPoint (APD.cu:2434-2484). Same result as the reference's 201x201 scan (min
+// distance, then max confidence, then first in x-major scan order) but visits the window in rings
+// of increasing distance (offsets pre-sorted by (d^2, x, y)) and stops after the first ring that
+// holds a candidate.
+__global__ __launch_bounds__(BLOCK) void k_find_nearest(Args a, int n_off) {
+    const int c = blockIdx.x * BLOCK + threadIdx.x;
+    if (c >= a.HW) return;
+    const int py = c / a.W, px = c - py * a.W;
+    const uint8_t w = a.weak[c];
+    short2 out = make_short2(-1, -1);
+    if (w == APD_WEAK || w == APD_UNKNOWN) {
+        const uint8_t cc = a.conf[c];
+        int best_d2 = -1, bc = -1;
+        for (int k = 0; k < n_off; ++k) {
+            const short2 o = a.near_offsets[k];
+            const int d2 = o.x * o.x + o.y * o.y;
+            if (best_d2 >= 0 && d2 > best_d2) break;
+            const int tx = px + o.x, ty = py + o.y;
+            if (tx < 0 || tx >= a.W || ty < 0 || ty >= a.H) continue;
+            const int t = tx + ty * a.W;
+            if (a.weak[t] != APD_STRONG) continue;
+            const int tc = a.conf[t];
+            if (tc < cc) continue;
+            if (best_d2 < 0 || tc > bc) { best_d2 = d2; bc = tc; out = make_short2((short)tx, (short)ty); }
+        }
+    } else if (w == APD_STRONG) {
+        out = make_short2((short)px, (short)py);
+    }
+    a.nearest[c] = out;
+}
+
+// PointinTriangle (APD.cu:122-143)
+__device__ __forceinline__ bool point_in_triangle(int ax, int ay, int bx, int by, int cx, int cy, int px, int py) {
+    float ABx = (float)(bx - ax), ABy = (float)(by - ay);
+    float BCx = (float)(cx - bx), BCy = (float)(cy - by);
+    float CAx = (float)(ax - cx), CAy = (float)(ay - cy);
+    float AB = sqrtf(ABx * ABx + ABy * ABy), BC = sqrtf(BCx * BCx + BCy * BCy), CA = sqrtf(CAx * CAx + CAy * CAy);
+    if (AB <= 2 || BC <= 2 || CA <= 2) return false;
+    if (!(AB + BC > CA && BC + CA > AB && AB + CA > BC)) return false;
+    float PAx = (float)(ax - px), PAy = (float)(ay - py);
+    float PBx = (float)(bx - px), PBy = (float)(by - py);
+    float PCx = (float)(cx - px), PCy = (float)(cy - py);
+    float t1 = PAx * PBy - PAy * PBx;
+    float t2 = PBx * PCy - PBy * PCx;
+    float t3 = PCx * PAy - PCy * PAx;
+    return t1 * t2 >= 0 && t1 * t3 >= 0;
+}
+
+// GenAnchors (APD.cu:1857-2082): directional search for strong anchors + RANSAC plane.
+__global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
+    const int c = blockIdx.x * BLOCK + threadIdx.x;
+    if (c >= a.HW) return;
+    if (a.weak[c] != APD_WEAK) return;
+    const int W = a.W, H = a.H;
+    const int py = c / W, px = c - py * W;
+    const int margin = 6;
+    const float depth_diff = a.dmax - a.dmin;
+    const Cam &cam = a.cams[0];
+    short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
+    Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_ANCHORS);
+    for (int i = 0; i < 9; ++i) anc[i] = make_short2(-1, -1);
+    anc[0] = make_short2((short)px, (short)py);
+    short2 sp[32];
+    uint32_t dvalid = 0;
+    for (int i = 0; i < 32; ++i) sp[i] = make_short2(-1, -1);
+    int odi = -1, nsp = 0;
+    const int rt = a.rotate_time;
+    const unsigned shift = (unsigned)a.anc_shift;
+    for (int odx = -1; odx <= 1; ++odx) {
+        for (int ody = -1; ody <= 1; ++ody) {
+            if (odx == 0 && ody == 0) continue;
+            float dx = (float)odx, dy = (float)ody;
+            normalize2(dx, dy);
+            odi++;
+            for (int ri = 0; ri < rt; ++ri) {
+                const int di = odi * 4 + ri;
+                for (int radius = 2; radius <= APD_MAX_SEARCH_RADIUS; radius = min(radius * 2, radius + 25)) {
+                    float tx = (float)px + dx * (float)radius, ty = (float)py + dy * (float)radius;
+                    if (tx < 0 || ty < 0 || tx >= (float)W || ty >= (float)H) break;
+                    for (int t = 0; t < 4; ++t) {
+                        uint32_t sx = g.u32();
+                        uint32_t mx = g.u32();
+                        int rxs = (int)(((sx % 2u == 0) ? mx : (0u - mx)) % shift);
+                        uint32_t sy = g.u32();
+                        uint32_t my = g.u32();
+                        int rys = (int)(((sy % 2u == 0) ? my : (0u - my)) % shift);
+                        float ddx = dx * 20 + (float)rxs, ddy = dy * 20 + (float)rys;
+                        normalize2(ddx, ddy);
+                        int ax = (int16_t)(int)((float)px + ddx * (float)radius);
+                        int ay = (int16_t)(int)((float)py + ddy * (float)radius);
+                        if (ax < margin || ay < margin || ax >= W - margin || ay >= H - margin) continue;
+                        short2 nn = a.nearest[ax + ay * W];
+                        if (nn.x == -1 || nn.y == -1) continue;
+                        float tdx = (float)(nn.x - px), tdy = (float)(nn.y - py);
+                        normalize2(tdx, tdy);
+                        float ca = tdx * dx + tdy * dy;
+                        if (ca > a.anc_thr) { sp[di] = nn; dvalid |= 1u << di; nsp++; break; }
+                    }
+                    if ((dvalid >> di) & 1u) break;
+                }
+                float rx = dx * a.anc_cos - dy * a.anc_sin;
+                float ry = dx * a.anc_sin + dy * a.anc_cos;
+                normalize2(rx, ry);
+                dx = rx; dy = ry;
+            }
+        }
+    }
+    if (nsp <= 3) { a.reliable[c] = 0; return; }
+    short2 vp[32];
+    float v3[32][3];
+    int vc = 0;
+    float X[3];
+    get3d(cam, (float)px, (float)py, a.plane[c].w, X);
+    const float cw0 = X[0], cw1 = X[1], cw2 = X[2];
+    for (int i = 0; i < 32; ++i) {
+        vp[i] = make_short2(-1, -1);
+        if ((dvalid >> i) & 1u) {
+            vp[vc] = sp[i];
+            get3d(cam, (float)sp[i].x, (float)sp[i].y, a.plane[sp[i].x + sp[i].y * W].w, X);
+            v3[vc][0] = X[0]; v3[vc][1] = X[1]; v3[vc][2] = X[2];
+            vc++;
+        }
+    }
+    float4 best = make_float4(0, 0, 0, 0);
+    int ua = -1, ub = -1, uc = -1;
+    bool has = false;
+    float min_cost = APD_FLT_MAX;
+    int max_count = 3;
+    for (int it = 0; it < 50; ++it) {
+        int ia = (int)(g.u32() % (uint32_t)vc);
+        int ib = (int)(g.u32() % (uint32_t)vc);
+        int ic = (int)(g.u32() % (uint32_t)vc);
+        if (ia == ib || ib == ic || ia == ic) continue;
+        if (!point_in_triangle(vp[ia].x, vp[ia].y, vp[ib].x, vp[ib].y, vp[ic].x, vp[ic].y, px, py)) continue;
+        const float *A = v3[ia], *B = v3[ib], *C = v3[ic];
+        float ACx = A[0] - C[0], ACy = A[1] - C[1], ACz = A[2] - C[2];
+        float BCx = B[0] - C[0], BCy = B[1] - C[1], BCz = B[2] - C[2];
+        float4 cr = make_float4(ACy * BCz - BCy * ACz, -(ACx * BCz - BCx * ACz), ACx * BCy - BCx * ACy, 0.0f);
+        if ((cr.x == 0 && cr.y == 0 && cr.z == 0) || isnan(cr.x) || isnan(cr.y) || isnan(cr.z)) continue;
+        normalize3(cr);
+        cr.w = -(cr.x * A[0] + cr.y * A[1] + cr.z * A[2]);
+        int tcnt = 0;
+        for (int k = 0; k < vc; ++k) {
+            float d = fabsf(cr.x * v3[k][0] + cr.y * v3[k][1] + cr.z * v3[k][2] + cr.w);
+            if (d / depth_diff < a.ransac_thr) tcnt++;
+        }
+        if (tcnt < 6) continue;
+        if (tcnt > max_count) {
+            max_count = tcnt;
+            min_cost = fabsf(cr.x * cw0 + cr.y * cw1 + cr.z * cw2 + cr.w);
+            best = cr; has = true; ua = ia; ub = ib; uc = ic;
+        } else if (tcnt == max_count) {
+            float cd = fabsf(cr.x * cw0 + cr.y * cw1 + cr.z * cw2 + cr.w);
+            if (cd < min_cost) { min_cost = cd; best = cr; ua = ia; ub = ib; uc = ic; }
+        }
+    }
+    if (!has) { a.reliable[c] = 0; return; }
+    float wgt[32];
+    for (int i = 0; i < vc; ++i) {
+        float d = fabsf(best.x * v3[i][0] + best.y * v3[i][1] + best.z * v3[i][2] + best.w);
+        if (d / depth_diff >= a.ransac_thr) { vp[i] = make_short2(-1, -1); wgt[i] = APD_FLT_MAX; continue; }
+        if (i == ua || i == ub || i == uc) d -= 1;
+        wgt[i] = d;
+    }
+    for (int i = 1; i < vc; ++i) {  // sort_small_weighted, APD.cu:25-38
+        short2 tp = vp[i];
+        float tw = wgt[i];
+        int j;
+        for (j = i; j >= 1 && tw < wgt[j - 1]; j--) { vp[j] = vp[j - 1]; wgt[j] = wgt[j - 1]; }
+        vp[j] = tp; wgt[j] = tw;
+    }
+    for (int i = 1; i < 9; ++i) anc[i] = vp[i - 1];
+    a.reliable[c] = 1;
+}
+
+// NeigbourUpdate (APD.cu:2084-2100)
+__global__ __launch_bounds__(BLOCK) void k_neighbour_update(Args a) {
+    const int c = blockIdx.x * BLOCK + threadIdx.x;
+    if (c >= a.HW) return;
+    if (a.weak[c] == APD_WEAK && a.reliable[c] != 1) a.weak[c] = APD_UNKNOWN;
+}
+
+// RANSACToGetFitPlane (APD.cu:2486-2598)
+__global__ __launch_bounds__(BLOCK) void k_ransac_fit(Args a, int iter) {
+    const int c = blockIdx.x * BLOCK + threadIdx.x;
+    if (c >= a.HW) return;
+    if (a.weak[c] != APD_WEAK) { a.fit[c] = a.plane[c]; return; }
+    const int W = a.W;
+    const int py = c / W, px = c - py * W;
+    const Cam &cam = a.cams[0];
+    const short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
+    int sx[8], sy[8], cnt = 0;
+    float s3[8][3], X[3];
+    for (int i = 1; i < 9; ++i) {
+        short2 t = anc[i];
+        if (t.x == -1 || t.y == -1) continue;
+        sx[cnt] = t.x; sy[cnt] = t.y;
+        float d = depth_from_plane(cam, a.plane[t.x + t.y * W], t.x, t.y);
+        get3d(cam, (float)t.x, (float)t.y, d, X);
+        s3[cnt][0] = X[0]; s3[cnt][1] = X[1]; s3[cnt][2] = X[2];
+        cnt++;
+    }
+    if (cnt < 3) { a.fit[c] = a.plane[c]; return; }
+    Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ord_fit(iter));
+    float min_cost = APD_FLT_MAX;
+    float4 best = make_float4(0, 0, 0, 0);
+    bool has = false;
+    for (int it = 0; it < 50; ++it) {
+        int ia = (int)(g.u32() % (uint32_t)cnt);
+        int ib = (int)(g.u32() % (uint32_t)cnt);
+        int ic = (int)(g.u32() % (uint32_t)cnt);
+        if (ia == ib || ib == ic || ia == ic) continue;
+        if (!point_in_triangle(sx[ia], sy[ia], sx[ib], sy[ib], sx[ic], sy[ic], px, py)) continue;
+        const float *A = s3[ia], *B = s3[ib], *C = s3[ic];
+        float ACx = A[0] - C[0], ACy = A[1] - C[1], ACz = A[2] - C[2];
+        float BCx = B[0] - C[0], BCy = B[1] - C[1], BCz = B[2] - C[2];
+        float4 cr = make_float4(ACy * BCz - BCy * ACz, -(ACx * BCz - BCx * ACz), ACx * BCy - BCx * ACy, 0.0f);
+        if ((cr.x == 0 && cr.y == 0 && cr.z == 0) || isnan(cr.x) || isnan(cr.y) || isnan(cr.z)) continue;
+        normalize3(cr);
+        cr.w = -(cr.x * A[0] + cr.y * A[1] + cr.z * A[2]);
+        float tc = 0.0f;
+        for (int k = 0; k < cnt; ++k) {
+            if (k == ia || k == ib || k == ic) continue;
+            tc += fabsf(cr.x * s3[k][0] + cr.y * s3[k][1] + cr.z * s3[k][2] + cr.w);
+        }
+        if (tc < min_cost) { min_cost = tc; best = cr; has = true; }
+        if (min_cost == 0) break;
+    }
+    if (has) {
+        float d = depth_from_plane(cam, a.plane[c], px, py);
+        float4 vd = view_dir(cam, px, py, d);
+        float dot = best.x * vd.x + best.y * vd.y + best.z * vd.z;
+        if (dot > 0) { best.x = -best.x; best.y = -best.y; best.z = -best.z; best.w = -best.w; }
+        a.fit[c] = best;
+    } else {
+        a.fit[c] = make_float4(0, 0, 0, 0);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// RandomInitialization (APD.cu:919-948) + ComputeMultiViewInitialCostandSelectedViews (723-774)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_random_init(Args a) {
+    const int N = a.N;
+    const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
+    const int P = WAVE / N;
+    if (wave * P >= a.HW) return;
+    const Group G = make_group(N, a.HW, wave);
+    const int c = G.li;
+    const int py = c / a.W, px = c - py * a.W;
+    const Cam &cam = a.cams[0];
+    float4 pl;
+    if (a.state == APD_FIRST_INIT) {
+        Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_INIT);
+        float depth = g.uniform() * (a.dmax - a.dmin) + a.dmin;
+        pl = random_normal(cam, px, py, g, depth);
+        pl.w = dist2origin(cam, px, py, depth, pl);
+    } else {
+        pl = to_ref(cam, a.plane[c]);
+        float depth = pl.w;
+        pl.w = dist2origin(cam, px, py, depth, pl);
+    }
+    const bool use_new = a.use_apd && a.weak[c] == APD_WEAK;
+    const int s = G.v + 1;
+    float cv;
+    if (use_new) {
+        cv = ncc_new(a, px, py, s, pl);
+    } else {
+        RefWin rw;
+        build_refwin(a, px, py, rw);
+        cv = ncc_old(a, px, py, s, pl, rw);
+    }
+    // stable top-k of the N costs (insertion sort, APD.cu:3-12, 754-769)
+    const int topk_max = 4;
+    float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+    int nt = 0, nvalid = 0;
+    for (int k = 0; k < N; ++k) {
+        const float x = __shfl(cv, G.base + k);
+        if (x < APD_COST_MAX) nvalid++;
+        // position = number of kept values <= x
+        int p = (nt > 0 && t0 <= x) + (nt > 1 && t1 <= x) + (nt > 2 && t2 <= x) + (nt > 3 && t3 <= x);
+        if (p < topk_max) {
+            if (p <= 2) t3 = t2;
+            if (p <= 1) t2 = t1;
+            if (p <= 0) t1 = t0;
+            if (p == 0) t0 = x;
+            else if (p == 1) t1 = x;
+            else if (p == 2) t2 = x;
+            else t3 = x;
+            if (nt < topk_max) nt++;
+        }
+    }
+    const int top_k = min(nvalid, a.top_k);
+    const float thr = top_k <= 1 ? t0 : (top_k == 2 ? t1 : (top_k == 3 ? t2 : t3));
+    const uint32_t bits = group_bits(cv <= thr, G);
+    if (G.valid && G.v == 0) {
+        float cost_out = APD_COST_MAX;
+        uint32_t sv = 0;
+        if (top_k > 0) {
+            float sum = 0.0f;
+            sum += t0;
+            if (top_k > 1) sum += t1;
+            if (top_k > 2) sum += t2;
+            if (top_k > 3) sum += t3;
+            cost_out = sum / (float)top_k;
+            sv = bits;
+        }
+        a.plane[c] = pl;
+        a.cost[c] = cost_out;
+        a.sel[c] = sv;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// shared pieces of the two checkerboard sweeps
+// ---------------------------------------------------------------------------------------------
+// Multi-hypothesis joint view selection (APD.cu:1339-1374 / 1505-1540) for the lane's view.
+// Returns this lane's view weight (0..15).
+__device__ __forceinline__ int view_selection(const float ca[8], float prior, int iter, Rng &g, const Group &G,
+                                              int N) {
+    const float thr = (float)(0.8 * (double)d_expf((float)(iter * iter) / (-90.0f)));
+    float count = 0.0f, tmpw = 0.0f;
+    int cf = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float c = ca[j];
+        if (c < thr) { tmpw += d_expf(c * c / (-0.18f)); count += 1.0f; }
+        if (c > 1.2f) cf++;
+    }
+    float sp = 0.0f;
+    if (count > 2 && cf < 3) sp = tmpw / count;
+    else if (cf < 3) sp = d_expf(thr * thr / (-0.32f));
+    sp = sp * prior;
+    // TransformPDFToCDF (APD.cu:174-188): in-order sums over the pixel's N lanes
+    float sum = 0.0f;
+    for (int k = 0; k < N; ++k) sum += __shfl(sp, G.base + k);
+    const float inv = 1.0f / sum;
+    float cum = 0.0f, mycdf = 0.0f;
+    for (int k = 0; k < N; ++k) {
+        cum = fmaf(__shfl(sp, G.base + k), inv, cum);
+        if (k == G.v) mycdf = cum;
+    }
+    int w = 0;
+    for (int smp = 0; smp < 15; ++smp) {
+        const float u = g.uniform() - APD_FLT_EPSILON;
+        const uint32_t m = group_bits(mycdf > u, G);
+        if (m != 0u && (__ffs(m) - 1) == G.v) w++;
+    }
+    return w;
+}
+
+// PlaneHypothesisRefinement{Strong,Weak} candidate generation (APD.cu:961-980 / 1054-1067)
+struct Cands {
+    float4 nrand, npert;
+    float drand, dpert;
+};
+__device__ __forceinline__ Cands refine_candidates(const Args &a, int px, int py, Rng &g, float4 cur, float depth) {
+    const Cam &cam = a.cams[0];
+    Cands C;
+    C.drand = g.uniform() * (a.dmax - a.dmin) + a.dmin;
+    C.nrand = random_normal(cam, px, py, g, depth);
+    float dp = depth;
+    const float dminp = (1 - 0.02f) * dp;
+    const float dmaxp = (1 + 0.02f) * dp;
+    int guard = 0;
+    do {
+        dp = g.uniform() * (dmaxp - dminp) + dminp;
+    } while (dp < a.dmin && dp > a.dmax && ++guard < 64);
+    C.dpert = dp;
+    const float pert = (float)((double)0.02f * 3.14159265358979323846);
+    C.npert = perturbed_normal(cam, px, py, cur, g, pert);
+    return C;
+}
+// candidate k of {depth_rand,cur,depth_rand,cur,perturbed} x {cur,rand,rand,perturbed,cur}
+__device__ __forceinline__ float4 candidate(const Cands &C, int k, float4 cur0, float d0, float &dk) {
+    dk = (k == 0 || k == 2) ? C.drand : (k == 4 ? C.dpert : d0);
+    return (k == 0 || k == 4) ? cur0 : (k == 3 ? C.npert : C.nrand);
+}
+
+// ---------------------------------------------------------------------------------------------
+// CheckerboardPropagationStrong + PlaneHypothesisRefinementStrong (APD.cu:1098-1440, 950-1006)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_sweep_strong(Args a, const int *__restrict__ list, int count, int iter) {
+    const int N = a.N, W = a.W, H = a.H;
+    const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
+    if (wave * (WAVE / N) >= count) return;
+    const Group G = make_group(N, count, wave);
+    const int c = list[G.li];
+    const int py = c / W, px = c - py * W;
+    const int s = G.v + 1;
+    const Cam &cam0 = a.cams[0];
+    const float *__restrict__ cost = a.cost;
+
+    // adaptive checkerboard neighbour selection (APD.cu:1127-1316); identical in every lane
+    int pos[8];
+    bool flag[8];
+    {
+        float cmin;
+        int cminp;
+        int up_near = c - W, up_far = c - 3 * W, down_near = c + W, down_far = c + 3 * W;
+        int left_near = c - 1, left_far = c - 3, right_near = c + 1, right_far = c + 3;
+        flag[1] = py > 2;
+        if (flag[1]) {
+            cmin = cost[up_far]; cminp = up_far;
+            for (int i = 1; i < 11; ++i)
+                if (py > 2 + 2 * i) { int t = up_far - 2 * i * W; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
+            up_far = cminp;
+        }
+        flag[3] = py < H - 3;
+        if (flag[3]) {
+            cmin = cost[down_far]; cminp = down_far;
+            for (int i = 1; i < 11; ++i)
+                if (py < H - 3 - 2 * i) { int t = down_far + 2 * i * W; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
+            down_far = cminp;
+        }
+        flag[5] = px > 2;
+        if (flag[5]) {
+            cmin = cost[left_far]; cminp = left_far;
+            for (int i = 1; i < 11; ++i)
+                if (px > 2 + 2 * i) { int t = left_far - 2 * i; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
+            left_far = cminp;
+        }
+        flag[7] = px < W - 3;
+        if (flag[7]) {
+            cmin = cost[right_far]; cminp = right_far;
+            for (int i = 1; i < 11; ++i)
+                if (px < W - 3 - 2 * i) { int t = right_far + 2 * i; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
+            right_far = cminp;
+        }
+        flag[0] = py > 0;
+        if (flag[0]) {
+            cmin = cost[up_near]; cminp = up_near;
+            for (int i = 0; i < 3; ++i) {
+                if (py > 1 + i && px > i) { int t = up_near - (1 + i) * W - (i + 1); float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
+                if (py > 1 + i && px < W - 1 - i) { int t = up_near - (1 + i) * W + (i + 1); float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
+            }
+            up_near = cminp;
+        }
+        flag[2] = py < H - 1;
+        if (flag[2]) {
+            cmin = cost[down_near]; cminp = down_near;
+            for (int i = 0; i < 3; ++i) {
+                if (py < H - 2 - i && px > i) { int t = down_near + (1 + i) * W - (i + 1); float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
+                if (py < H - 2 - i && px < W - 1 - i) { int t = down_near + (1 + i) * W + (i + 1); float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
+            }
+            down_near = cminp;
+        }
+        flag[4] = px > 0;
+        if (flag[4]) {
+            cmin = cost[left_near]; cminp = left_near;
+            for (int i = 0; i < 3; ++i) {
+                if (px > 1 + i && py > i) { int t = left_near - (1 + i) - (i + 1) * W; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
+                if (px > 1 + i && py < H - 1 - i) { int t = left_near - (1 + i) + (i + 1) * W; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
+            }
+            left_near = cminp;
+        }
+        flag[6] = px < W - 1;
+        if (flag[6]) {
+            cmin = cost[right_near]; cminp = right_near;
+            for (int i = 0; i < 3; ++i) {
+                if (px < W - 2 - i && py > i) { int t = right_near + (1 + i) - (i + 1) * W; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
+                if (px < W - 2 - i && py < H - 1 - i) { int t = right_near + (1 + i) + (i + 1) * W; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
+            }
+            right_near = cminp;
+        }
+        pos[0] = up_near; pos[1] = up_far; pos[2] = down_near; pos[3] = down_far;
+        pos[4] = left_near; pos[5] = left_far; pos[6] = right_near; pos[7] = right_far;
+    }
+
+    RefWin rw;
+    build_refwin(a, px, py, rw);
+    const bool geom_imp = a.geom && a.impetus;
+    const float gf = a.gf;
+    const float4 cur = a.plane[c];
+
+    // hypotheses 0..7 = propagated planes, 8 = current plane (cost_now)
+    float ca[8];
+    float cv_now = 0.0f;
+#pragma unroll 1
+    for (int h = 0; h < 9; ++h) {
+        int ph = pos[0];
+        bool fh = flag[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) if (h == k) { ph = pos[k]; fh = flag[k]; }
+        if (h == 8) fh = true;
+        float val = (h == 0 && G.v == 0) ? 2.0f : 0.0f;  // float cost_array[8][32] = {2.0f} (APD.cu:1120)
+        if (fh) {
+            const float4 pl = (h == 8) ? cur : a.plane[ph];
+            val = ncc_old(a, px, py, s, pl, rw);
+            if (h == 8 && geom_imp) val = fmaf(gf, geom_cost(a, px, py, s, pl), val);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) if (h == k) ca[k] = val;
+        if (h == 8) cv_now = val;
+    }
+
+    // view selection priors from the 4 direct neighbours (APD.cu:1323-1337)
+    float prior = 0.0f;
+    {
+        const int nb[4] = {c - W, c + W, c - 1, c + 1};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (flag[2 * i]) prior += ((a.sel[nb[i]] >> G.v) & 1u) ? 0.9f : 0.1f;
+    }
+    Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ord_strong(iter));
+    const int w = view_selection(ca, prior, iter, g, G, N);
+    const uint32_t tsel = group_bits(w > 0, G);
+
+    // weighted hypothesis costs (APD.cu:1388-1399), weight_norm, cost_now (1401-1413)
+    float fc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float wn = 0.0f, cost_now = 0.0f;
+    for (int k = 0; k < N; ++k) {
+        const int wk = __shfl(w, G.base + k);
+        const float fwk = (float)wk;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float ck = __shfl(ca[j], G.base + k);
+            if (wk > 0) fc[j] = fmaf(fwk, ck, fc[j]);
+        }
+        if (wk > 0) wn += fwk;
+        cost_now = fmaf(fwk, __shfl(cv_now, G.base + k), cost_now);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fc[j] /= wn;
+    cost_now /= wn;
+    const float cost_init = cost_now;
+    int mi = 0;
+    {
+        float m = fc[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) if (fc[j] <= m) { m = fc[j]; mi = j; }
+    }
+    float depth_now = depth_from_plane(cam0, cur, px, py);
+    float4 pnow = cur;
+    {
+        int pm = pos[0];
+        bool fm = flag[0];
+        float fcm = fc[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) if (mi == k) { pm = pos[k]; fm = flag[k]; fcm = fc[k]; }
+        if (fm) {
+            const float4 cand = a.plane[pm];
+            const float db = depth_from_plane(cam0, cand, px, py);
+            if (db >= a.dmin && db <= a.dmax && fcm < cost_now) {
+                depth_now = db; pnow = cand; cost_now = fcm;
+                if (G.valid && G.v == 0) a.sel[c] = tsel;
+            }
+        }
+    }
+
+    // PlaneHypothesisRefinementStrong (APD.cu:950-1006)
+    const Cands C = refine_candidates(a, px, py, g, pnow, depth_now);
+    const float4 cur0 = pnow;
+    const float d0 = depth_now;
+#pragma unroll 1
+    for (int k = 0; k < 5; ++k) {
+        float dk;
+        float4 t = candidate(C, k, cur0, d0, dk);
+        t.w = dist2origin(cam0, px, py, dk, t);
+        float cv = ncc_old(a, px, py, s, t, rw);
+        if (geom_imp) cv = fmaf(gf, geom_cost(a, px, py, s, t), cv);
+        float tc = 0.0f;
+        for (int kk = 0; kk < N; ++kk) tc = fmaf((float)__shfl(w, G.base + kk), __shfl(cv, G.base + kk), tc);
+        tc /= wn;
+        const float db = depth_from_plane(cam0, t, px, py);
+        if (db >= a.dmin && db <= a.dmax && tc < cost_now) { depth_now = db; pnow = t; cost_now = tc; }
+    }
+    if (G.valid) {
+        a.vw[(size_t)G.v * a.HW + c] = (uint8_t)w;
+        if (G.v == 0) {
+            if (a.state == APD_REFINE_INIT) {
+                if ((double)cost_now < (double)cost_init - 0.1) { a.cost[c] = cost_now; a.plane[c] = pnow; }
+                else a.cost[c] = cost_init;
+            } else {
+                a.cost[c] = cost_now;
+                a.plane[c] = pnow;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// CheckerboardPropagationWeak + PlaneHypothesisRefinementWeak (APD.cu:1442-1615, 1008-1096)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_sweep_weak(Args a, const int *__restrict__ list, int count, int iter) {
+    const int N = a.N, W = a.W;
+    const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
+    if (wave * (WAVE / N) >= count) return;
+    const Group G = make_group(N, count, wave);
+    const int c = list[G.li];
+    const int py = c / W, px = c - py * W;
+    const int s = G.v + 1;
+    const Cam &cam0 = a.cams[0];
+    const short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
+    const bool geom = a.geom != 0;
+    const float gf = a.gf;
+    const float4 cur = a.plane[c];
+
+    int pos[8];
+    bool flag[8];
+    float prior = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const short2 ap = anc[i + 1];
+        const bool ok = !(ap.x == -1 || ap.y == -1);
+        pos[i] = ok ? ap.x + ap.y * W : 0;
+        flag[i] = ok && a.weak[pos[i]] == APD_STRONG;
+        if (ok) prior += ((a.sel[pos[i]] >> G.v) & 1u) ? 0.9f : 0.1f;
+    }
+    float ca[8];
+    float cv_now = 0.0f;
+#pragma unroll 1
+    for (int h = 0; h < 9; ++h) {
+        int ph = pos[0];
+        bool fh = flag[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) if (h == k) { ph = pos[k]; fh = flag[k]; }
+        if (h == 8) fh = true;
+        float val = (h == 0 && G.v == 0) ? 2.0f : 0.0f;
+        if (fh) {
+            const float4 pl = (h == 8) ? cur : a.plane[ph];
+            val = ncc_new(a, px, py, s, pl);
+            if (h == 8 && geom) val = fmaf(gf, geom_cost(a, px, py, s, pl), val);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) if (h == k) ca[k] = val;
+        if (h == 8) cv_now = val;
+    }
+    Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ord_weak(iter));
+    const int w = view_selection(ca, prior, iter, g, G, N);
+    const uint32_t tsel = group_bits(w > 0, G);
+
+    // hypothesis costs with the geometric term (APD.cu:1554-1573)
+    float gval[8];
+#pragma unroll 1
+    for (int j = 0; j < 8; ++j) {
+        int pj = pos[0];
+        bool fj = flag[0];
+        float cj = ca[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) if (j == k) { pj = pos[k]; fj = flag[k]; cj = ca[k]; }
+        float v = cj;
+        if (geom && w > 0) v = fj ? fmaf(gf, geom_cost(a, px, py, s, a.plane[pj]), cj) : fmaf(gf, 3.0f, cj);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) if (j == k) gval[k] = v;
+    }
+    float fc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float wn = 0.0f, cost_now = 0.0f;
+    for (int k = 0; k < N; ++k) {
+        const int wk = __shfl(w, G.base + k);
+        const float fwk = (float)wk;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float vk = __shfl(gval[j], G.base + k);
+            if (wk > 0) fc[j] = fmaf(fwk, vk, fc[j]);
+        }
+        if (wk > 0) wn += fwk;
+        cost_now = fmaf(fwk, __shfl(cv_now, G.base + k), cost_now);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fc[j] /= wn;
+    cost_now /= wn;
+    const float cost_init = cost_now;
+    int mi = 0;
+    {
+        float m = fc[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) if (fc[j] <= m) { m = fc[j]; mi = j; }
+    }
+    float depth_now = depth_from_plane(cam0, cur, px, py);
+    float4 pnow = cur;
+    {
+        int pm = pos[0];
+        bool fm = flag[0];
+        float fcm = fc[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) if (mi == k) { pm = pos[k]; fm = flag[k]; fcm = fc[k]; }
+        if (fm) {
+            const float4 cand = a.plane[pm];
+            const float db = depth_from_plane(cam0, cand, px, py);
+            if (db >= a.dmin && db <= a.dmax && fcm < cost_now) {
+                depth_now = db; pnow = cand; cost_now = fcm;
+                if (G.valid && G.v == 0) a.sel[c] = tsel;
+            }
+        }
+    }
+    // PlaneHypothesisRefinementWeak (APD.cu:1008-1096): fit plane first, then 5 random candidates;
+    // a zero fit normal skips the whole refinement (APD.cu:1028-1030).
+    const float4 fit = a.fit[c];
+    if (!(fit.x == 0 && fit.y == 0 && fit.z == 0)) {  // group-uniform
+        {
+            float cv = 0.0f;
+            if (w > 0) {
+                cv = ncc_new(a, px, py, s, fit);
+                if (geom) cv = fmaf(gf, geom_cost(a, px, py, s, fit), cv);
+            }
+            float tc = 0.0f;
+            for (int kk = 0; kk < N; ++kk) {
+                const int wk = __shfl(w, G.base + kk);
+                const float vk = __shfl(cv, G.base + kk);
+                if (wk > 0) tc = fmaf((float)wk, vk, tc);
+            }
+            tc /= wn;
+            const float db = depth_from_plane(cam0, fit, px, py);
+            if (db >= a.dmin && db <= a.dmax && tc < cost_now) { depth_now = db; pnow = fit; cost_now = tc; }
+        }
+        const Cands C = refine_candidates(a, px, py, g, pnow, depth_now);
+        const float4 cur0 = pnow;
+        const float d0 = depth_now;
+#pragma unroll 1
+        for (int k = 0; k < 5; ++k) {
+            float dk;
+            float4 t = candidate(C, k, cur0, d0, dk);
+            t.w = dist2origin(cam0, px, py, dk, t);
+            float cv = 0.0f;
+            if (w > 0) {
+                cv = ncc_new(a, px, py, s, t);
+                if (geom) cv = fmaf(gf, geom_cost(a, px, py, s, t), cv);
+            }
+            float tc = 0.0f;
+            for (int kk = 0; kk < N; ++kk) {
+                const int wk = __shfl(w, G.base + kk);
+                const float vk = __shfl(cv, G.base + kk);
+                if (wk > 0) tc = fmaf((float)wk, vk, tc);
+            }
+            tc /= wn;
+            const float db = depth_from_plane(cam0, t, px, py);
+            if (db >= a.dmin && db <= a.dmax && tc < cost_now) { depth_now = db; pnow = t; cost_now = tc; }
+        }
+    }
+    if (G.valid) {
+        a.vw[(size_t)G.v * a.HW + c] = (uint8_t)w;
+        if (G.v == 0) {
+            if (a.state == APD_REFINE_INIT) {
+                if ((double)cost_now < (double)cost_init - 0.1) { a.cost[c] = cost_now; a.plane[c] = pnow; }
+                else a.cost[c] = cost_init;
+            } else {
+                a.cost[c] = cost_now;
+                a.plane[c] = pnow;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// post-sweep kernels
+// ---------------------------------------------------------------------------------------------
+// GetDepthandNormal (APD.cu:1694-1709)
+__global__ __launch_bounds__(BLOCK) void k_depth_normal(Args a) {
+    const int c = blockIdx.x * BLOCK + threadIdx.x;
+    if (c >= a.HW) return;
+    const int py = c / a.W, px = c - py * a.W;
+    float4 p = a.plane[c];
+    p.w = depth_from_plane(a.cams[0], p, px, py);
+    a.plane[c] = to_world(a.cams[0], p);
+}
+
+// CheckerboardFilterStrong (APD.cu:1711-1821), over the Strong-sweep pixel list of one colour
+__global__ __launch_bounds__(BLOCK) void k_filter(Args a, const int *__restrict__ list, int count) {
+    const int li = blockIdx.x * BLOCK + threadIdx.x;
+    if (li >= count) return;
+    const int W = a.W, H = a.H;
+    const int c = list[li];
+    const int py = c / W, px = c - py * W;
+    if (a.cost[c] < 0.001f) return;
+    float f[21];
+    int n = 0;
+    f[n++] = a.plane[c].w;
+    const int left = c - 1, leftleft = c - 3, up = c - W, upup = c - 3 * W;
+    const int down = c + W, downdown = c + 3 * W, right = c + 1, rightright = c + 3;
+    const uint8_t *wk = a.weak;
+#define FADD(cond, idx) if ((cond) && wk[(idx)] == APD_STRONG) f[n++] = a.plane[(idx)].w
+    FADD(py > 0, up);
+    FADD(py > 2, upup);
+    FADD(py > 4, upup - W * 2);
+    FADD(py < H - 1, down);
+    FADD(py < H - 3, downdown);
+    FADD(py < H - 5, downdown + W * 2);
+    FADD(px > 0, left);
+    FADD(px > 2, leftleft);
+    FADD(px > 4, leftleft - 2);
+    FADD(px < W - 1, right);
+    FADD(px < W - 3, rightright);
+    FADD(px < W - 5, rightright + 2);
+    FADD(py > 0 && px < W - 2, up + 2);
+    FADD(py < H - 1 && px < W - 2, down + 2);
+    FADD(py > 0 && px > 1, up - 2);
+    FADD(py < H - 1 && px > 1, down - 2);
+    FADD(px > 0 && py > 2, left - W * 2);
+    FADD(px < W - 1 && py > 2, right - W * 2);
+    FADD(px > 0 && py < H - 2, left + W * 2);
+    FADD(px < W - 1 && py < H - 2, right + W * 2);
+#undef FADD
+    for (int i = 1; i < n; ++i) {
+        float t = f[i];
+        int j;
+        for (j = i; j >= 1 && t < f[j - 1]; j--) f[j] = f[j - 1];
+        f[j] = t;
+    }
+    const int m = n / 2;
+    a.plane[c].w = (n % 2 == 0) ? (f[m - 1] + f[m]) / 2 : f[m];
+}
+
+// DepthToWeak (APD.cu:2103-2250): 61-sample disparity sweep of the selected views -> PixelState.
+// The cost curve of each pixel is staged in LDS for the peak analysis.
+__global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
+    extern __shared__ float lds_curve[];
+    const int N = a.N, W = a.W, H = a.H;
+    const int P = WAVE / N;
+    const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
+    const Group G = make_group(N, a.HW, wave);   // no early exit: __syncthreads below
+    const int c = G.li;
+    const int py = c / W, px = c - py * W;
+    const int s = G.v + 1;
+    const Cam &cam0 = a.cams[0];
+    float *pc = lds_curve + ((threadIdx.x >> 6) * P + G.slot) * 61;
+    const bool border = px < 6 || py < 6 || px >= W - 6 || py >= H - 6;
+    const float4 pl = to_ref(cam0, a.plane[c]);
+    const float od = pl.w;
+    const uint32_t sv = a.sel[c];
+    const bool mine = (sv >> G.v) & 1u;
+    const int wv = a.vw[(size_t)G.v * a.HW + c];
+    float mydist;
+    {
+        const Cam &sc = a.cams[s];
+        float d0 = cam0.c[0] - sc.c[0], d1 = cam0.c[1] - sc.c[1], d2 = cam0.c[2] - sc.c[2];
+        mydist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+    }
+    float base = 0.0f, wn = 0.0f;
+    int valid = 0;
+    for (int k = 0; k < N; ++k) {
+        const float dk = __shfl(mydist, G.base + k);
+        const int wk = __shfl(wv, G.base + k);
+        if ((sv >> k) & 1u) { wn += (float)wk; base += dk; valid++; }
+    }
+    // per-pixel early outs (group-uniform)
+    int state = -1;
+    if (border || od == 0) state = APD_UNKNOWN;
+    else if (valid == 0) state = APD_UNKNOWN;
+    const bool active = state < 0;
+    if (active) base /= (float)valid;
+    const float disp = cam0.K[0] * base / od;
+    RefWin rw;
+    build_refwin(a, px, py, rw);
+    const bool geom = a.geom != 0;
+    const float gf = a.gf;
+#pragma unroll 1
+    for (int d = 0; d < 61; ++d) {
+        const float pdepth = cam0.K[0] * base / (disp + (float)(d - 30));
+        const bool in_range = !(pdepth < a.dmin || pdepth > a.dmax);
+        float tc = 0.0f;
+        if (active && in_range && mine) {
+            float4 t = pl;
+            t.w = dist2origin(cam0, px, py, pdepth, t);
+            tc = ncc_old(a, px, py, s, t, rw);
+            if (geom) tc = fmaf(gf, geom_cost(a, px, py, s, t), tc);
+        }
+        float p = 0.0f;
+        for (int k = 0; k < N; ++k) {
+            const float tk = __shfl(tc, G.base + k);
+            const int wk = __shfl(wv, G.base + k);
+            if ((sv >> k) & 1u) p = fmaf(tk, (float)wk, p);
+        }
+        p /= wn;
+        const float val = in_range ? ((2.0f > p) ? p : 2.0f) : 2.0f;
+        if (G.v == 0 && G.valid) {
+            pc[d] = val;
+            if (a.curve && active) a.curve[(size_t)c * 61 + d] = val;
+        }
+    }
+    __syncthreads();
+    if (active) {
+        int cnt = 0, min_peak = 0;
+        float min_cost = 2.0f;
+        uint64_t peaks = 0;
+        for (int i = 2; i < 59; ++i) {
+            const float ci = pc[i];
+            if (pc[i - 1] > ci && pc[i + 1] > ci) {
+                peaks |= 1ull << i;
+                cnt++;
+                if (ci < min_cost) { min_peak = i; min_cost = ci; }
+            }
+        }
+        if (abs(min_peak - 30) > a.peak_radius || pc[min_peak] > 0.5f) {
+            state = APD_WEAK;
+        } else if (cnt == 1) {
+            state = (pc[min_peak] <= 0.15f) ? APD_STRONG : APD_WEAK;
+        } else {
+            float var = 0.0f;
+            for (int i = 2; i < 59; ++i) {
+                if (((peaks >> i) & 1ull) && i != min_peak) { float dd = pc[i] - min_cost; var = fmaf(dd, dd, var); }
+            }
+            var = sqrtf(var);
+            var /= (float)(cnt - 1);
+            state = (var > 0.2f) ? APD_STRONG : APD_WEAK;
+        }
+    }
+    if (G.valid && G.v == 0) a.weak[c] = (uint8_t)state;
+}
+
+// ConfidenceCompute (APD.cu:2282-2344)
+__global__ __launch_bounds__(BLOCK) void k_confidence(Args a) {
+    const int c = blockIdx.x * BLOCK + threadIdx.x;
+    if (c >= a.HW) return;
+    const int W = a.W;
+    const int py = c / W, px = c - py * W;
+    a.conf[c] = 0;
+    const Cam &rc = a.cams[0];
+    const uint32_t sv = a.sel[c];
+    const float rd = a.plane[c].w;
+    if (rd <= 0.0f) { a.weak[c] = APD_UNKNOWN; return; }
+    float P[3];
+    world_point(rc, (float)px, (float)py, rd, P);
+    int nc = 1;
+    for (int i = 0; i < a.N; ++i) {
+        if (!((sv >> i) & 1u)) continue;
+        const int s = i + 1;
+        const Cam &sc = a.cams[s];
+        float sx, sy, sd;
+        project_cam(P, sc, sx, sy, sd);
+        const float src_depth = a.depth[(size_t)s * a.HW + trunc_clamp(sy, a.H) * W + trunc_clamp(sx, W)];
+        if (src_depth <= 0.0f) continue;
+        nc += 1;
+        float Q[3];
+        world_point(sc, sx, sy, src_depth, Q);
+        float bx, by, refd;
+        project_cam(Q, rc, bx, by, refd);
+        const float dx = (float)px - bx, dy = (float)py - by;
+        if (sqrtf(dx * dx + dy * dy) <= 2.0f) nc += 2;
+        if (fabsf(rd - refd) / rd <= 0.02f) nc += 2;
+    }
+    if (nc > 255) nc = 255;
+    a.conf[c] = (uint8_t)nc;
+}
+
+// LocalRefine (APD.cu:2346-2432)
+__global__ __launch_bounds__(BLOCK) void k_local_refine(Args a) {
+    const int N = a.N, W = a.W;
+    const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
+    if (wave * (WAVE / N) >= a.HW) return;
+    const Group G = make_group(N, a.HW, wave);
+    const int c = G.li;
+    const int py = c / W, px = c - py * W;
+    const int s = G.v + 1;
+    const Cam &cam0 = a.cams[0];
+    const float4 pl = to_ref(cam0, a.plane[c]);
+    const float od = pl.w;
+    const uint32_t sv = a.sel[c];
+    const bool mine = (sv >> G.v) & 1u;
+    const int wv = a.vw[(size_t)G.v * a.HW + c];
+    const bool geom = a.geom != 0;
+    const float gf = a.gf;
+    RefWin rw;
+    build_refwin(a, px, py, rw);
+    float mydist, tc0 = 0.0f;
+    {
+        const Cam &sc = a.cams[s];
+        float d0 = cam0.c[0] - sc.c[0], d1 = cam0.c[1] - sc.c[1], d2 = cam0.c[2] - sc.c[2];
+        mydist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+    }
+    const bool live = od != 0;  // group-uniform
+    if (live && mine) {
+        float4 t = pl;
+        t.w = dist2origin(cam0, px, py, od, t);
+        tc0 = ncc_old(a, px, py, s, t, rw);
+        if (geom) tc0 = fmaf(gf, geom_cost(a, px, py, s, t), tc0);
+    }
+    float cost_now = 0.0f, base = 0.0f, wn = 0.0f;
+    int valid = 0;
+    for (int k = 0; k < N; ++k) {
+        const float tk = __shfl(tc0, G.base + k);
+        const int wk = __shfl(wv, G.base + k);
+        const float dk = __shfl(mydist, G.base + k);
+        if ((sv >> k) & 1u) {
+            cost_now = fmaf(tk, (float)wk, cost_now);
+            wn += (float)wk;
+            base += dk;
+            valid++;
+        }
+    }
+    const bool run = live && !(wn == 0 || valid == 0);
+    if (run) { cost_now /= wn; base /= (float)valid; }
+    const float disp = cam0.K[0] * base / od;
+    float min_cost = 2.0f, best = od;
+#pragma unroll 1
+    for (int d = -5; d <= 5; ++d) {
+        const float pdepth = cam0.K[0] * base / (disp + (float)d);
+        const bool in_range = !(pdepth < a.dmin || pdepth > a.dmax);
+        float nv = 0.0f, gv = 0.0f;
+        if (run && in_range && mine) {
+            float4 t = pl;
+            t.w = dist2origin(cam0, px, py, pdepth, t);
+            nv = ncc_old(a, px, py, s, t, rw);
+            if (geom) gv = gf * geom_cost(a, px, py, s, t);
+        }
+        float tc = 0.0f;
+        for (int k = 0; k < N; ++k) {
+            const float nk = __shfl(nv, G.base + k);
+            const float gk = __shfl(gv, G.base + k);
+            const int wk = __shfl(wv, G.base + k);
+            if ((sv >> k) & 1u) {
+                tc = fmaf(nk, (float)wk, tc);
+                if (geom) tc = fmaf(gk, (float)wk, tc);
+            }
+        }
+        tc /= wn;
+        if (run && in_range && tc < min_cost) { min_cost = tc; best = pdepth; }
+    }
+    if (run && G.valid && G.v == 0 && (double)(cost_now - min_cost) > 0.1) a.plane[c].w = best;
+}
+
+// =============================================================================================
+// host side: context, buffers, C ABI
+// =============================================================================================
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+const char *g_global_err = "";
+std::string g_global_err_store;
+
+void set_global_err(const std::string &s) {
+    g_global_err_store = s;
+    g_global_err = g_global_err_store.c_str();
+}
+
+}  // namespace
+
+struct apd_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // buffers
+    DevBuf imgs, quad, depth, views, cams, plane, cost, sel, vw, weak, conf, sa, amap, anchors, reliable, nearest,
+        fit, curve, lists, rowcnt, rowoff, totals, near_off;
+    int n_near = 0;
+    Args args{};
+    bool loaded = false, prepared = false;
+    int weak_count = 0;
+    int cnt[4] = {0, 0, 0, 0};     // strong black, strong red, weak black, weak red
+    size_t list_cap = 0;
+    bool want_curve = false;
+    apd_params params{};
+    // timing
+    hipEvent_t ev[16] = {};
+    apd_timing timing{};
+    // profiling of the dominant kernel
+    bool prof = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
+    int64_t prof_pixels = 0;
+};
+
+#define HIP_OK(ctx, call)                                                                          \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);                        \
+            return APD_EDEVICE;                                                                    \
+        }                                                                                          \
+    } while (0)
+
+static int ensure(apd_ctx *ctx, DevBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return APD_OK;
+    if (b.p) hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    if (hipMalloc(&b.p, bytes) != hipSuccess) {
+        ctx->err = "hipMalloc(" + std::to_string(bytes) + ") failed";
+        return APD_ENOMEM;
+    }
+    b.bytes = bytes;
+    return APD_OK;
+}
+
+static int check_launch(apd_ctx *ctx, const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        ctx->err = std::string("launch ") + what + ": " + hipGetErrorString(e);
+        return APD_EDEVICE;
+    }
+    return APD_OK;
+}
+
+// Per-source precompute of the homography pieces, in double (same formulas as the oracle).
+static void precompute_views(const apd_camera *cams, int ni, SrcView *views, Args &a) {
+    const apd_camera &r = cams[0];
+    const double kr0 = r.K[0], kr2 = r.K[2], kr4 = r.K[4], kr5 = r.K[5];
+    const double Kri[9] = {1.0 / kr0, 0.0, -kr2 / kr0, 0.0, 1.0 / kr4, -kr5 / kr4, 0.0, 0.0, 1.0};
+    a.ikx = (float)(1.0 / kr0);
+    a.iky = (float)(1.0 / kr4);
+    a.cxk = (float)(kr2 / kr0);
+    a.cyk = (float)(kr5 / kr4);
+    double rC[3];
+    for (int j = 0; j < 3; ++j)
+        rC[j] = -((double)r.R[j] * r.t[0] + (double)r.R[3 + j] * r.t[1] + (double)r.R[6 + j] * r.t[2]);
+    for (int s = 0; s < ni; ++s) {
+        const apd_camera &c = cams[s];
+        double sC[3], Crel[3], trel[3], Rrel[9];
+        for (int j = 0; j < 3; ++j)
+            sC[j] = -((double)c.R[j] * c.t[0] + (double)c.R[3 + j] * c.t[1] + (double)c.R[6 + j] * c.t[2]);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                Rrel[3 * i + j] = (double)c.R[3 * i] * r.R[3 * j] + (double)c.R[3 * i + 1] * r.R[3 * j + 1] +
+                                  (double)c.R[3 * i + 2] * r.R[3 * j + 2];
+        for (int j = 0; j < 3; ++j) Crel[j] = rC[j] - sC[j];
+        for (int i = 0; i < 3; ++i)
+            trel[i] = (double)c.R[3 * i] * Crel[0] + (double)c.R[3 * i + 1] * Crel[1] + (double)c.R[3 * i + 2] * Crel[2];
+        const double Ks[9] = {c.K[0], 0.0, c.K[2], 0.0, c.K[4], c.K[5], 0.0, 0.0, c.K[8]};
+        double KR[9], A[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                KR[3 * i + j] = Ks[3 * i] * Rrel[j] + Ks[3 * i + 1] * Rrel[3 + j] + Ks[3 * i + 2] * Rrel[6 + j];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                A[3 * i + j] = KR[3 * i] * Kri[j] + KR[3 * i + 1] * Kri[3 + j] + KR[3 * i + 2] * Kri[6 + j];
+        for (int k = 0; k < 9; ++k) views[s].A[k] = (float)A[k];
+        for (int i = 0; i < 3; ++i)
+            views[s].b[i] = (float)(Ks[3 * i] * trel[0] + Ks[3 * i + 1] * trel[1] + Ks[3 * i + 2] * trel[2]);
+    }
+}
+
+static int build_near_offsets(apd_ctx *ctx) {
+    if (ctx->n_near) return APD_OK;
+    std::vector<short2> off;
+    off.reserve(201 * 201);
+    for (int x = -100; x <= 100; ++x)
+        for (int y = -100; y <= 100; ++y) off.push_back(make_short2((short)x, (short)y));
+    std::stable_sort(off.begin(), off.end(), [](const short2 &p, const short2 &q) {
+        return p.x * p.x + p.y * p.y < q.x * q.x + q.y * q.y;  // stable: keeps x-major, y-minor order
+    });
+    int st = ensure(ctx, ctx->near_off, off.size() * sizeof(short2));
+    if (st) return st;
+    HIP_OK(ctx, hipMemcpy(ctx->near_off.p, off.data(), off.size() * sizeof(short2), hipMemcpyHostToDevice));
+    ctx->n_near = (int)off.size();
+    return APD_OK;
+}
+
+static inline unsigned blocks_for(size_t n, int per_block) { return (unsigned)((n + per_block - 1) / per_block); }
+static inline unsigned group_blocks(int n_pixels, int N) {
+    const int P = WAVE / N;
+    const int waves = (n_pixels + P - 1) / P;
+    return (unsigned)((waves + (BLOCK / WAVE) - 1) / (BLOCK / WAVE));
+}
+
+extern "C" {
+
+int32_t apd_abi_version(void) { return APD_ABI_VERSION; }
+
+int32_t apd_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+apd_ctx *apd_create(int32_t device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        set_global_err("no HIP device visible");
+        return nullptr;
+    }
+    if (device < 0 || device >= n) {
+        set_global_err("device index out of range");
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        set_global_err("hipSetDevice failed");
+        return nullptr;
+    }
+    apd_ctx *ctx = new apd_ctx();
+    ctx->device = device;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        set_global_err("hipStreamCreate failed");
+        delete ctx;
+        return nullptr;
+    }
+    for (auto &e : ctx->ev) hipEventCreate(&e);
+    return ctx;
+}
+
+void apd_destroy(apd_ctx *ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
+                      &ctx->sel, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
+                      &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
+                      &ctx->rowoff, &ctx->totals, &ctx->near_off};
+    for (DevBuf *b : bufs)
+        if (b->p) hipFree(b->p);
+    for (auto &e : ctx->ev) hipEventDestroy(e);
+    for (auto &pe : ctx->prof_ev) { hipEventDestroy(pe.first); hipEventDestroy(pe.second); }
+    hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *apd_last_error(const apd_ctx *ctx) { return ctx ? ctx->err.c_str() : g_global_err; }
+
+int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
+    if (!ctx || !pb) return APD_EINVAL;
+    hipSetDevice(ctx->device);
+    ctx->loaded = ctx->prepared = false;
+    const int W = pb->width, H = pb->height, NI = pb->num_images;
+    if (NI > APD_MAX_IMAGES) { ctx->err = "num_images > 32"; return APD_ETOOMANYVIEWS; }
+    if (W < 1 || H < 1 || NI < 2 || !pb->images || !pb->cameras) { ctx->err = "bad problem dimensions"; return APD_EINVAL; }
+    if (W > 32767 || H > 32767 || (size_t)W * H > (size_t)1 << 30) { ctx->err = "image too large"; return APD_EINVAL; }
+    const apd_params &P = pb->params;
+    if (P.strong_radius != 5 || P.strong_increment != 2 || P.weak_radius != 5 || P.weak_increment != 5) {
+        ctx->err = "kernels are specialised for strong 5/2 and weak 5/5 windows (main.h:88-91)";
+        return APD_EINVAL;
+    }
+    if (P.top_k < 1 || P.top_k > 4) { ctx->err = "top_k must be 1..4"; return APD_EINVAL; }
+    if (P.max_iterations < 0) { ctx->err = "max_iterations < 0"; return APD_EINVAL; }
+    if (P.use_APD && (P.rotate_time < 1 || P.rotate_time > 4)) { ctx->err = "rotate_time must be 1..4"; return APD_EINVAL; }
+    if ((P.geom_consistency || P.use_APD) && !pb->depths) { ctx->err = "depth maps required (geom/APD)"; return APD_EINVAL; }
+    const int N = NI - 1;
+    const size_t HW = (size_t)W * H;
+    const size_t qstride = (size_t)(W + 1) * (H + 1);
+    int st;
+    if ((st = ensure(ctx, ctx->imgs, HW * NI * sizeof(float)))) return st;
+    if ((st = ensure(ctx, ctx->quad, qstride * N * sizeof(float4)))) return st;
+    if ((st = ensure(ctx, ctx->views, NI * sizeof(SrcView)))) return st;
+    if ((st = ensure(ctx, ctx->cams, NI * sizeof(Cam)))) return st;
+    if ((st = ensure(ctx, ctx->plane, HW * sizeof(float4)))) return st;
+    if ((st = ensure(ctx, ctx->cost, HW * sizeof(float)))) return st;
+    if ((st = ensure(ctx, ctx->sel, HW * sizeof(uint32_t)))) return st;
+    if ((st = ensure(ctx, ctx->vw, HW * N))) return st;
+    if ((st = ensure(ctx, ctx->weak, HW))) return st;
+    if ((st = ensure(ctx, ctx->conf, HW))) return st;
+    if ((st = ensure(ctx, ctx->sa, HW))) return st;
+    if ((st = ensure(ctx, ctx->lists, (HW + 8) * sizeof(int)))) return st;
+    if ((st = ensure(ctx, ctx->rowcnt, (size_t)H * sizeof(int)))) return st;
+    if ((st = ensure(ctx, ctx->rowoff, (size_t)H * sizeof(int)))) return st;
+    if ((st = ensure(ctx, ctx->totals, 8 * sizeof(int)))) return st;
+    const bool need_depth = P.geom_consistency || P.use_APD;
+    if (need_depth && (st = ensure(ctx, ctx->depth, HW * NI * sizeof(float)))) return st;
+    hipStream_t s = ctx->stream;
+    for (int i = 0; i < NI; ++i) {
+        if (!pb->images[i]) { ctx->err = "null image pointer"; return APD_EINVAL; }
+        HIP_OK(ctx, hipMemcpyAsync((float *)ctx->imgs.p + HW * i, pb->images[i], HW * sizeof(float),
+                                   hipMemcpyHostToDevice, s));
+    }
+    if (need_depth) {
+        for (int i = 0; i < NI; ++i) {
+            if (!pb->depths[i]) { ctx->err = "null depth pointer"; return APD_EINVAL; }
+            HIP_OK(ctx, hipMemcpyAsync((float *)ctx->depth.p + HW * i, pb->depths[i], HW * sizeof(float),
+                                       hipMemcpyHostToDevice, s));
+        }
+    }
+    std::vector<Cam> cams(NI);
+    std::vector<SrcView> views(NI);
+    for (int i = 0; i < NI; ++i) {
+        memcpy(cams[i].K, pb->cameras[i].K, 9 * sizeof(float));
+        memcpy(cams[i].R, pb->cameras[i].R, 9 * sizeof(float));
+        memcpy(cams[i].t, pb->cameras[i].t, 3 * sizeof(float));
+        memcpy(cams[i].c, pb->cameras[i].c, 3 * sizeof(float));
+    }
+    Args &a = ctx->args;
+    a = Args{};
+    precompute_views(pb->cameras, NI, views.data(), a);
+    HIP_OK(ctx, hipMemcpyAsync(ctx->cams.p, cams.data(), NI * sizeof(Cam), hipMemcpyHostToDevice, s));
+    HIP_OK(ctx, hipMemcpyAsync(ctx->views.p, views.data(), NI * sizeof(SrcView), hipMemcpyHostToDevice, s));
+    // priors (APD.cpp:612-683)
+    if (P.state != APD_FIRST_INIT && pb->init_planes)
+        HIP_OK(ctx, hipMemcpyAsync(ctx->plane.p, pb->init_planes, HW * sizeof(float4), hipMemcpyHostToDevice, s));
+    else
+        HIP_OK(ctx, hipMemsetAsync(ctx->plane.p, 0, HW * sizeof(float4), s));
+    int weak_count = 0;
+    if (P.use_APD && pb->weak_info) {
+        HIP_OK(ctx, hipMemcpyAsync(ctx->weak.p, pb->weak_info, HW, hipMemcpyHostToDevice, s));
+        for (size_t i = 0; i < HW; ++i) weak_count += pb->weak_info[i] == APD_WEAK;
+    } else {
+        HIP_OK(ctx, hipMemsetAsync(ctx->weak.p, APD_STRONG, HW, s));
+    }
+    if (P.use_APD && pb->confidence)
+        HIP_OK(ctx, hipMemcpyAsync(ctx->conf.p, pb->confidence, HW, hipMemcpyHostToDevice, s));
+    else
+        HIP_OK(ctx, hipMemsetAsync(ctx->conf.p, 1, HW, s));
+    int sa_any = 0;
+    if (pb->sa_mask) {
+        for (size_t i = 0; i < HW && !sa_any; ++i) sa_any = pb->sa_mask[i] != 0;
+    }
+    if (sa_any) HIP_OK(ctx, hipMemcpyAsync(ctx->sa.p, pb->sa_mask, HW, hipMemcpyHostToDevice, s));
+    else HIP_OK(ctx, hipMemsetAsync(ctx->sa.p, 0, HW, s));
+    HIP_OK(ctx, hipMemsetAsync(ctx->vw.p, 0, HW * N, s));
+    HIP_OK(ctx, hipMemsetAsync(ctx->cost.p, 0, HW * sizeof(float), s));
+    HIP_OK(ctx, hipMemsetAsync(ctx->sel.p, 0, HW * sizeof(uint32_t), s));
+    ctx->weak_count = weak_count;
+    if (P.use_APD) {
+        if ((st = ensure(ctx, ctx->amap, HW * sizeof(int)))) return st;
+        if ((st = ensure(ctx, ctx->anchors, (size_t)std::max(weak_count, 1) * 9 * sizeof(short2)))) return st;
+        if ((st = ensure(ctx, ctx->reliable, HW))) return st;
+        if ((st = ensure(ctx, ctx->nearest, HW * sizeof(short2)))) return st;
+        if ((st = ensure(ctx, ctx->fit, HW * sizeof(float4)))) return st;
+        HIP_OK(ctx, hipMemsetAsync(ctx->reliable.p, 0, HW, s));
+        HIP_OK(ctx, hipMemsetAsync(ctx->fit.p, 0, HW * sizeof(float4), s));
+        if ((st = build_near_offsets(ctx))) return st;
+    }
+    // kernel arguments
+    a.W = W; a.H = H; a.HW = (int)HW; a.N = N;
+    {
+        const int hh = H / 2;
+        const int rl = 32 * ((hh + 15) / 16);  // half-grid coverage of BLOCK_H=16 blocks (APD.cu:2676-2683)
+        a.row_limit = rl < H ? rl : H;
+    }
+    a.state = P.state;
+    a.dmin = P.depth_min; a.dmax = P.depth_max; a.gf = P.geom_factor; a.ransac_thr = P.ransac_threshold;
+    a.geom = P.geom_consistency != 0; a.impetus = P.use_impetus != 0; a.use_apd = P.use_APD != 0;
+    a.peak_radius = P.weak_peak_radius; a.rotate_time = P.rotate_time; a.sa_any = sa_any; a.top_k = P.top_k;
+    a.seed_lo = (uint32_t)pb->seed; a.seed_hi = (uint32_t)(pb->seed >> 32);
+    if (P.use_APD) {  // GenAnchors per-launch constants in double, as the reference (APD.cu:1897-1901)
+        const float angle = 45.0f / (float)P.rotate_time;
+        a.anc_cos = (float)cos((double)angle * 3.14159265358979323846 / 180.0f);
+        a.anc_sin = (float)sin((double)angle * 3.14159265358979323846 / 180.0f);
+        a.anc_thr = (float)cos((double)(angle / 2.0f) * 3.14159265358979323846 / 180.0f);
+        const int sr = (int)(tan((double)(angle / 2.0f) * 3.14159265358979323846 / 180.0f) * 20);
+        a.anc_shift = sr < 1 ? 1 : sr;
+    }
+    a.qstride = qstride;
+    a.ref = (const float *)ctx->imgs.p;
+    a.quad = (const float4 *)ctx->quad.p;
+    a.depth = need_depth ? (const float *)ctx->depth.p : nullptr;
+    a.views = (const SrcView *)ctx->views.p;
+    a.cams = (const Cam *)ctx->cams.p;
+    a.plane = (float4 *)ctx->plane.p;
+    a.cost = (float *)ctx->cost.p;
+    a.sel = (uint32_t *)ctx->sel.p;
+    a.vw = (uint8_t *)ctx->vw.p;
+    a.weak = (uint8_t *)ctx->weak.p;
+    a.conf = (uint8_t *)ctx->conf.p;
+    a.sa = (const uint8_t *)ctx->sa.p;
+    a.amap = P.use_APD ? (const int *)ctx->amap.p : nullptr;
+    a.anchors = P.use_APD ? (short2 *)ctx->anchors.p : nullptr;
+    a.reliable = P.use_APD ? (uint8_t *)ctx->reliable.p : nullptr;
+    a.nearest = P.use_APD ? (short2 *)ctx->nearest.p : nullptr;
+    a.fit = P.use_APD ? (float4 *)ctx->fit.p : nullptr;
+    a.near_offsets = P.use_APD ? (const short2 *)ctx->near_off.p : nullptr;
+    a.curve = nullptr;
+    // source images -> quad gather layout
+    {
+        const size_t total = qstride * N;
+        unsigned g = (unsigned)std::min<size_t>(blocks_for(total, BLOCK), 65535u * 8u);
+        hipLaunchKernelGGL(k_build_quads, dim3(g), dim3(BLOCK), 0, s, (const float *)ctx->imgs.p,
+                           (float4 *)ctx->quad.p, W, H, N, qstride);
+        if ((st = check_launch(ctx, "k_build_quads"))) return st;
+    }
+    ctx->params = P;
+    ctx->loaded = true;
+    return APD_OK;
+}
+
+// device-side ordered compaction of one pixel set
+static int build_list(apd_ctx *ctx, int mode, int colour, int *out, int *total_dev) {
+    Args &a = ctx->args;
+    hipStream_t s = ctx->stream;
+    hipLaunchKernelGGL(k_list_count, dim3(a.H), dim3(BLOCK), 0, s, a, mode, colour, (int *)ctx->rowcnt.p);
+    hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(1024), 0, s, (const int *)ctx->rowcnt.p, a.H, (int *)ctx->rowoff.p,
+                       total_dev);
+    hipLaunchKernelGGL(k_list_fill, dim3(a.H), dim3(BLOCK), 0, s, a, mode, colour, (const int *)ctx->rowoff.p, out);
+    return check_launch(ctx, "list build");
+}
+
+static int *list_ptr(apd_ctx *ctx, int which) {
+    // 4 lists share one HW-sized buffer: [strong black][strong red][weak black][weak red] are disjoint
+    // subsets of the pixels, so their concatenation never exceeds H*W entries.
+    int *base = (int *)ctx->lists.p;
+    size_t off = 0;
+    for (int i = 0; i < which; ++i) off += (size_t)ctx->cnt[i];
+    return base + off;
+}
+
+int32_t apd_stage_prepare(apd_ctx *ctx) {
+    if (!ctx || !ctx->loaded) return APD_ESTATE;
+    hipSetDevice(ctx->device);
+    Args &a = ctx->args;
+    hipStream_t s = ctx->stream;
+    const unsigned gpx = blocks_for((size_t)a.HW, BLOCK);
+    int st;
+    hipEventRecord(ctx->ev[0], s);
+    if (a.use_apd) {
+        // anchors_map from the input WEAK mask (APD.cpp:627-640)
+        if ((st = build_list(ctx, 2, 0, (int *)ctx->amap.p, (int *)ctx->totals.p + 4))) return st;
+        hipLaunchKernelGGL(k_find_nearest, dim3(gpx), dim3(BLOCK), 0, s, a, ctx->n_near);
+        hipLaunchKernelGGL(k_gen_anchors, dim3(gpx), dim3(BLOCK), 0, s, a);
+        hipLaunchKernelGGL(k_neighbour_update, dim3(gpx), dim3(BLOCK), 0, s, a);
+        if ((st = check_launch(ctx, "anchors"))) return st;
+    }
+    hipEventRecord(ctx->ev[1], s);
+    // pixel lists for the sweeps (after NeigbourUpdate)
+    {
+        int *tot = (int *)ctx->totals.p;
+        // counts first (lists are packed back to back), so build each list into a scratch region
+        // at the end of the shared buffer is unnecessary: compute counts, read them back, then fill.
+        const int modes[4][2] = {{0, 0}, {0, 1}, {1, 0}, {1, 1}};
+        for (int i = 0; i < 4; ++i) {
+            hipLaunchKernelGGL(k_list_count, dim3(a.H), dim3(BLOCK), 0, s, a, modes[i][0], modes[i][1],
+                               (int *)ctx->rowcnt.p);
+            hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(1024), 0, s, (const int *)ctx->rowcnt.p, a.H,
+                               (int *)ctx->rowoff.p, tot + i);
+        }
+        int host_tot[4];
+        HIP_OK(ctx, hipMemcpyAsync(host_tot, tot, 4 * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIP_OK(ctx, hipStreamSynchronize(s));
+        for (int i = 0; i < 4; ++i) ctx->cnt[i] = host_tot[i];
+        for (int i = 0; i < 4; ++i) {
+            if ((st = build_list(ctx, modes[i][0], modes[i][1], list_ptr(ctx, i), tot + i))) return st;
+        }
+    }
+    hipEventRecord(ctx->ev[2], s);
+    hipLaunchKernelGGL(k_random_init, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), 0, s, a);
+    if ((st = check_launch(ctx, "k_random_init"))) return st;
+    hipEventRecord(ctx->ev[3], s);
+    ctx->prepared = true;
+    return APD_OK;
+}
+
+int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
+    if (!ctx || !ctx->prepared) return APD_ESTATE;
+    hipSetDevice(ctx->device);
+    Args &a = ctx->args;
+    hipStream_t s = ctx->stream;
+    int st;
+    for (int colour = 0; colour < 2; ++colour) {
+        const int n = ctx->cnt[colour];
+        if (n <= 0) continue;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (ctx->prof) {
+            hipEventCreate(&e0);
+            hipEventCreate(&e1);
+            hipEventRecord(e0, s);
+        }
+        hipLaunchKernelGGL(k_sweep_strong, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
+                           (const int *)list_ptr(ctx, colour), n, iter);
+        if (ctx->prof) {
+            hipEventRecord(e1, s);
+            ctx->prof_ev.emplace_back(e0, e1);
+            ctx->prof_pixels += n;
+        }
+        if ((st = check_launch(ctx, "k_sweep_strong"))) return st;
+    }
+    if (a.use_apd) {
+        hipLaunchKernelGGL(k_ransac_fit, dim3(blocks_for((size_t)a.HW, BLOCK)), dim3(BLOCK), 0, s, a, iter);
+        for (int colour = 0; colour < 2; ++colour) {
+            const int n = ctx->cnt[2 + colour];
+            if (n <= 0) continue;
+            hipLaunchKernelGGL(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
+                               (const int *)list_ptr(ctx, 2 + colour), n, iter);
+        }
+        if ((st = check_launch(ctx, "weak sweep"))) return st;
+    }
+    return APD_OK;
+}
+
+int32_t apd_stage_finish(apd_ctx *ctx) {
+    if (!ctx || !ctx->prepared) return APD_ESTATE;
+    hipSetDevice(ctx->device);
+    Args a = ctx->args;
+    hipStream_t s = ctx->stream;
+    int st;
+    const unsigned gpx = blocks_for((size_t)a.HW, BLOCK);
+    hipLaunchKernelGGL(k_depth_normal, dim3(gpx), dim3(BLOCK), 0, s, a);
+    for (int colour = 0; colour < 2; ++colour) {
+        const int n = ctx->cnt[colour];
+        if (n > 0)
+            hipLaunchKernelGGL(k_filter, dim3(blocks_for((size_t)n, BLOCK)), dim3(BLOCK), 0, s, a,
+                               (const int *)list_ptr(ctx, colour), n);
+    }
+    if (ctx->want_curve && ctx->curve.p) a.curve = (float *)ctx->curve.p;
+    {
+        const int P = WAVE / a.N;
+        const size_t lds = (size_t)(BLOCK / WAVE) * P * 61 * sizeof(float);
+        hipLaunchKernelGGL(k_depth_to_weak, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), lds, s, a);
+    }
+    if (a.geom || a.use_apd) hipLaunchKernelGGL(k_confidence, dim3(gpx), dim3(BLOCK), 0, s, a);
+    hipLaunchKernelGGL(k_local_refine, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), 0, s, a);
+    if ((st = check_launch(ctx, "finish"))) return st;
+    return APD_OK;
+}
+
+int32_t apd_run_patchmatch(apd_ctx *ctx) {
+    if (!ctx || !ctx->loaded) return APD_ESTATE;
+    hipSetDevice(ctx->device);
+    int st;
+    hipStream_t s = ctx->stream;
+    if ((st = apd_stage_prepare(ctx))) return st;
+    const int iters = ctx->params.max_iterations;
+    for (int i = 0; i < iters; ++i) {
+        if (i < 8) hipEventRecord(ctx->ev[4 + i], s);
+        if ((st = apd_stage_iteration(ctx, i))) return st;
+    }
+    hipEventRecord(ctx->ev[12], s);
+    if ((st = apd_stage_finish(ctx))) return st;
+    hipEventRecord(ctx->ev[13], s);
+    HIP_OK(ctx, hipStreamSynchronize(s));
+    apd_timing &t = ctx->timing;
+    memset(&t, 0, sizeof(t));
+    hipEventElapsedTime(&t.total_ms, ctx->ev[0], ctx->ev[13]);
+    hipEventElapsedTime(&t.anchors_ms, ctx->ev[0], ctx->ev[1]);
+    hipEventElapsedTime(&t.init_ms, ctx->ev[2], ctx->ev[3]);
+    hipEventElapsedTime(&t.sweep_ms, ctx->ev[3], ctx->ev[12]);
+    hipEventElapsedTime(&t.post_ms, ctx->ev[12], ctx->ev[13]);
+    const int ni = std::min(iters, 8);
+    for (int i = 0; i < ni; ++i)
+        hipEventElapsedTime(&t.iter_ms[i], ctx->ev[4 + i], (i + 1 < ni) ? ctx->ev[5 + i] : ctx->ev[12]);
+    t.iterations = iters;
+    return APD_OK;
+}
+
+int32_t apd_synchronize(apd_ctx *ctx) {
+    if (!ctx) return APD_EINVAL;
+    hipSetDevice(ctx->device);
+    HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+    return APD_OK;
+}
+
+int32_t apd_get_results(apd_ctx *ctx, const apd_outputs *out) {
+    if (!ctx || !out) return APD_EINVAL;
+    if (!ctx->loaded) return APD_ESTATE;
+    hipSetDevice(ctx->device);
+    hipStream_t s = ctx->stream;
+    const Args &a = ctx->args;
+    const size_t HW = (size_t)a.HW;
+    if (out->planes) HIP_OK(ctx, hipMemcpyAsync(out->planes, ctx->plane.p, HW * sizeof(float4), hipMemcpyDeviceToHost, s));
+    if (out->weak_info) HIP_OK(ctx, hipMemcpyAsync(out->weak_info, ctx->weak.p, HW, hipMemcpyDeviceToHost, s));
+    if (out->confidence) HIP_OK(ctx, hipMemcpyAsync(out->confidence, ctx->conf.p, HW, hipMemcpyDeviceToHost, s));
+    if (out->costs) HIP_OK(ctx, hipMemcpyAsync(out->costs, ctx->cost.p, HW * sizeof(float), hipMemcpyDeviceToHost, s));
+    if (out->selected_views)
+        HIP_OK(ctx, hipMemcpyAsync(out->selected_views, ctx->sel.p, HW * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (out->view_weights) HIP_OK(ctx, hipMemcpyAsync(out->view_weights, ctx->vw.p, HW * a.N, hipMemcpyDeviceToHost, s));
+    if (out->anchors && a.use_apd && ctx->weak_count > 0)
+        HIP_OK(ctx, hipMemcpyAsync(out->anchors, ctx->anchors.p, (size_t)ctx->weak_count * 9 * sizeof(short2),
+                                   hipMemcpyDeviceToHost, s));
+    if (out->weak_count) *out->weak_count = ctx->weak_count;
+    HIP_OK(ctx, hipStreamSynchronize(s));
+    return APD_OK;
+}
+
+int32_t apd_get_timing(apd_ctx *ctx, apd_timing *timing) {
+    if (!ctx || !timing) return APD_EINVAL;
+    *timing = ctx->timing;
+    return APD_OK;
+}
+
+int32_t apd_profile_reset(apd_ctx *ctx, int32_t enable) {
+    if (!ctx) return APD_EINVAL;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    for (auto &pe : ctx->prof_ev) { hipEventDestroy(pe.first); hipEventDestroy(pe.second); }
+    ctx->prof_ev.clear();
+    ctx->prof_pixels = 0;
+    ctx->prof = enable != 0;
+    return APD_OK;
+}
+
+int32_t apd_profile_query(apd_ctx *ctx, double *sweep_ms_total, int64_t *sweep_launches, int64_t *sweep_pixels) {
+    if (!ctx) return APD_EINVAL;
+    hipSetDevice(ctx->device);
+    HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+    double tot = 0.0;
+    for (auto &pe : ctx->prof_ev) {
+        float ms = 0.0f;
+        hipEventElapsedTime(&ms, pe.first, pe.second);
+        tot += ms;
+    }
+    if (sweep_ms_total) *sweep_ms_total = tot;
+    if (sweep_launches) *sweep_launches = (int64_t)ctx->prof_ev.size();
+    if (sweep_pixels) *sweep_pixels = ctx->prof_pixels;
+    return APD_OK;
+}
+
+int32_t apd_epilogue(int32_t width, int32_t height, const float *planes, float depth_min, float depth_max,
+                     float *depth_out, float *normal_out, uint8_t *weak_inout) {
+    if (!planes || width < 1 || height < 1) return APD_EINVAL;
+    const size_t HW = (size_t)width * height;
+    for (size_t i = 0; i < HW; ++i) {
+        float d = planes[4 * i + 3];
+        if (d < depth_min || d > depth_max) {
+            d = 0;
+            if (weak_inout) weak_inout[i] = APD_UNKNOWN;
+        }
+        if (depth_out) depth_out[i] = d;
+        if (normal_out) {
+            normal_out[3 * i] = planes[4 * i];
+            normal_out[3 * i + 1] = planes[4 * i + 1];
+            normal_out[3 * i + 2] = planes[4 * i + 2];
+        }
+    }
+    return APD_OK;
+}
+
+}  // extern "C"

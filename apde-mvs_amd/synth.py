@@ -1,0 +1,243 @@
+"""Seeded synthetic piecewise-planar scenes in the MVSNet scan layout.
+
+Stands in for ETH3D / Tanks&Temples data, which are not available offline:
+a back wall, a floor and slanted boxes, each textured with band-limited noise, plus large
+constant-intensity patches that force WEAK (textureless) pixels. N+1 pinhole cameras with
+f = 0.8*W, principal point at the centre, sources on an arc with baselines of 5-15 % of the median
+depth looking at the scene centre. The scan layout (cams/%08d_cam.txt, images/, pair.txt) is the one
+tools/colmap2mvsnet.py:494-514 writes and APD.cpp:85-135 / main.cpp:44-102 read.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+
+@dataclass
+class Camera:
+    K: np.ndarray  # 3x3
+    R: np.ndarray  # 3x3 world->camera
+    t: np.ndarray  # 3
+    depth_min: float = 0.0
+    depth_max: float = 1.0
+    interval: float = 0.0
+    depth_num: float = 192.0
+
+    @property
+    def center(self) -> np.ndarray:
+        return -self.R.T @ self.t
+
+
+@dataclass
+class Scene:
+    width: int
+    height: int
+    images: list  # float32 HxW, values are integers 0..255
+    cameras: list  # Camera
+    gt_depth: list  # float32 HxW per view (0 = no surface)
+    labels: list  # uint8 HxW per view: plane id + 1 (SA mask stand-in)
+    pairs: list = field(default_factory=list)  # per view: list of (src_id, score)
+
+
+def _look_at(center, target, up=np.array([0.0, -1.0, 0.0])):
+    z = target - center
+    z = z / np.linalg.norm(z)
+    x = np.cross(z, up)
+    x = x / np.linalg.norm(x)
+    y = np.cross(z, x)
+    R = np.stack([x, y, z], axis=0)
+    t = -R @ center
+    return R, t
+
+
+class _Texture:
+    """Band-limited noise: a sum of random plane waves, evaluated at in-plane coordinates."""
+
+    def __init__(self, rng, n_waves=24, base_freq=6.0, flat_patches=()):
+        self.k = rng.normal(size=(n_waves, 2)) * base_freq
+        self.phase = rng.uniform(0, 2 * np.pi, size=n_waves)
+        self.amp = rng.uniform(0.4, 1.0, size=n_waves) / np.sqrt(n_waves)
+        self.flat = list(flat_patches)  # (u0, v0, u1, v1, value)
+        self.mean = rng.uniform(90, 160)
+        self.scale = rng.uniform(55, 80)
+
+    def __call__(self, u, v):
+        ph = u[..., None] * self.k[:, 0] + v[..., None] * self.k[:, 1] + self.phase
+        val = self.mean + self.scale * (np.sin(ph) * self.amp).sum(-1)
+        for (u0, v0, u1, v1, value) in self.flat:
+            m = (u >= u0) & (u <= u1) & (v >= v0) & (v <= v1)
+            val = np.where(m, value, val)
+        return val
+
+
+class _Quad:
+    """A bounded planar patch: origin + s*eu + t*ev, s,t in [0,1]."""
+
+    def __init__(self, origin, eu, ev, tex):
+        self.o = np.asarray(origin, float)
+        self.eu = np.asarray(eu, float)
+        self.ev = np.asarray(ev, float)
+        n = np.cross(self.eu, self.ev)
+        self.n = n / np.linalg.norm(n)
+        self.tex = tex
+        G = np.array([[self.eu @ self.eu, self.eu @ self.ev], [self.eu @ self.ev, self.ev @ self.ev]])
+        self.Ginv = np.linalg.inv(G)
+
+    def intersect(self, C, D):
+        """C: camera centre (3,), D: ray dirs (...,3). Returns t (inf where missed), s, r coords."""
+        den = D @ self.n
+        with np.errstate(divide="ignore", invalid="ignore"):
+            t = ((self.o - C) @ self.n) / den
+        P = C + t[..., None] * D
+        rel = P - self.o
+        b = np.stack([rel @ self.eu, rel @ self.ev], -1)
+        sr = b @ self.Ginv.T
+        s, r = sr[..., 0], sr[..., 1]
+        ok = (t > 1e-6) & (s >= 0) & (s <= 1) & (r >= 0) & (r <= 1) & np.isfinite(t)
+        return np.where(ok, t, np.inf), s * np.linalg.norm(self.eu), r * np.linalg.norm(self.ev)
+
+
+def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=True, depth=6.0) -> Scene:
+    rng = np.random.default_rng(seed)
+    f = 0.8 * width
+    K = np.array([[f, 0.0, width / 2.0], [0.0, f, height / 2.0], [0.0, 0.0, 1.0]])
+    # scene geometry in world coords (ref camera at origin looking along +z)
+    half_w = depth * (width / 2.0) / f * 1.6
+    half_h = depth * (height / 2.0) / f * 1.6
+    quads = []
+    flat = [(0.15 * half_w, 0.2 * half_h, 0.75 * half_w, 0.9 * half_h, 128.0)] if weak_patches else []
+    quads.append(_Quad([-half_w, -half_h, depth], [2 * half_w, 0, 0.35 * depth], [0, 2 * half_h, 0],
+                       _Texture(rng, base_freq=4.0, flat_patches=flat)))  # slanted back wall
+    quads.append(_Quad([-half_w, 0.55 * half_h, 0.45 * depth], [2 * half_w, 0, 0],
+                       [0, 0.45 * half_h, 0.9 * depth], _Texture(rng, base_freq=5.0)))  # floor
+    for b in range(3):
+        cx = rng.uniform(-0.6, 0.6) * half_w
+        cy = rng.uniform(-0.5, 0.3) * half_h
+        cz = rng.uniform(0.6, 0.85) * depth
+        sz = rng.uniform(0.15, 0.3) * half_w
+        ang = rng.uniform(-0.6, 0.6)
+        eu = np.array([np.cos(ang), 0, np.sin(ang)]) * sz
+        ev = np.array([0, 1.0, rng.uniform(-0.3, 0.3)]) * sz
+        bflat = [(0.1 * sz, 0.1 * sz, 0.7 * sz, 0.7 * sz, rng.uniform(60, 200))] if (weak_patches and b == 0) else []
+        quads.append(_Quad([cx, cy, cz], eu, ev, _Texture(rng, base_freq=7.0, flat_patches=bflat)))
+
+    # cameras: ref at origin, sources on an arc around the scene centre
+    target = np.array([0.0, 0.0, 0.8 * depth])
+    cams = [Camera(K.copy(), np.eye(3), np.zeros(3))]
+    for i in range(num_src):
+        ang = (i + 1) / (num_src + 1) * 2 * np.pi
+        base = rng.uniform(0.05, 0.15) * depth
+        C = np.array([np.cos(ang) * base, np.sin(ang) * base * 0.6, rng.uniform(-0.03, 0.03) * depth])
+        R, t = _look_at(C, target + rng.normal(size=3) * 0.02 * depth)
+        cams.append(Camera(K.copy(), R, t))
+
+    ys, xs = np.mgrid[0:height, 0:width].astype(np.float64)
+    pix = np.stack([xs, ys, np.ones_like(xs)], -1)
+    Kinv = np.linalg.inv(K)
+    images, depths, labels = [], [], []
+    for cam in cams:
+        Dc = pix @ Kinv.T  # camera-frame rays with z = 1
+        Dw = Dc @ cam.R  # R^T d
+        C = cam.center
+        best_t = np.full((height, width), np.inf)
+        val = np.zeros((height, width))
+        lab = np.zeros((height, width), np.uint8)
+        for qi, q in enumerate(quads):
+            t, s, r = q.intersect(C, Dw)
+            closer = t < best_t
+            if closer.any():
+                tv = q.tex(s, r)
+                val = np.where(closer, tv, val)
+                lab = np.where(closer, qi + 1, lab).astype(np.uint8)
+                best_t = np.where(closer, t, best_t)
+        hit = np.isfinite(best_t)
+        img = np.where(hit, val, 30.0)
+        img = np.clip(np.round(img), 0, 255).astype(np.float32)
+        images.append(img)
+        depths.append(np.where(hit, best_t, 0.0).astype(np.float32))  # ray z = 1 in camera frame
+        labels.append(lab)
+    valid = np.concatenate([d[d > 0] for d in depths])
+    dmin = float(np.percentile(valid, 1) * 0.75)
+    dmax = float(np.percentile(valid, 99) * 1.25)
+    for cam in cams:
+        cam.depth_min, cam.depth_max = dmin, dmax
+        cam.depth_num = 192.0
+        cam.interval = (dmax - dmin) / 192.0
+    nv = len(cams)
+    pairs = []
+    for i in range(nv):
+        others = [j for j in range(nv) if j != i]
+        dists = [np.linalg.norm(cams[i].center - cams[j].center) for j in others]
+        order = [others[k] for k in np.argsort(dists)]
+        pairs.append([(j, float(nv - r)) for r, j in enumerate(order)])
+    return Scene(width, height, images, cams, depths, labels, pairs)
+
+
+def camera_struct_values(cam: Camera, width: int, height: int):
+    """Field values of apd_camera / Camera (main.h:50-61), c computed as APD.cpp:114-119."""
+    R = cam.R.astype(np.float32)
+    t = cam.t.astype(np.float32)
+    c = np.array([-(float(np.float64(R[0, j]) * t[0] + np.float64(R[1, j]) * t[1] + np.float64(R[2, j]) * t[2]))
+                  for j in range(3)], np.float32)
+    return dict(K=cam.K.astype(np.float32).ravel(), R=R.ravel(), t=t, c=c, height=height, width=width,
+                depth_min=np.float32(cam.depth_min), depth_max=np.float32(cam.depth_max),
+                interval=np.float32(cam.interval), depth_num=np.float32(cam.depth_num))
+
+
+def write_scan(scene: Scene, folder: str, ext: str = ".pgm", write_masks: bool = False) -> None:
+    """Write the MVSNet scan layout read by the reference (APD.cpp:85-135, main.cpp:44-102)."""
+    os.makedirs(os.path.join(folder, "images"), exist_ok=True)
+    os.makedirs(os.path.join(folder, "cams"), exist_ok=True)
+    for i, (img, cam) in enumerate(zip(scene.images, scene.cameras)):
+        name = f"{i:08d}"
+        write_pgm(os.path.join(folder, "images", name + ext), img.astype(np.uint8))
+        with open(os.path.join(folder, "cams", name + "_cam.txt"), "w") as fh:
+            fh.write("extrinsic\n")
+            for r in range(3):
+                fh.write(" ".join(repr(float(v)) for v in cam.R[r]) + " " + repr(float(cam.t[r])) + "\n")
+            fh.write("0.0 0.0 0.0 1.0\n\nintrinsic\n")
+            for r in range(3):
+                fh.write(" ".join(repr(float(v)) for v in cam.K[r]) + "\n")
+            fh.write(f"\n{cam.depth_min!r} {cam.interval!r} {cam.depth_num!r} {cam.depth_max!r}\n")
+    with open(os.path.join(folder, "pair.txt"), "w") as fh:
+        fh.write(f"{len(scene.images)}\n")
+        for i, pl in enumerate(scene.pairs):
+            fh.write(f"{i}\n{len(pl)} " + " ".join(f"{j} {s}" for j, s in pl) + "\n")
+    if write_masks:
+        os.makedirs(os.path.join(folder, "sa_masks"), exist_ok=True)
+        for i, lab in enumerate(scene.labels):
+            write_bin_mat(os.path.join(folder, "sa_masks", f"{i:08d}.bin"), lab)
+
+
+def write_pgm(path: str, img_u8: np.ndarray) -> None:
+    h, w = img_u8.shape
+    with open(path, "wb") as fh:
+        fh.write(f"P5\n{w} {h}\n255\n".encode())
+        fh.write(np.ascontiguousarray(img_u8, np.uint8).tobytes())
+
+
+_CV_TYPES = {(np.dtype(np.uint8), 1): 0, (np.dtype(np.int32), 1): 4, (np.dtype(np.float32), 1): 5,
+             (np.dtype(np.float32), 3): 21}
+
+
+def write_bin_mat(path: str, mat: np.ndarray) -> None:
+    """WriteBinMat, APD.cpp:58-83: int32 version=1, rows, cols, cv type, raw row-major data."""
+    ch = 1 if mat.ndim == 2 else mat.shape[2]
+    cvt = _CV_TYPES[(mat.dtype, ch)]
+    with open(path, "wb") as fh:
+        np.array([1, mat.shape[0], mat.shape[1], cvt], np.int32).tofile(fh)
+        fh.write(np.ascontiguousarray(mat).tobytes())
+
+
+def read_bin_mat(path: str) -> np.ndarray:
+    """ReadBinMat, APD.cpp:18-56."""
+    with open(path, "rb") as fh:
+        hdr = np.frombuffer(fh.read(16), np.int32)
+        version, rows, cols, cvt = (int(v) for v in hdr)
+        if version != 1:
+            raise ValueError(f"bin-mat version {version} != 1: {path}")
+        dt, ch = {0: (np.uint8, 1), 4: (np.int32, 1), 5: (np.float32, 1), 21: (np.float32, 3)}[cvt]
+        data = np.frombuffer(fh.read(), dt)
+    return data.reshape((rows, cols) if ch == 1 else (rows, cols, ch)).copy()

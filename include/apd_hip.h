@@ -1,0 +1,205 @@
+/*
+ * apd_hip.h — C-ABI of the MI355X-native PatchMatch depth engine (libapd_hip.so).
+ *
+ * This is the drop-in boundary for the per-reference-view PatchMatch hot path of APDe-MVS.
+ * It replaces the in-process `class APD` lifecycle of the reference:
+ *
+ *   reference (APD.h:205-232, APD.cpp:458-842, APD.cu:2663-2737)     this ABI
+ *   ---------------------------------------------------------------  -----------------------------
+ *   APD::APD(const Problem&)                   APD.cpp:458             apd_create()
+ *   APD::InuputInitialization()                APD.cpp:501-685  \
+ *   APD::CudaSpaceInitialization()             APD.cpp:687-788   >     apd_set_problem()
+ *   APD::SetDataPassHelperInCuda()             APD.cpp:790-814  /
+ *   APD::RunPatchMatch()                       APD.cu:2663-2737        apd_run_patchmatch()
+ *   APD::GetPlaneHypothesis / GetPixelStates / GetConfidence
+ *                                              APD.cpp:816-826         apd_get_results()
+ *   APD::~APD()                                APD.cpp:463-499         apd_destroy()
+ *   CudaSafeCall / exit(EXIT_FAILURE)          APD.cpp:417-450         return codes + apd_last_error()
+ *
+ * Host-side file I/O (cv::imread, cv::resize, pair.txt / cam.txt parsing, bin-mat writing) stays
+ * outside the library, in the `apd` driver (apde-mvs_amd/host), exactly as it lives outside the
+ * CUDA kernels in the reference (APD.cpp:501-685, main.cpp).
+ *
+ * Conventions
+ *  - Plain C types only: pointers + sizes; no torch / HIP types in any signature.
+ *  - Images are H*W row-major float32 gray values (already resized to the pass resolution),
+ *    index 0 = reference view, 1..N = source views (N <= 31, MAX_IMAGES 32, main.h:40).
+ *  - Planes ("plane hypotheses") are float4 {x,y,z,w}: on input (init_planes) and output they are
+ *    {world-frame normal, depth} exactly like plane_hypotheses_host after GetDepthandNormal
+ *    (APD.cu:1694-1709, APD.cpp:661-683).
+ *  - Every entry point returns APD_OK (0) or a negative apd_status; it never calls exit().
+ *  - One apd_ctx per device; a ctx is bound to one HIP stream and is not thread-safe. Several ctxs
+ *    (one per GPU) may run concurrently from different threads / processes.
+ */
+#ifndef APD_HIP_H_
+#define APD_HIP_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define APD_ABI_VERSION 1
+#define APD_MAX_IMAGES 32          /* main.h:40  MAX_IMAGES            */
+#define APD_ANCHOR_NUM 9           /* main.h:41  ANCHOR_NUM            */
+#define APD_MAX_SEARCH_RADIUS 4096 /* main.h:42  MAX_SEARCH_RADIUS     */
+#define APD_CURVE_SAMPLES 61       /* main.h:45  RELIABLE_CURVE_SAMPLE_NUM */
+
+typedef enum apd_status {
+    APD_OK = 0,
+    APD_EINVAL = -1,          /* bad argument / unsupported parameter value            */
+    APD_ENOMEM = -2,          /* device or host allocation failed                      */
+    APD_EDEVICE = -3,         /* HIP runtime error (launch, copy, no device)           */
+    APD_ETOOMANYVIEWS = -4,   /* num_images > APD_MAX_IMAGES (APD.cpp:528-531 exits)    */
+    APD_ESTATE = -5           /* call out of lifecycle order (e.g. run before set)     */
+} apd_status;
+
+/* RunState, main.h:68-72 */
+enum { APD_FIRST_INIT = 0, APD_REFINE_INIT = 1, APD_REFINE_ITER = 2 };
+/* PixelState, main.h:74-78 */
+enum { APD_WEAK = 0, APD_STRONG = 1, APD_UNKNOWN = 2 };
+
+/* Byte-compatible with `struct Camera` (main.h:50-61): 120 bytes. */
+typedef struct apd_camera {
+    float K[9];
+    float R[9];
+    float t[3];
+    float c[3];           /* camera centre in world coords (APD.cpp:114-119) */
+    int32_t height;
+    int32_t width;
+    float depth_min;
+    float depth_max;
+    float interval;
+    float depth_num;
+} apd_camera;
+
+/* Mirrors `struct PatchMatchParams` (main.h:80-100). The reference's `bool` members are int32 here
+ * so the ABI has no implementation-defined layout. depth_min/depth_max are the *already scaled*
+ * range (cam.depth_min*0.6, cam.depth_max*1.2, APD.cpp:554-555). strong/weak radius/increment must
+ * be the reference defaults (5/2 and 5/5; main.cpp never changes them): the kernels are
+ * specialised for those window shapes and apd_set_problem rejects anything else with APD_EINVAL. */
+typedef struct apd_params {
+    int32_t max_iterations;   /* 3   */
+    int32_t num_images;       /* ref + src, <= 32 */
+    int32_t top_k;            /* 4   */
+    float depth_min;
+    float depth_max;
+    int32_t geom_consistency; /* bool */
+    int32_t use_impetus;      /* bool */
+    int32_t strong_radius;    /* 5   */
+    int32_t strong_increment; /* 2   */
+    int32_t weak_radius;      /* 5   */
+    int32_t weak_increment;   /* 5   */
+    int32_t use_APD;          /* bool */
+    int32_t use_sa;           /* bool (host-side only: decides whether sa_mask is passed) */
+    int32_t weak_peak_radius; /* 2..6 */
+    int32_t rotate_time;      /* 1, 2 or 4 */
+    float ransac_threshold;
+    float geom_factor;        /* 0.2 ETH/DTU/General, 0.05 TaT (main.cpp:293-299) */
+    int32_t state;            /* APD_FIRST_INIT / APD_REFINE_INIT / APD_REFINE_ITER */
+} apd_params;
+
+/* One Problem (main.h:102-115) at its pass resolution, with every input the reference reads in
+ * InuputInitialization (APD.cpp:501-685), already decoded/resized by the host. */
+typedef struct apd_problem {
+    int32_t width;
+    int32_t height;
+    int32_t num_images;                /* ref + src                                          */
+    const float *const *images;        /* [num_images] -> H*W float32                         */
+    const apd_camera *cameras;         /* [num_images], K already scaled (APD.cpp:580-585)    */
+    apd_params params;
+    /* geom_consistency || use_APD: [num_images] -> H*W depth maps (index 0 = own prior),
+       already resized INTER_NEAREST (APD.cpp:592-610). NULL otherwise. */
+    const float *const *depths;
+    /* state != FIRST_INIT: H*W*4 floats {world normal xyz, depth} (APD.cpp:661-683). */
+    const float *init_planes;
+    /* use_APD: H*W PixelState bytes and confidence bytes (APD.cpp:614-626); NULL otherwise
+       (then every pixel is STRONG and confidence 1, APD.cpp:655-658). */
+    const uint8_t *weak_info;
+    const uint8_t *confidence;
+    /* use_APD && use_sa && mask present: H*W segment labels (APD.cpp:641-652); NULL = all 0. */
+    const uint8_t *sa_mask;
+    /* Deterministic RNG contract (replaces curand_init(clock64(),...), APD.cu:904-917). */
+    uint64_t seed;
+} apd_problem;
+
+/* Caller-allocated outputs (D2H of APD.cu:2731-2736). Any pointer may be NULL to skip it. */
+typedef struct apd_outputs {
+    float *planes;             /* H*W*4: {world normal xyz, depth} (after GetDepthandNormal, filter, LocalRefine) */
+    uint8_t *weak_info;        /* H*W PixelState after DepthToWeak / ConfidenceCompute */
+    uint8_t *confidence;       /* H*W (valid iff geom_consistency || use_APD)         */
+    float *costs;              /* H*W final matching cost                            */
+    uint32_t *selected_views;  /* H*W view bitmask                                   */
+    uint8_t *view_weights;     /* N*H*W (view-major) sampled view weights, N = num_images-1 */
+    int16_t *anchors;          /* weak_count*9*2 (x,y) anchors, APD.cu:2614-2626 export   */
+    int32_t *weak_count;       /* out: number of WEAK pixels in the input weak_info       */
+    float *reliable_curve;     /* H*W*61 DepthToWeak cost curves (APD.cu:2188-2198), optional */
+} apd_outputs;
+
+/* Device-time breakdown of the last apd_run_patchmatch (HIP events on the ctx stream), ms. */
+typedef struct apd_timing {
+    float total_ms;            /* whole RunPatchMatch bracket (main.cpp:157-159 equivalent) */
+    float init_ms;             /* RandomInitialization                                     */
+    float anchors_ms;          /* FindNearestStrongPoint + GenAnchors + NeigbourUpdate      */
+    float sweep_ms;            /* all sweep iterations (Strong + RANSAC fit + Weak)         */
+    float post_ms;             /* GetDepthandNormal + filter + DepthToWeak + Confidence + LocalRefine */
+    float iter_ms[8];          /* per-iteration sweep time (first 8 iterations)             */
+    int32_t iterations;
+} apd_timing;
+
+typedef struct apd_ctx apd_ctx;
+
+/* Library / device queries. */
+int32_t apd_abi_version(void);
+int32_t apd_device_count(void);
+
+/* apd_create: bind a new context to HIP device `device` (cudaSetDevice, main.cpp:264). Returns
+   NULL on failure; the reason is available from apd_last_error(NULL). */
+apd_ctx *apd_create(int32_t device);
+void apd_destroy(apd_ctx *ctx);
+const char *apd_last_error(const apd_ctx *ctx);
+
+/* Upload one problem: images (plus the LDS/quad gather layout built on device), cameras, priors,
+   masks, params. Device buffers are reused across problems of the same or smaller size. */
+int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *problem);
+
+/* Run the full RunPatchMatch kernel sequence (APD.cu:2663-2737) on the loaded problem. */
+int32_t apd_run_patchmatch(apd_ctx *ctx);
+
+/* Fine-grained stages of the same sequence, for benchmarking the per-iteration metric:
+   apd_stage_prepare = InitRandomStates..RandomInitialization (APD.cu:2685-2697);
+   apd_stage_iteration(i) = loop body i (APD.cu:2700-2707);
+   apd_stage_finish = GetDepthandNormal..LocalRefine (APD.cu:2710-2729).
+   prepare + iteration(0..max_iterations-1) + finish == apd_run_patchmatch. */
+int32_t apd_stage_prepare(apd_ctx *ctx);
+int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter);
+int32_t apd_stage_finish(apd_ctx *ctx);
+
+/* Block until every launch on the ctx stream completed. */
+int32_t apd_synchronize(apd_ctx *ctx);
+
+/* Copy results to host (GetPlaneHypothesis/GetPixelStates/GetConfidence, APD.cpp:816-826). */
+int32_t apd_get_results(apd_ctx *ctx, const apd_outputs *out);
+
+/* Device timing of the last apd_run_patchmatch. */
+int32_t apd_get_timing(apd_ctx *ctx, apd_timing *timing);
+
+/* Average duration (ms) of the dominant kernel (the Strong checkerboard sweep) over the launches
+   since the last reset, measured with HIP events on the ctx stream; and the algorithmic NCC
+   sample count those launches processed. Used by bench.py for roofline.achieved. */
+int32_t apd_profile_reset(apd_ctx *ctx, int32_t enable);
+int32_t apd_profile_query(apd_ctx *ctx, double *sweep_ms_total, int64_t *sweep_launches,
+                          int64_t *sweep_pixels);
+
+/* Host epilogue of ProcessProblem (main.cpp:168-178): depth = plane.w clipped to
+   [depth_min, depth_max] (else 0 and PixelState UNKNOWN), normal = plane.xyz. Pure host code. */
+int32_t apd_epilogue(int32_t width, int32_t height, const float *planes, float depth_min,
+                     float depth_max, float *depth_out, float *normal_out, uint8_t *weak_inout);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* APD_HIP_H_ */

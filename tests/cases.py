@@ -1,0 +1,125 @@
+"""Seeded parity cases shared by the CPU (oracle/golden) and GPU (HIP vs oracle) tests.
+
+Every case is a small synthetic scene (≤160x120, N≤8) so the oracle finishes in seconds. The
+prior-dependent states (REFINE_INIT / REFINE_ITER, geometric consistency, APD anchors, SA masks)
+take their priors from an oracle FIRST_INIT pass over the neighbouring views, exactly the data flow
+of main.cpp:306-367 (depths.bin / normals.bin / weak.bin / confidence.bin of the previous pass).
+"""
+from __future__ import annotations
+
+import functools
+
+import numpy as np
+
+import apd_abi as A
+import synth
+
+
+@functools.lru_cache(maxsize=None)
+def scene(w=160, h=120, n_src=4, seed=20251114, weak=True):
+    return synth.make_scene(w, h, n_src, seed=seed, weak_patches=weak)
+
+
+def base_problem(sc, ref=0, n_src=None, **params):
+    srcs = [j for j, _ in sc.pairs[ref]]
+    if n_src is not None:
+        srcs = srcs[:n_src]
+    arr = A.scene_problem(sc, ref, srcs)
+    for k, v in params.items():
+        setattr(arr.params, k, v)
+    return arr
+
+
+def first_pass(oracle_run, sc, n_src=None):
+    """Oracle FIRST_INIT pass over every view -> per-view (planes, weak, conf) after the epilogue."""
+    outs = []
+    for ref in range(len(sc.images)):
+        arr = base_problem(sc, ref, n_src)
+        out = oracle_run(arr)
+        outs.append(out)
+    return outs
+
+
+def epilogue(out, dmin, dmax):
+    """ProcessProblem's host epilogue (main.cpp:168-178)."""
+    planes = out.planes
+    d = planes[..., 3].copy()
+    weak = out.weak_info.copy()
+    bad = (d < dmin) | (d > dmax)
+    d[bad] = 0
+    weak[bad] = A.UNKNOWN
+    return d, planes[..., :3].copy(), weak
+
+
+def refine_problem(sc, priors, ref=0, n_src=None, state=A.REFINE_ITER, geom=True, apd=False, sa=False,
+                   **params):
+    """A REFINE_* problem for view `ref` whose priors come from `priors` (list of oracle outputs)."""
+    arr = base_problem(sc, ref, n_src)
+    ids = [ref] + [j for j, _ in sc.pairs[ref]][: (len(arr.images) - 1)]
+    dmin, dmax = arr.params.depth_min, arr.params.depth_max
+    deps = []
+    for i in ids:
+        d, _, _ = epilogue(priors[i], dmin, dmax)
+        deps.append(d)
+    d0, n0, w0 = epilogue(priors[ref], dmin, dmax)
+    planes = np.concatenate([n0, d0[..., None]], -1).astype(np.float32)
+    arr.depths = deps
+    arr.init_planes = planes
+    arr.params.state = state
+    arr.params.geom_consistency = int(geom)
+    arr.params.use_APD = int(apd)
+    if apd:
+        arr.weak_info = w0
+        arr.confidence = priors[ref].confidence.copy()
+        arr.params.rotate_time = 2
+        arr.params.ransac_threshold = 0.01 - 1 * 0.00125
+    if sa:
+        arr.sa_mask = sc.labels[ref].copy()
+    for k, v in params.items():
+        setattr(arr.params, k, v)
+    return arr
+
+
+CASES = {
+    # name: (w, h, n_src, kind)
+    "first_n4": (160, 120, 4, "first"),
+    "first_n8": (128, 96, 8, "first"),
+    "first_n3_odd": (96, 65, 3, "first"),      # odd H with H/2 % 16 == 0: last row never swept
+    "first_n1": (64, 48, 1, "first"),
+    "refine_iter_geom": (128, 96, 4, "geom"),
+    "refine_init_apd": (128, 96, 4, "apd"),
+    "refine_iter_apd_geom_sa": (128, 96, 4, "apd_geom_sa"),
+}
+
+
+def make_case(name, oracle_run):
+    w, h, n, kind = CASES[name]
+    sc = scene(w, h, max(n, 4))
+    if kind == "first":
+        return base_problem(sc, 0, n)
+    priors = first_pass(oracle_run, sc, n)
+    if kind == "geom":
+        return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True)
+    if kind == "apd":
+        return refine_problem(sc, priors, 0, n, state=A.REFINE_INIT, geom=False, apd=True)
+    if kind == "apd_geom_sa":
+        return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, sa=True)
+    raise KeyError(kind)
+
+
+FIELDS = ("planes", "costs", "weak_info", "confidence", "selected_views", "view_weights")
+
+
+def compare(a, b, fields=FIELDS):
+    """Bit-level comparison; returns {field: number of differing elements} (NaN == NaN)."""
+    diffs = {}
+    for f in fields:
+        x, y = getattr(a, f), getattr(b, f)
+        if x.dtype.kind == "f":
+            xb = x.view(np.uint32)
+            yb = y.view(np.uint32)
+            same = (xb == yb) | (np.isnan(x) & np.isnan(y))
+        else:
+            same = x == y
+        diffs[f] = int((~same).sum())
+    return diffs
