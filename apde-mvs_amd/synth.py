@@ -53,23 +53,47 @@ def _look_at(center, target, up=np.array([0.0, -1.0, 0.0])):
 
 
 class _Texture:
-    """Band-limited noise: a sum of random plane waves, evaluated at in-plane coordinates."""
+    """Band-limited noise: a seeded FFT-filtered tileable noise image, sampled bilinearly (wrap) at
+    in-plane coordinates, so every view sees the same surface texture."""
 
-    def __init__(self, rng, n_waves=24, base_freq=6.0, flat_patches=()):
-        self.k = rng.normal(size=(n_waves, 2)) * base_freq
-        self.phase = rng.uniform(0, 2 * np.pi, size=n_waves)
-        self.amp = rng.uniform(0.4, 1.0, size=n_waves) / np.sqrt(n_waves)
+    SIZE = 512
+
+    def __init__(self, rng, base_freq=6.0, flat_patches=()):
+        n = self.SIZE
+        white = rng.normal(size=(n, n))
+        fy = np.fft.fftfreq(n)[:, None]
+        fx = np.fft.fftfreq(n)[None, :]
+        band = np.exp(-((np.hypot(fx, fy) * n / 24.0) ** 2))  # keep ~24 cycles per tile
+        tex = np.real(np.fft.ifft2(np.fft.fft2(white) * band))
+        self.tex = (tex / tex.std()).astype(np.float32)
+        self.k = base_freq * n / 24.0 / (2 * np.pi) * 2.0  # texels per world unit
         self.flat = list(flat_patches)  # (u0, v0, u1, v1, value)
         self.mean = rng.uniform(90, 160)
-        self.scale = rng.uniform(55, 80)
+        self.scale = rng.uniform(28, 40)
 
     def __call__(self, u, v):
-        ph = u[..., None] * self.k[:, 0] + v[..., None] * self.k[:, 1] + self.phase
-        val = self.mean + self.scale * (np.sin(ph) * self.amp).sum(-1)
+        """Returns (value, flat_mask): flat_mask marks the textureless patches."""
+        n = self.SIZE
+        x = u * self.k
+        y = v * self.k
+        x0 = np.floor(x)
+        y0 = np.floor(y)
+        ax = x - x0
+        ay = y - y0
+        x0 = x0.astype(np.int64) % n
+        y0 = y0.astype(np.int64) % n
+        x1 = (x0 + 1) % n
+        y1 = (y0 + 1) % n
+        T = self.tex
+        top = T[y0, x0] * (1 - ax) + T[y0, x1] * ax
+        bot = T[y1, x0] * (1 - ax) + T[y1, x1] * ax
+        val = self.mean + self.scale * (top * (1 - ay) + bot * ay)
+        flat = np.zeros(val.shape, bool)
         for (u0, v0, u1, v1, value) in self.flat:
             m = (u >= u0) & (u <= u1) & (v >= v0) & (v <= v1)
             val = np.where(m, value, val)
-        return val
+            flat |= m
+        return val, flat
 
 
 class _Quad:
@@ -85,16 +109,21 @@ class _Quad:
         G = np.array([[self.eu @ self.eu, self.eu @ self.ev], [self.eu @ self.ev, self.ev @ self.ev]])
         self.Ginv = np.linalg.inv(G)
 
-    def intersect(self, C, D):
-        """C: camera centre (3,), D: ray dirs (...,3). Returns t (inf where missed), s, r coords."""
-        den = D @ self.n
+    def intersect(self, C, M, xs, ys):
+        """Ray cast for pixel rays D(x,y) = M @ (x, y, 1) from centre C. Every dot product of D is
+        affine in (x, y), so the whole image is built from broadcast row/column vectors.
+        Returns t (inf where missed) and in-plane coordinates (u, v)."""
+        def lin(vec):
+            w = M.T @ vec
+            return w[0] * xs[None, :] + w[1] * ys[:, None] + w[2]
+
         with np.errstate(divide="ignore", invalid="ignore"):
-            t = ((self.o - C) @ self.n) / den
-        P = C + t[..., None] * D
-        rel = P - self.o
-        b = np.stack([rel @ self.eu, rel @ self.ev], -1)
-        sr = b @ self.Ginv.T
-        s, r = sr[..., 0], sr[..., 1]
+            t = ((self.o - C) @ self.n) / lin(self.n)
+        rel0 = C - self.o
+        b0 = rel0 @ self.eu + t * lin(self.eu)
+        b1 = rel0 @ self.ev + t * lin(self.ev)
+        s = self.Ginv[0, 0] * b0 + self.Ginv[0, 1] * b1
+        r = self.Ginv[1, 0] * b0 + self.Ginv[1, 1] * b1
         ok = (t > 1e-6) & (s >= 0) & (s <= 1) & (r >= 0) & (r <= 1) & np.isfinite(t)
         return np.where(ok, t, np.inf), s * np.linalg.norm(self.eu), r * np.linalg.norm(self.ev)
 
@@ -107,7 +136,7 @@ def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=Tru
     half_w = depth * (width / 2.0) / f * 1.6
     half_h = depth * (height / 2.0) / f * 1.6
     quads = []
-    flat = [(0.15 * half_w, 0.2 * half_h, 0.75 * half_w, 0.9 * half_h, 128.0)] if weak_patches else []
+    flat = [(0.68 * half_w, 0.25 * half_h, 1.2 * half_w, 1.1 * half_h, 128.0)] if weak_patches else []
     quads.append(_Quad([-half_w, -half_h, depth], [2 * half_w, 0, 0.35 * depth], [0, 2 * half_h, 0],
                        _Texture(rng, base_freq=4.0, flat_patches=flat)))  # slanted back wall
     quads.append(_Quad([-half_w, 0.55 * half_h, 0.45 * depth], [2 * half_w, 0, 0],
@@ -133,26 +162,35 @@ def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=Tru
         R, t = _look_at(C, target + rng.normal(size=3) * 0.02 * depth)
         cams.append(Camera(K.copy(), R, t))
 
-    ys, xs = np.mgrid[0:height, 0:width].astype(np.float64)
-    pix = np.stack([xs, ys, np.ones_like(xs)], -1)
+    xs = np.arange(width, dtype=np.float64)
+    ys = np.arange(height, dtype=np.float64)
     Kinv = np.linalg.inv(K)
     images, depths, labels = [], [], []
     for cam in cams:
-        Dc = pix @ Kinv.T  # camera-frame rays with z = 1
-        Dw = Dc @ cam.R  # R^T d
+        M = cam.R.T @ Kinv  # world-frame ray of pixel (x, y) with camera-frame z = 1
         C = cam.center
         best_t = np.full((height, width), np.inf)
-        val = np.zeros((height, width))
-        lab = np.zeros((height, width), np.uint8)
+        best_q = np.full((height, width), -1, np.int64)
+        hits = []
         for qi, q in enumerate(quads):
-            t, s, r = q.intersect(C, Dw)
+            t, s, r = q.intersect(C, M, xs, ys)
             closer = t < best_t
-            if closer.any():
-                tv = q.tex(s, r)
-                val = np.where(closer, tv, val)
-                lab = np.where(closer, qi + 1, lab).astype(np.uint8)
-                best_t = np.where(closer, t, best_t)
+            best_t = np.where(closer, t, best_t)
+            best_q = np.where(closer, qi, best_q)
+            hits.append((s, r))
+        val = np.zeros((height, width))
+        flat = np.zeros((height, width), bool)
+        for qi, q in enumerate(quads):
+            m = best_q == qi
+            if m.any():
+                tv, tf = q.tex(hits[qi][0][m], hits[qi][1][m])
+                val[m] = tv
+                flat[m] = tf
+        lab = (best_q + 1).astype(np.uint8)
         hit = np.isfinite(best_t)
+        # textureless patches: constant albedo + per-view sensor noise (uncorrelated across views, so
+        # NCC cannot lock on and DepthToWeak classifies them WEAK, APD.cu:2220-2249)
+        val = np.where(flat, val + rng.normal(0.0, 2.0, size=val.shape), val)
         img = np.where(hit, val, 30.0)
         img = np.clip(np.round(img), 0, 255).astype(np.float32)
         images.append(img)
