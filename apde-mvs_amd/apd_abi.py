@@ -53,7 +53,8 @@ class ApdProblem(C.Structure):
                 ("images", C.POINTER(C.POINTER(C.c_float))), ("cameras", C.POINTER(ApdCamera)),
                 ("params", ApdParams), ("depths", C.POINTER(C.POINTER(C.c_float))),
                 ("init_planes", C.POINTER(C.c_float)), ("weak_info", C.POINTER(C.c_uint8)),
-                ("confidence", C.POINTER(C.c_uint8)), ("sa_mask", C.POINTER(C.c_uint8)), ("seed", C.c_uint64)]
+                ("confidence", C.POINTER(C.c_uint8)), ("sa_mask", C.POINTER(C.c_uint8)), ("seed", C.c_uint64),
+                ("export_reliable_curve", C.c_int32)]
 
 
 class ApdOutputs(C.Structure):
@@ -101,6 +102,7 @@ class ProblemArrays:
     confidence: Optional[np.ndarray] = None
     sa_mask: Optional[np.ndarray] = None
     seed: int = 0x5EED
+    export_reliable_curve: bool = False
 
     def build(self) -> ApdProblem:
         n = len(self.images)
@@ -137,6 +139,7 @@ class ProblemArrays:
         pb.confidence = _ptr(self._conf, C.c_uint8)
         pb.sa_mask = _ptr(self._sa, C.c_uint8)
         pb.seed = self.seed
+        pb.export_reliable_curve = int(self.export_reliable_curve)
         self._pb = pb
         return pb
 

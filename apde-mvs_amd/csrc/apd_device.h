@@ -18,6 +18,14 @@
 #define APD_FLT_EPSILON 1.19209290e-07f
 #define APD_FLT_MAX 3.40282347e+38f
 
+// Device pointers live in the global address space: without the qualifier every load through a
+// struct member is a FLAT load (no scalar path, waits on both vmcnt and lgkmcnt).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define APD_G __attribute__((address_space(1)))
+#else
+#define APD_G
+#endif
+
 namespace apd {
 
 // launch ordinals of the RNG contract (identical to the oracle)
@@ -47,25 +55,27 @@ struct Args {
     float anc_cos, anc_sin, anc_thr;       // GenAnchors per-launch constants (APD.cu:1897-1901)
     int anc_shift;
     size_t qstride;                        // float4 elements per source quad image ((W+1)*(H+1))
-    const float *__restrict__ ref;         // reference image, H*W
-    const float4 *__restrict__ quad;       // source images 1..N in quad layout, view v at (v-1)*qstride
-    const float *__restrict__ depth;       // [N+1][H*W] depth maps (geom / APD)
-    const SrcView *__restrict__ views;     // [N+1]
-    const Cam *__restrict__ cams;          // [N+1]
-    float4 *plane;
-    float *cost;
-    uint32_t *sel;
-    uint8_t *vw;                           // view-major [N][H*W]
-    uint8_t *weak;
-    uint8_t *conf;
-    const uint8_t *sa;
-    const int *amap;
-    short2 *anchors;                       // weak_count*9
-    uint8_t *reliable;
-    short2 *nearest;
-    float4 *fit;
-    float *curve;                          // optional H*W*61
-    const short2 *near_offsets;            // 201*201 offsets sorted by (d^2, x, y)
+    const APD_G float *ref;                // reference image, H*W
+    const APD_G float4 *quad;              // source images 1..N in quad layout, view v at (v-1)*qstride
+    const APD_G float *depth;              // [N+1][H*W] depth maps (geom / APD)
+    const APD_G SrcView *views;            // [N+1]
+    const APD_G Cam *cams;                 // [N+1]
+    APD_G float4 *plane;
+    APD_G float *cost;
+    APD_G uint32_t *sel;
+    APD_G uint32_t *sel_next;              // RandomInitialization output (launch-start snapshot of sel)
+    APD_G uint8_t *vw;                     // view-major [N][H*W]
+    APD_G uint8_t *weak;
+    APD_G uint8_t *conf;
+    const APD_G uint8_t *sa;
+    const APD_G int *amap;
+    APD_G short2 *anchors;                 // weak_count*9
+    APD_G uint8_t *reliable;
+    APD_G short2 *nearest;
+    APD_G float4 *fit;
+    APD_G float *curve;                    // optional H*W*61
+    const APD_G short2 *near_offsets;      // 201*201 offsets sorted by (d^2, x, y)
+    const APD_G struct Args *self;         // this struct in device memory, for out-of-line callees
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -160,27 +170,27 @@ __device__ __forceinline__ void normalize2(float &x, float &y) {
     float inv = 1.0f / sqrtf(ns);
     x *= inv; y *= inv;
 }
-__device__ __forceinline__ void get3d(const Cam &c, float px, float py, float depth, float X[3]) {
+__device__ __forceinline__ void get3d(const APD_G Cam &c, float px, float py, float depth, float X[3]) {
     X[0] = depth * (px - c.K[2]) / c.K[0];
     X[1] = depth * (py - c.K[5]) / c.K[4];
     X[2] = depth;
 }
-__device__ __forceinline__ float4 view_dir(const Cam &c, int px, int py, float depth) {
+__device__ __forceinline__ float4 view_dir(const APD_G Cam &c, int px, int py, float depth) {
     float X[3];
     get3d(c, (float)px, (float)py, depth, X);
     float norm = sqrtf(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
     return make_float4(X[0] / norm, X[1] / norm, X[2] / norm, 0.0f);
 }
-__device__ __forceinline__ float dist2origin(const Cam &c, int px, int py, float depth, float4 n) {
+__device__ __forceinline__ float dist2origin(const APD_G Cam &c, int px, int py, float depth, float4 n) {
     float X[3];
     get3d(c, (float)px, (float)py, depth, X);
     return -(n.x * X[0] + n.y * X[1] + n.z * X[2]);
 }
-__device__ __forceinline__ float depth_from_plane(const Cam &c, float4 pl, int px, int py) {
+__device__ __forceinline__ float depth_from_plane(const APD_G Cam &c, float4 pl, int px, int py) {
     return -pl.w * c.K[0] /
            (((float)px - c.K[2]) * pl.x + (c.K[0] / c.K[4]) * ((float)py - c.K[5]) * pl.y + c.K[0] * pl.z);
 }
-__device__ __forceinline__ float4 random_normal(const Cam &c, int px, int py, Rng &g, float depth) {
+__device__ __forceinline__ float4 random_normal(const APD_G Cam &c, int px, int py, Rng &g, float depth) {
     float q1 = 1.0f, q2 = 1.0f, s = 2.0f;
     while (s >= 1.0f) {
         q1 = 2.0f * g.uniform() - 1.0f;
@@ -195,7 +205,7 @@ __device__ __forceinline__ float4 random_normal(const Cam &c, int px, int py, Rn
     normalize3(n);
     return n;
 }
-__device__ __forceinline__ float4 perturbed_normal(const Cam &c, int px, int py, float4 n, Rng &g, float pert) {
+__device__ __forceinline__ float4 perturbed_normal(const APD_G Cam &c, int px, int py, float4 n, Rng &g, float pert) {
     float4 vd = view_dir(c, px, py, 1.0f);
     float a1 = (g.uniform() - 0.5f) * pert;
     float a2 = (g.uniform() - 0.5f) * pert;
@@ -217,15 +227,15 @@ __device__ __forceinline__ float4 perturbed_normal(const Cam &c, int px, int py,
     normalize3(p);
     return p;
 }
-__device__ __forceinline__ float4 to_world(const Cam &c, float4 p) {
+__device__ __forceinline__ float4 to_world(const APD_G Cam &c, float4 p) {
     return make_float4(c.R[0] * p.x + c.R[3] * p.y + c.R[6] * p.z, c.R[1] * p.x + c.R[4] * p.y + c.R[7] * p.z,
                        c.R[2] * p.x + c.R[5] * p.y + c.R[8] * p.z, p.w);
 }
-__device__ __forceinline__ float4 to_ref(const Cam &c, float4 p) {
+__device__ __forceinline__ float4 to_ref(const APD_G Cam &c, float4 p) {
     return make_float4(c.R[0] * p.x + c.R[1] * p.y + c.R[2] * p.z, c.R[3] * p.x + c.R[4] * p.y + c.R[5] * p.z,
                        c.R[6] * p.x + c.R[7] * p.y + c.R[8] * p.z, p.w);
 }
-__device__ __forceinline__ void world_point(const Cam &c, float x, float y, float depth, float P[3]) {
+__device__ __forceinline__ void world_point(const APD_G Cam &c, float x, float y, float depth, float P[3]) {
     float X0 = depth * (x - c.K[2]) / c.K[0];
     float X1 = depth * (y - c.K[5]) / c.K[4];
     float X2 = depth;
@@ -234,7 +244,7 @@ __device__ __forceinline__ void world_point(const Cam &c, float x, float y, floa
     float t2 = c.R[2] * X0 + c.R[5] * X1 + c.R[8] * X2;
     P[0] = t0 + c.c[0]; P[1] = t1 + c.c[1]; P[2] = t2 + c.c[2];
 }
-__device__ __forceinline__ void project_cam(const float P[3], const Cam &c, float &px, float &py, float &d) {
+__device__ __forceinline__ void project_cam(const float P[3], const APD_G Cam &c, float &px, float &py, float &d) {
     float t0 = c.R[0] * P[0] + c.R[1] * P[1] + c.R[2] * P[2] + c.t[0];
     float t1 = c.R[3] * P[0] + c.R[4] * P[1] + c.R[5] * P[2] + c.t[1];
     float t2 = c.R[6] * P[0] + c.R[7] * P[1] + c.R[8] * P[2] + c.t[2];
@@ -255,13 +265,14 @@ __device__ __forceinline__ int trunc_clamp(float x, int n) {
 // ---------------------------------------------------------------------------------------------
 struct Hom { float h[9]; };
 
-__device__ __forceinline__ Hom homography(const Args &a, int s, float4 pl) {
+template <class AT>
+__device__ __forceinline__ Hom homography(const AT &a, int s, float4 pl) {
     float m0 = pl.x * a.ikx;
     float m1 = pl.y * a.iky;
     float m2 = fmaf(-pl.y, a.cyk, fmaf(-pl.x, a.cxk, pl.z));
     float iw = 1.0f / pl.w;
     m0 *= iw; m1 *= iw; m2 *= iw;
-    const SrcView &V = a.views[s];
+    const APD_G SrcView &V = a.views[s];
     Hom H;
     H.h[0] = fmaf(-V.b[0], m0, V.A[0]); H.h[1] = fmaf(-V.b[0], m1, V.A[1]); H.h[2] = fmaf(-V.b[0], m2, V.A[2]);
     H.h[3] = fmaf(-V.b[1], m0, V.A[3]); H.h[4] = fmaf(-V.b[1], m1, V.A[4]); H.h[5] = fmaf(-V.b[1], m2, V.A[5]);
@@ -280,24 +291,38 @@ __device__ __forceinline__ void project(const Hom &H, float x, float y, float &o
 // ---------------------------------------------------------------------------------------------
 // texture sampling
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float tex_ref(const Args &a, int x, int y) {
+template <class AT>
+__device__ __forceinline__ float tex_ref(const AT &a, int x, int y) {
     return a.ref[clampi(y, 0, a.H - 1) * a.W + clampi(x, 0, a.W - 1)];
 }
 // Quad layout: Q[(iy+1)*(W+1) + (ix+1)] = {T(ix,iy), T(ix+1,iy), T(ix,iy+1), T(ix+1,iy+1)} with
 // clamp-to-edge, for ix in [-1, W-1], iy in [-1, H-1] — one 16-byte gather per bilinear sample.
-__device__ __forceinline__ float sample_quad(const float4 *__restrict__ Q, int W, int H, float x, float y) {
-    x = fminf(fmaxf(x, -1.0f), (float)W);
-    y = fminf(fmaxf(y, -1.0f), (float)H);
-    int qx = (int)fmaf(x, 256.0f, 512.5f) - 512;
-    int qy = (int)fmaf(y, 256.0f, 512.5f) - 512;
-    int ix = min(((qx + 512) >> 8) - 2, W - 1);
-    int iy = min(((qy + 512) >> 8) - 2, H - 1);
-    float ax = (float)(qx & 255) * 0.00390625f;
-    float ay = (float)(qy & 255) * 0.00390625f;
-    float4 q = Q[(iy + 1) * (W + 1) + (ix + 1)];
-    float top = fmaf(ax, q.y - q.x, q.x);
-    float bot = fmaf(ax, q.w - q.z, q.z);
+// One bilinear tap: quad index + 1/256 fractions. The coordinate is clamped to [-1, W-1] x [-1, H-1];
+// this is bit-identical to clamp-to-edge over [-1, W] x [-1, H] (the oracle's statement), because past
+// the last texel both taps of the lerp hold the same texel and fmaf(a, 0, t) == t for any fraction a.
+struct QuadTap {
+    uint32_t idx;
+    float ax, ay;
+};
+__device__ __forceinline__ QuadTap quad_tap(float Wm1, float Hm1, uint32_t W1, float x, float y) {
+    x = fminf(fmaxf(x, -1.0f), Wm1);
+    y = fminf(fmaxf(y, -1.0f), Hm1);
+    const int qx = (int)fmaf(x, 256.0f, 512.5f);  // floor(256 x + 0.5) + 512, always >= 256
+    const int qy = (int)fmaf(y, 256.0f, 512.5f);
+    QuadTap t;
+    t.idx = __umul24((uint32_t)((qy >> 8) - 1), W1) + (uint32_t)((qx >> 8) - 1);
+    t.ax = (float)(qx & 255) * 0.00390625f;
+    t.ay = (float)(qy & 255) * 0.00390625f;
+    return t;
+}
+__device__ __forceinline__ float bilerp(const float4 q, float ax, float ay) {
+    const float top = fmaf(ax, q.y - q.x, q.x);
+    const float bot = fmaf(ax, q.w - q.z, q.z);
     return fmaf(ay, bot - top, top);
+}
+__device__ __forceinline__ float sample_quad(const APD_G float4 *__restrict__ Q, int W, int H, float x, float y) {
+    const QuadTap t = quad_tap((float)(W - 1), (float)(H - 1), (uint32_t)(W + 1), x, y);
+    return bilerp(Q[t.idx], t.ax, t.ay);
 }
 
 __device__ __forceinline__ float ncc_finalize(float sr, float srr, float ss, float sss, float srs, float wsum) {
@@ -337,10 +362,11 @@ __device__ __forceinline__ void build_refwin(const Args &a, int px, int py, RefW
 }
 
 // SA quadrant branch of ComputeBilateralNCCOld (APD.cu:664-719); rarely taken, kept out of line.
-__device__ __noinline__ float ncc_old_sa(const Args &a, int px, int py, int s, const Hom &H, uint8_t cid) {
+__device__ __noinline__ float ncc_old_sa(const APD_G Args *ap, int px, int py, int s, const Hom &H, uint8_t cid) {
+    const APD_G Args &a = *ap;
     const int sign[8] = {1, 1, -1, -1, 1, -1, -1, 1};
     const int off[18] = {1, 1, 3, 1, 1, 3, 1, 5, 3, 3, 5, 1, 5, 3, 3, 5, 5, 5};
-    const float4 *Q = a.quad + (size_t)(s - 1) * a.qstride;
+    const APD_G float4 *Q = a.quad + (size_t)(s - 1) * a.qstride;
     float sr = 0.0f, srr = 0.0f, ss = 0.0f, sss = 0.0f, srs = 0.0f, wsum = 0.0f;
     for (int q = 0; q < 4; ++q) {
         for (int j = 0; j < 9; ++j) {
@@ -370,25 +396,44 @@ __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, f
     if (ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f) return APD_COST_MAX;
     if (a.sa_any) {
         int pidx = clampi((int)fmaf(pty, (float)W, ptx), 0, a.HW - 1);
-        if (a.sa[pidx] != 0) return ncc_old_sa(a, px, py, s, Hm, a.sa[py * W + px]);
+        if (a.sa[pidx] != 0) return ncc_old_sa(a.self, px, py, s, Hm, a.sa[py * W + px]);
     }
-    const float4 *__restrict__ Q = a.quad + (size_t)(s - 1) * a.qstride;
+    const APD_G float4 *__restrict__ Q = a.quad + (size_t)(s - 1) * a.qstride;
+    const float Wm1 = (float)(W - 1), Hm1 = (float)(H - 1);
+    const uint32_t W1 = (uint32_t)(W + 1);
     float ss = 0.0f, sss = 0.0f, srs = 0.0f;
+    // One window column (6 taps) per step: all 6 gathers are issued before the first is consumed.
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
         const float x = (float)(px - 5 + 2 * i);
         const float cx = fmaf(Hm.h[0], x, Hm.h[2]);
         const float cy = fmaf(Hm.h[3], x, Hm.h[5]);
         const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
+        QuadTap t[6];
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
             const float y = (float)(py - 5 + 2 * j);
-            float X = fmaf(Hm.h[1], y, cx);
-            float Y = fmaf(Hm.h[4], y, cy);
-            float Z = fmaf(Hm.h[7], y, cz);
-            float iz = 1.0f / Z;
-            float v = sample_quad(Q, W, H, X * iz, Y * iz);
-            float r = rw.r[i * 6 + j];
+            const float X = fmaf(Hm.h[1], y, cx);
+            const float Y = fmaf(Hm.h[4], y, cy);
+            const float Z = fmaf(Hm.h[7], y, cz);
+#ifdef APD_ABLATE_NO_DIV  // timing-only ablation build: no IEEE reciprocal
+            const float iz = Z;
+#else
+            const float iz = 1.0f / Z;
+#endif
+            t[j] = quad_tap(Wm1, Hm1, W1, X * iz, Y * iz);
+        }
+        float4 q[6];
+#pragma unroll
+#ifdef APD_ABLATE_SAME_ADDR  // timing-only ablation build: every gather hits a 1 KiB footprint
+        for (int j = 0; j < 6; ++j) q[j] = Q[t[j].idx & 63];
+#else
+        for (int j = 0; j < 6; ++j) q[j] = Q[t[j].idx];
+#endif
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const float v = bilerp(q[j], t[j].ax, t[j].ay);
+            const float r = rw.r[i * 6 + j];
             ss += v;
             sss = fmaf(v, v, sss);
             srs = fmaf(r, v, srs);
@@ -404,14 +449,16 @@ __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, f
 }
 
 // sa label at a possibly out-of-image linear index (same rule as the oracle's sa_at)
-__device__ __forceinline__ int sa_at(const Args &a, int x, int y) {
+template <class AT>
+__device__ __forceinline__ int sa_at(const AT &a, int x, int y) {
     long idx = (long)y * a.W + x;
     if (idx < 0 || idx >= a.HW) return -1;
     return a.sa[idx];
 }
 
 // ComputeBilateralNCCNew + Softmax focal weighting (APD.cu:448-593, 431-446)
-__device__ __noinline__ float ncc_new(const Args &a, int px, int py, int s, float4 pl) {
+__device__ __noinline__ float ncc_new(const APD_G Args *ap, int px, int py, int s, float4 pl) {
+    const APD_G Args &a = *ap;
     const int W = a.W, H = a.H;
     const int center = px + py * W;
     const int cid = a.sa_any ? a.sa[center] : 0;
@@ -421,8 +468,8 @@ __device__ __noinline__ float ncc_new(const Args &a, int px, int py, int s, floa
     project(Hm, (float)px, (float)py, ptx, pty);
     if (ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f) return APD_COST_MAX;
     if (a.weak[center] != APD_WEAK) return 0.0f;
-    const float4 *__restrict__ Q = a.quad + (size_t)(s - 1) * a.qstride;
-    const short2 *anc = a.anchors + (size_t)a.amap[center] * 9;
+    const APD_G float4 *__restrict__ Q = a.quad + (size_t)(s - 1) * a.qstride;
+    const APD_G short2 *anc = a.anchors + (size_t)a.amap[center] * 9;
     float sc[9];
     int ns = 0;
     float center_cost = 0.0f, strong_weight = 0.0f;
@@ -501,8 +548,8 @@ __device__ __noinline__ float ncc_new(const Args &a, int px, int py, int s, floa
 
 // ComputeGeomConsistencyCost (APD.cu:865-902)
 __device__ __forceinline__ float geom_cost(const Args &a, int px, int py, int s, float4 pl) {
-    const Cam &rc = a.cams[0];
-    const Cam &sc = a.cams[s];
+    const APD_G Cam &rc = a.cams[0];
+    const APD_G Cam &sc = a.cams[s];
     float depth = depth_from_plane(rc, pl, px, py);
     float P[3];
     world_point(rc, (float)px, (float)py, depth, P);

@@ -28,6 +28,9 @@ using namespace apd;
 
 #define WAVE 64
 #define BLOCK 256
+#ifndef APD_SWEEP_WAVES
+#define APD_SWEEP_WAVES 2  // min waves per SIMD requested for the sweep kernels (VGPR budget 512/w)
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // view-group lane mapping
@@ -149,6 +152,52 @@ __global__ __launch_bounds__(BLOCK) void k_list_fill(Args a, int mode, int colou
     }
 }
 
+// Tile-ordered compaction for the sweep pixel sets (modes 0/1). The order of a sweep list does not
+// change any result (pixels of one colour are independent), only locality: pixels are listed by
+// 16x16 tiles, and inside a tile by 4x4 micro-tiles (8 same-colour pixels = one wavefront at N=8),
+// so a wavefront's and a workgroup's NCC windows overlap in the source images.
+#define TILE 16
+__device__ __forceinline__ void tile_pixel(int tile, int tiles_x, int k, int &x, int &y) {
+    const int micro = k >> 4, inner = k & 15;
+    const int lx = ((micro & 3) << 2) + (inner & 3);
+    const int ly = ((micro >> 2) << 2) + (inner >> 2);
+    x = (tile % tiles_x) * TILE + lx;
+    y = (tile / tiles_x) * TILE + ly;
+}
+__global__ __launch_bounds__(BLOCK) void k_tile_count(Args a, int mode, int colour, int tiles_x,
+                                                    int *__restrict__ counts) {
+    int x, y;
+    tile_pixel(blockIdx.x, tiles_x, threadIdx.x, x, y);
+    const bool p = x < a.W && y < a.H && list_pred(a, mode, colour, x, y);
+    __shared__ int wsum[BLOCK / WAVE];
+    const int c = __popcll(__ballot(p));
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) counts[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+__global__ __launch_bounds__(BLOCK) void k_tile_fill(Args a, int mode, int colour, int tiles_x,
+                                                   const int *__restrict__ offs, int *__restrict__ out) {
+    int x, y;
+    tile_pixel(blockIdx.x, tiles_x, threadIdx.x, x, y);
+    const bool p = x < a.W && y < a.H && list_pred(a, mode, colour, x, y);
+    __shared__ int wcnt[BLOCK / WAVE];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(p);
+    if (lane == 0) wcnt[wv] = __popcll(m);
+    __syncthreads();
+    int wo = 0;
+    for (int k = 0; k < wv; ++k) wo += wcnt[k];
+    if (p) out[offs[blockIdx.x] + wo + __popcll(m & ((1ull << lane) - 1ull))] = y * a.W + x;
+}
+
+// XCD-aware workgroup order (cdna_hip_programming.md §5.5 T1): workgroups are dealt round-robin to
+// the 8 XCDs, so give the workgroups of one XCD (b, b+8, ...) one contiguous chunk of the pixel list;
+// each XCD's L2 then serves one compact region of the source images. Bijective for any grid size.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, x = b & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
 // ---------------------------------------------------------------------------------------------
 // APD anchor kernels (pixel kernels)
 // ---------------------------------------------------------------------------------------------
@@ -209,8 +258,8 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
     const int py = c / W, px = c - py * W;
     const int margin = 6;
     const float depth_diff = a.dmax - a.dmin;
-    const Cam &cam = a.cams[0];
-    short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
+    const APD_G Cam &cam = a.cams[0];
+    APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
     Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_ANCHORS);
     for (int i = 0; i < 9; ++i) anc[i] = make_short2(-1, -1);
     anc[0] = make_short2((short)px, (short)py);
@@ -341,8 +390,8 @@ __global__ __launch_bounds__(BLOCK) void k_ransac_fit(Args a, int iter) {
     if (a.weak[c] != APD_WEAK) { a.fit[c] = a.plane[c]; return; }
     const int W = a.W;
     const int py = c / W, px = c - py * W;
-    const Cam &cam = a.cams[0];
-    const short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
+    const APD_G Cam &cam = a.cams[0];
+    const APD_G APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
     int sx[8], sy[8], cnt = 0;
     float s3[8][3], X[3];
     for (int i = 1; i < 9; ++i) {
@@ -402,7 +451,7 @@ __global__ __launch_bounds__(BLOCK) void k_random_init(Args a) {
     const Group G = make_group(N, a.HW, wave);
     const int c = G.li;
     const int py = c / a.W, px = c - py * a.W;
-    const Cam &cam = a.cams[0];
+    const APD_G Cam &cam = a.cams[0];
     float4 pl;
     if (a.state == APD_FIRST_INIT) {
         Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_INIT);
@@ -418,7 +467,7 @@ __global__ __launch_bounds__(BLOCK) void k_random_init(Args a) {
     const int s = G.v + 1;
     float cv;
     if (use_new) {
-        cv = ncc_new(a, px, py, s, pl);
+        cv = ncc_new(a.self, px, py, s, pl);
     } else {
         RefWin rw;
         build_refwin(a, px, py, rw);
@@ -461,7 +510,7 @@ __global__ __launch_bounds__(BLOCK) void k_random_init(Args a) {
         }
         a.plane[c] = pl;
         a.cost[c] = cost_out;
-        a.sel[c] = sv;
+        a.sel_next[c] = sv;  // launch-start snapshot semantics (oracle k_random_init)
     }
 }
 
@@ -509,7 +558,7 @@ struct Cands {
     float drand, dpert;
 };
 __device__ __forceinline__ Cands refine_candidates(const Args &a, int px, int py, Rng &g, float4 cur, float depth) {
-    const Cam &cam = a.cams[0];
+    const APD_G Cam &cam = a.cams[0];
     Cands C;
     C.drand = g.uniform() * (a.dmax - a.dmin) + a.dmin;
     C.nrand = random_normal(cam, px, py, g, depth);
@@ -534,16 +583,16 @@ __device__ __forceinline__ float4 candidate(const Cands &C, int k, float4 cur0, 
 // ---------------------------------------------------------------------------------------------
 // CheckerboardPropagationStrong + PlaneHypothesisRefinementStrong (APD.cu:1098-1440, 950-1006)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BLOCK) void k_sweep_strong(Args a, const int *__restrict__ list, int count, int iter) {
+__global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a, const int *__restrict__ list, int count, int iter) {
     const int N = a.N, W = a.W, H = a.H;
-    const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
+    const int wave = xcd_remap(blockIdx.x, gridDim.x) * (BLOCK / WAVE) + (threadIdx.x >> 6);
     if (wave * (WAVE / N) >= count) return;
     const Group G = make_group(N, count, wave);
     const int c = list[G.li];
     const int py = c / W, px = c - py * W;
     const int s = G.v + 1;
-    const Cam &cam0 = a.cams[0];
-    const float *__restrict__ cost = a.cost;
+    const APD_G Cam &cam0 = a.cams[0];
+    const APD_G float *__restrict__ cost = a.cost;
 
     // adaptive checkerboard neighbour selection (APD.cu:1127-1316); identical in every lane
     int pos[8];
@@ -738,14 +787,14 @@ __global__ __launch_bounds__(BLOCK) void k_sweep_strong(Args a, const int *__res
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(BLOCK) void k_sweep_weak(Args a, const int *__restrict__ list, int count, int iter) {
     const int N = a.N, W = a.W;
-    const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
+    const int wave = xcd_remap(blockIdx.x, gridDim.x) * (BLOCK / WAVE) + (threadIdx.x >> 6);
     if (wave * (WAVE / N) >= count) return;
     const Group G = make_group(N, count, wave);
     const int c = list[G.li];
     const int py = c / W, px = c - py * W;
     const int s = G.v + 1;
-    const Cam &cam0 = a.cams[0];
-    const short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
+    const APD_G Cam &cam0 = a.cams[0];
+    const APD_G APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
     const bool geom = a.geom != 0;
     const float gf = a.gf;
     const float4 cur = a.plane[c];
@@ -773,7 +822,7 @@ __global__ __launch_bounds__(BLOCK) void k_sweep_weak(Args a, const int *__restr
         float val = (h == 0 && G.v == 0) ? 2.0f : 0.0f;
         if (fh) {
             const float4 pl = (h == 8) ? cur : a.plane[ph];
-            val = ncc_new(a, px, py, s, pl);
+            val = ncc_new(a.self, px, py, s, pl);
             if (h == 8 && geom) val = fmaf(gf, geom_cost(a, px, py, s, pl), val);
         }
 #pragma unroll
@@ -845,7 +894,7 @@ __global__ __launch_bounds__(BLOCK) void k_sweep_weak(Args a, const int *__restr
         {
             float cv = 0.0f;
             if (w > 0) {
-                cv = ncc_new(a, px, py, s, fit);
+                cv = ncc_new(a.self, px, py, s, fit);
                 if (geom) cv = fmaf(gf, geom_cost(a, px, py, s, fit), cv);
             }
             float tc = 0.0f;
@@ -868,7 +917,7 @@ __global__ __launch_bounds__(BLOCK) void k_sweep_weak(Args a, const int *__restr
             t.w = dist2origin(cam0, px, py, dk, t);
             float cv = 0.0f;
             if (w > 0) {
-                cv = ncc_new(a, px, py, s, t);
+                cv = ncc_new(a.self, px, py, s, t);
                 if (geom) cv = fmaf(gf, geom_cost(a, px, py, s, t), cv);
             }
             float tc = 0.0f;
@@ -966,7 +1015,7 @@ __global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
     const int c = G.li;
     const int py = c / W, px = c - py * W;
     const int s = G.v + 1;
-    const Cam &cam0 = a.cams[0];
+    const APD_G Cam &cam0 = a.cams[0];
     float *pc = lds_curve + ((threadIdx.x >> 6) * P + G.slot) * 61;
     const bool border = px < 6 || py < 6 || px >= W - 6 || py >= H - 6;
     const float4 pl = to_ref(cam0, a.plane[c]);
@@ -976,7 +1025,7 @@ __global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
     const int wv = a.vw[(size_t)G.v * a.HW + c];
     float mydist;
     {
-        const Cam &sc = a.cams[s];
+        const APD_G Cam &sc = a.cams[s];
         float d0 = cam0.c[0] - sc.c[0], d1 = cam0.c[1] - sc.c[1], d2 = cam0.c[2] - sc.c[2];
         mydist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
     }
@@ -1059,7 +1108,7 @@ __global__ __launch_bounds__(BLOCK) void k_confidence(Args a) {
     const int W = a.W;
     const int py = c / W, px = c - py * W;
     a.conf[c] = 0;
-    const Cam &rc = a.cams[0];
+    const APD_G Cam &rc = a.cams[0];
     const uint32_t sv = a.sel[c];
     const float rd = a.plane[c].w;
     if (rd <= 0.0f) { a.weak[c] = APD_UNKNOWN; return; }
@@ -1069,7 +1118,7 @@ __global__ __launch_bounds__(BLOCK) void k_confidence(Args a) {
     for (int i = 0; i < a.N; ++i) {
         if (!((sv >> i) & 1u)) continue;
         const int s = i + 1;
-        const Cam &sc = a.cams[s];
+        const APD_G Cam &sc = a.cams[s];
         float sx, sy, sd;
         project_cam(P, sc, sx, sy, sd);
         const float src_depth = a.depth[(size_t)s * a.HW + trunc_clamp(sy, a.H) * W + trunc_clamp(sx, W)];
@@ -1096,7 +1145,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_refine(Args a) {
     const int c = G.li;
     const int py = c / W, px = c - py * W;
     const int s = G.v + 1;
-    const Cam &cam0 = a.cams[0];
+    const APD_G Cam &cam0 = a.cams[0];
     const float4 pl = to_ref(cam0, a.plane[c]);
     const float od = pl.w;
     const uint32_t sv = a.sel[c];
@@ -1108,7 +1157,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_refine(Args a) {
     build_refwin(a, px, py, rw);
     float mydist, tc0 = 0.0f;
     {
-        const Cam &sc = a.cams[s];
+        const APD_G Cam &sc = a.cams[s];
         float d0 = cam0.c[0] - sc.c[0], d1 = cam0.c[1] - sc.c[1], d2 = cam0.c[2] - sc.c[2];
         mydist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
     }
@@ -1188,8 +1237,8 @@ struct apd_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // buffers
-    DevBuf imgs, quad, depth, views, cams, plane, cost, sel, vw, weak, conf, sa, amap, anchors, reliable, nearest,
-        fit, curve, lists, rowcnt, rowoff, totals, near_off;
+    DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
+        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs;
     int n_near = 0;
     Args args{};
     bool loaded = false, prepared = false;
@@ -1293,6 +1342,10 @@ static int build_near_offsets(apd_ctx *ctx) {
     return APD_OK;
 }
 
+// host -> device pointer of any address space (the Args members are address_space(1) on device)
+template <class T>
+static inline T devptr(const void *p) { return reinterpret_cast<T>(reinterpret_cast<uintptr_t>(p)); }
+
 static inline unsigned blocks_for(size_t n, int per_block) { return (unsigned)((n + per_block - 1) / per_block); }
 static inline unsigned group_blocks(int n_pixels, int N) {
     const int P = WAVE / N;
@@ -1340,9 +1393,9 @@ void apd_destroy(apd_ctx *ctx) {
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
     DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
-                      &ctx->sel, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
+                      &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
-                      &ctx->rowoff, &ctx->totals, &ctx->near_off};
+                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs};
     for (DevBuf *b : bufs)
         if (b->p) hipFree(b->p);
     for (auto &e : ctx->ev) hipEventDestroy(e);
@@ -1381,13 +1434,15 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     if ((st = ensure(ctx, ctx->plane, HW * sizeof(float4)))) return st;
     if ((st = ensure(ctx, ctx->cost, HW * sizeof(float)))) return st;
     if ((st = ensure(ctx, ctx->sel, HW * sizeof(uint32_t)))) return st;
+    if ((st = ensure(ctx, ctx->sel2, HW * sizeof(uint32_t)))) return st;
     if ((st = ensure(ctx, ctx->vw, HW * N))) return st;
     if ((st = ensure(ctx, ctx->weak, HW))) return st;
     if ((st = ensure(ctx, ctx->conf, HW))) return st;
     if ((st = ensure(ctx, ctx->sa, HW))) return st;
     if ((st = ensure(ctx, ctx->lists, (HW + 8) * sizeof(int)))) return st;
-    if ((st = ensure(ctx, ctx->rowcnt, (size_t)H * sizeof(int)))) return st;
-    if ((st = ensure(ctx, ctx->rowoff, (size_t)H * sizeof(int)))) return st;
+    const size_t units = std::max<size_t>((size_t)H, (size_t)((W + TILE - 1) / TILE) * ((H + TILE - 1) / TILE));
+    if ((st = ensure(ctx, ctx->rowcnt, units * sizeof(int)))) return st;
+    if ((st = ensure(ctx, ctx->rowoff, units * sizeof(int)))) return st;
     if ((st = ensure(ctx, ctx->totals, 8 * sizeof(int)))) return st;
     const bool need_depth = P.geom_consistency || P.use_APD;
     if (need_depth && (st = ensure(ctx, ctx->depth, HW * NI * sizeof(float)))) return st;
@@ -1474,25 +1529,29 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
         a.anc_shift = sr < 1 ? 1 : sr;
     }
     a.qstride = qstride;
-    a.ref = (const float *)ctx->imgs.p;
-    a.quad = (const float4 *)ctx->quad.p;
-    a.depth = need_depth ? (const float *)ctx->depth.p : nullptr;
-    a.views = (const SrcView *)ctx->views.p;
-    a.cams = (const Cam *)ctx->cams.p;
-    a.plane = (float4 *)ctx->plane.p;
-    a.cost = (float *)ctx->cost.p;
-    a.sel = (uint32_t *)ctx->sel.p;
-    a.vw = (uint8_t *)ctx->vw.p;
-    a.weak = (uint8_t *)ctx->weak.p;
-    a.conf = (uint8_t *)ctx->conf.p;
-    a.sa = (const uint8_t *)ctx->sa.p;
-    a.amap = P.use_APD ? (const int *)ctx->amap.p : nullptr;
-    a.anchors = P.use_APD ? (short2 *)ctx->anchors.p : nullptr;
-    a.reliable = P.use_APD ? (uint8_t *)ctx->reliable.p : nullptr;
-    a.nearest = P.use_APD ? (short2 *)ctx->nearest.p : nullptr;
-    a.fit = P.use_APD ? (float4 *)ctx->fit.p : nullptr;
-    a.near_offsets = P.use_APD ? (const short2 *)ctx->near_off.p : nullptr;
+    a.ref = devptr<decltype(a.ref)>(ctx->imgs.p);
+    a.quad = devptr<decltype(a.quad)>(ctx->quad.p);
+    a.depth = devptr<decltype(a.depth)>(need_depth ? ctx->depth.p : nullptr);
+    a.views = devptr<decltype(a.views)>(ctx->views.p);
+    a.cams = devptr<decltype(a.cams)>(ctx->cams.p);
+    a.plane = devptr<decltype(a.plane)>(ctx->plane.p);
+    a.cost = devptr<decltype(a.cost)>(ctx->cost.p);
+    a.sel = devptr<decltype(a.sel)>(ctx->sel.p);
+    a.sel_next = devptr<decltype(a.sel_next)>(ctx->sel2.p);
+    a.vw = devptr<decltype(a.vw)>(ctx->vw.p);
+    a.weak = devptr<decltype(a.weak)>(ctx->weak.p);
+    a.conf = devptr<decltype(a.conf)>(ctx->conf.p);
+    a.sa = devptr<decltype(a.sa)>(ctx->sa.p);
+    a.amap = devptr<decltype(a.amap)>(P.use_APD ? ctx->amap.p : nullptr);
+    a.anchors = devptr<decltype(a.anchors)>(P.use_APD ? ctx->anchors.p : nullptr);
+    a.reliable = devptr<decltype(a.reliable)>(P.use_APD ? ctx->reliable.p : nullptr);
+    a.nearest = devptr<decltype(a.nearest)>(P.use_APD ? ctx->nearest.p : nullptr);
+    a.fit = devptr<decltype(a.fit)>(P.use_APD ? ctx->fit.p : nullptr);
+    a.near_offsets = devptr<decltype(a.near_offsets)>(P.use_APD ? ctx->near_off.p : nullptr);
     a.curve = nullptr;
+    if ((st = ensure(ctx, ctx->dargs, sizeof(Args)))) return st;
+    a.self = devptr<decltype(a.self)>(ctx->dargs.p);
+    HIP_OK(ctx, hipMemcpyAsync(ctx->dargs.p, &a, sizeof(Args), hipMemcpyHostToDevice, s));
     // source images -> quad gather layout
     {
         const size_t total = qstride * N;
@@ -1501,12 +1560,35 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
                            (float4 *)ctx->quad.p, W, H, N, qstride);
         if ((st = check_launch(ctx, "k_build_quads"))) return st;
     }
+    ctx->want_curve = pb->export_reliable_curve != 0;
+    if (ctx->want_curve) {  // DepthToWeak cost curves (APD.cu:2188-2198, 2713-2724)
+        if ((st = ensure(ctx, ctx->curve, HW * 61 * sizeof(float)))) return st;
+        HIP_OK(ctx, hipMemsetAsync(ctx->curve.p, 0, HW * 61 * sizeof(float), s));
+    }
     ctx->params = P;
     ctx->loaded = true;
     return APD_OK;
 }
 
 // device-side ordered compaction of one pixel set
+// Sweep lists (modes 0/1) in tile order: count per tile, scan, fill.
+static void tile_count_scan(apd_ctx *ctx, int mode, int colour, int *total_dev) {
+    Args &a = ctx->args;
+    const int tx = (a.W + TILE - 1) / TILE, ty = (a.H + TILE - 1) / TILE;
+    hipLaunchKernelGGL(k_tile_count, dim3(tx * ty), dim3(BLOCK), 0, ctx->stream, a, mode, colour, tx,
+                       (int *)ctx->rowcnt.p);
+    hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(1024), 0, ctx->stream, (const int *)ctx->rowcnt.p, tx * ty,
+                       (int *)ctx->rowoff.p, total_dev);
+}
+static int build_tile_list(apd_ctx *ctx, int mode, int colour, int *out, int *total_dev) {
+    Args &a = ctx->args;
+    const int tx = (a.W + TILE - 1) / TILE, ty = (a.H + TILE - 1) / TILE;
+    tile_count_scan(ctx, mode, colour, total_dev);
+    hipLaunchKernelGGL(k_tile_fill, dim3(tx * ty), dim3(BLOCK), 0, ctx->stream, a, mode, colour, tx,
+                       (const int *)ctx->rowoff.p, out);
+    return check_launch(ctx, "tile list build");
+}
+// anchors_map (mode 2) in row-major order (APD.cpp:627-640)
 static int build_list(apd_ctx *ctx, int mode, int colour, int *out, int *total_dev) {
     Args &a = ctx->args;
     hipStream_t s = ctx->stream;
@@ -1546,25 +1628,20 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
     // pixel lists for the sweeps (after NeigbourUpdate)
     {
         int *tot = (int *)ctx->totals.p;
-        // counts first (lists are packed back to back), so build each list into a scratch region
-        // at the end of the shared buffer is unnecessary: compute counts, read them back, then fill.
+        // the four lists are packed back to back: counts first (one small read-back), then fill
         const int modes[4][2] = {{0, 0}, {0, 1}, {1, 0}, {1, 1}};
-        for (int i = 0; i < 4; ++i) {
-            hipLaunchKernelGGL(k_list_count, dim3(a.H), dim3(BLOCK), 0, s, a, modes[i][0], modes[i][1],
-                               (int *)ctx->rowcnt.p);
-            hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(1024), 0, s, (const int *)ctx->rowcnt.p, a.H,
-                               (int *)ctx->rowoff.p, tot + i);
-        }
+        for (int i = 0; i < 4; ++i) tile_count_scan(ctx, modes[i][0], modes[i][1], tot + i);
         int host_tot[4];
         HIP_OK(ctx, hipMemcpyAsync(host_tot, tot, 4 * sizeof(int), hipMemcpyDeviceToHost, s));
         HIP_OK(ctx, hipStreamSynchronize(s));
         for (int i = 0; i < 4; ++i) ctx->cnt[i] = host_tot[i];
         for (int i = 0; i < 4; ++i) {
-            if ((st = build_list(ctx, modes[i][0], modes[i][1], list_ptr(ctx, i), tot + i))) return st;
+            if ((st = build_tile_list(ctx, modes[i][0], modes[i][1], list_ptr(ctx, i), tot + i))) return st;
         }
     }
     hipEventRecord(ctx->ev[2], s);
     hipLaunchKernelGGL(k_random_init, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), 0, s, a);
+    HIP_OK(ctx, hipMemcpyAsync(ctx->sel.p, ctx->sel2.p, (size_t)a.HW * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     if ((st = check_launch(ctx, "k_random_init"))) return st;
     hipEventRecord(ctx->ev[3], s);
     ctx->prepared = true;
@@ -1622,7 +1699,7 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
             hipLaunchKernelGGL(k_filter, dim3(blocks_for((size_t)n, BLOCK)), dim3(BLOCK), 0, s, a,
                                (const int *)list_ptr(ctx, colour), n);
     }
-    if (ctx->want_curve && ctx->curve.p) a.curve = (float *)ctx->curve.p;
+    if (ctx->want_curve && ctx->curve.p) a.curve = devptr<decltype(a.curve)>(ctx->curve.p);
     {
         const int P = WAVE / a.N;
         const size_t lds = (size_t)(BLOCK / WAVE) * P * 61 * sizeof(float);
@@ -1687,6 +1764,8 @@ int32_t apd_get_results(apd_ctx *ctx, const apd_outputs *out) {
     if (out->anchors && a.use_apd && ctx->weak_count > 0)
         HIP_OK(ctx, hipMemcpyAsync(out->anchors, ctx->anchors.p, (size_t)ctx->weak_count * 9 * sizeof(short2),
                                    hipMemcpyDeviceToHost, s));
+    if (out->reliable_curve && ctx->want_curve)
+        HIP_OK(ctx, hipMemcpyAsync(out->reliable_curve, ctx->curve.p, HW * 61 * sizeof(float), hipMemcpyDeviceToHost, s));
     if (out->weak_count) *out->weak_count = ctx->weak_count;
     HIP_OK(ctx, hipStreamSynchronize(s));
     return APD_OK;

@@ -123,6 +123,9 @@ typedef struct apd_problem {
     const uint8_t *sa_mask;
     /* Deterministic RNG contract (replaces curand_init(clock64(),...), APD.cu:904-917). */
     uint64_t seed;
+    /* Problem::export_reliable_curve (main.h:111): keep DepthToWeak's 61-sample cost curves so
+       apd_get_results can return them in apd_outputs.reliable_curve (APD.cu:2713-2724). */
+    int32_t export_reliable_curve;
 } apd_problem;
 
 /* Caller-allocated outputs (D2H of APD.cu:2731-2736). Any pointer may be NULL to skip it. */

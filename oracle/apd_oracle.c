@@ -170,6 +170,7 @@ typedef struct {
     f4 *plane;
     float *cost;
     uint32_t *sel;
+    uint32_t *sel_next; /* RandomInitialization output (launch-start snapshot semantics) */
     uint8_t *vw;      /* view-major: vw[v*HW + pix] */
     uint8_t *weak;
     uint8_t *conf;
@@ -575,7 +576,10 @@ static void k_random_init(octx *o, int px, int py) {
         for (j = i; j >= 1 && t < sorted[j - 1]; j--) sorted[j] = sorted[j - 1];
         sorted[j] = t;
     }
-    o->sel[c] = 0;
+    /* The reference writes selected_views[center] here while ComputeBilateralNCCNew of other WEAK pixels
+       reads the anchors' selected_views in the same launch (APD.cu:502 vs 755-766): a race on
+       uninitialised memory. Defined here as launch-start snapshot: results go to sel_next. */
+    o->sel_next[c] = 0;
     int top_k = nvalid < o->P.top_k ? nvalid : o->P.top_k;
     if (top_k > 0) {
         float cost = 0.0f;
@@ -583,7 +587,7 @@ static void k_random_init(octx *o, int px, int py) {
         float thr = sorted[top_k - 1];
         uint32_t sv = 0;
         for (int i = 0; i < N; ++i) if (cv[i] <= thr) sv |= (1u << i);
-        o->sel[c] = sv;
+        o->sel_next[c] = sv;
         o->cost[c] = cost / (float)top_k;
     } else {
         o->cost[c] = COST_MAX;
@@ -1360,6 +1364,7 @@ static void run_prepare(octx *o) {
         });
     }
     FOR_ALL(o, k_random_init(o, px, py));
+    memcpy(o->sel, o->sel_next, (size_t)o->HW * sizeof(uint32_t));
 }
 static void run_iteration(octx *o, int it) {
     FOR_COLOUR(o, 0, if (o->weak[py * o->W + px] != WEAK) k_sweep_strong(o, px, py, it));
@@ -1400,6 +1405,7 @@ static int ctx_init(octx *o, const apd_problem *pb) {
     o->plane = (f4 *)calloc(HW, sizeof(f4));
     o->cost = (float *)calloc(HW, sizeof(float));
     o->sel = (uint32_t *)calloc(HW, sizeof(uint32_t));
+    o->sel_next = (uint32_t *)calloc(HW, sizeof(uint32_t));
     o->vw = (uint8_t *)calloc(HW * (size_t)o->N, 1);
     o->weak = (uint8_t *)malloc(HW);
     o->conf = (uint8_t *)malloc(HW);
@@ -1408,7 +1414,7 @@ static int ctx_init(octx *o, const apd_problem *pb) {
     o->reliable = (uint8_t *)calloc(HW, 1);
     o->nearest = (int16_t *)calloc(HW * 2, sizeof(int16_t));
     o->fit = (f4 *)calloc(HW, sizeof(f4));
-    if (!o->plane || !o->cost || !o->sel || !o->vw || !o->weak || !o->conf || !o->sa_zero || !o->amap ||
+    if (!o->plane || !o->cost || !o->sel || !o->sel_next || !o->vw || !o->weak || !o->conf || !o->sa_zero || !o->amap ||
         !o->reliable || !o->nearest || !o->fit)
         return APD_ENOMEM;
     o->sa = pb->sa_mask ? pb->sa_mask : o->sa_zero;
@@ -1427,7 +1433,7 @@ static int ctx_init(octx *o, const apd_problem *pb) {
     return APD_OK;
 }
 static void ctx_free(octx *o) {
-    free(o->plane); free(o->cost); free(o->sel); free(o->vw); free(o->weak); free(o->conf);
+    free(o->plane); free(o->cost); free(o->sel); free(o->sel_next); free(o->vw); free(o->weak); free(o->conf);
     free(o->sa_zero); free(o->amap); free(o->reliable); free(o->nearest); free(o->fit); free(o->anchors);
 }
 static void ctx_output(const octx *o, const apd_outputs *out) {

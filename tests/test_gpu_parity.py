@@ -52,6 +52,19 @@ def test_bit_exact(name, oracle, engine):
         assert np.array_equal(ref.anchors[:wc], got.anchors[:wc])
 
 
+def test_reliable_curve_export(oracle, engine):
+    """DepthToWeak's 61-sample cost curves (--export_curve, APD.cu:2188-2198) match bit-for-bit."""
+    orun = lambda arr: oracle_lib.run(oracle, arr)
+    arr = cases.make_case("refine_iter_geom", orun)
+    arr.export_reliable_curve = True
+    ref = oracle_lib.run(oracle, arr, want_curve=True)
+    engine.set_problem(arr)
+    engine.run()
+    got = engine.results(A.Outputs(arr.width, arr.height, len(arr.images) - 1, want_curve=True))
+    assert (ref.reliable_curve != 0).any()
+    assert np.array_equal(ref.reliable_curve.view(np.uint32), got.reliable_curve.view(np.uint32))
+
+
 def test_stages_equal_full_run(oracle, engine):
     """prepare + iteration(i) + finish must be the same computation as apd_run_patchmatch."""
     orun = lambda arr: oracle_lib.run(oracle, arr)
