@@ -57,6 +57,8 @@ struct Args {
     size_t qstride;                        // float4 elements per source quad image ((W+1)*(H+1))
     const APD_G float *ref;                // reference image, H*W
     const APD_G float4 *quad;              // source images 1..N in quad layout, view v at (v-1)*qstride
+    const APD_G uint32_t *pairs;           // or in fp16 vertical-pair layout (tex_f16), same stride
+    int tex_f16;
     const APD_G float *depth;              // [N+1][H*W] depth maps (geom / APD)
     const APD_G SrcView *views;            // [N+1]
     const APD_G Cam *cams;                 // [N+1]
@@ -320,9 +322,39 @@ __device__ __forceinline__ float bilerp(const float4 q, float ax, float ay) {
     const float bot = fmaf(ax, q.w - q.z, q.z);
     return fmaf(ay, bot - top, top);
 }
-__device__ __forceinline__ float sample_quad(const APD_G float4 *__restrict__ Q, int W, int H, float x, float y) {
-    const QuadTap t = quad_tap((float)(W - 1), (float)(H - 1), (uint32_t)(W + 1), x, y);
-    return bilerp(Q[t.idx], t.ax, t.ay);
+// Source-image storage, selected per problem by the host:
+//  F16 = true : "vertical fp16 pairs", P[(iy+1)*(W+2) + (ix+1)] = {half T(ix,iy), half T(ix,iy+1)}
+//               (clamp-to-edge, ix in [-1, W], iy in [-1, H-1]); ONE 8-byte load at tap index idx
+//               returns the 2x2 footprint. 4 bytes per texel. Used when every source texel is
+//               exactly representable in fp16 (8-bit images and their dyadic INTER_LINEAR
+//               downscales are), so the fp32 arithmetic after the exact conversion is unchanged.
+//  F16 = false: fp32 quads, Q[(iy+1)*(W+1) + (ix+1)] = {T00, T10, T01, T11}, 16 bytes per texel.
+typedef _Float16 apd_h2 __attribute__((ext_vector_type(2)));
+typedef uint2 apd_u2_a4 __attribute__((aligned(4)));
+template <bool F16>
+struct SrcTex {
+    const APD_G void *base;
+    template <class AT>
+    __device__ __forceinline__ SrcTex(const AT &a, int s) {
+        if constexpr (F16) base = (const APD_G void *)(a.pairs + (size_t)(s - 1) * a.qstride);
+        else base = (const APD_G void *)(a.quad + (size_t)(s - 1) * a.qstride);
+    }
+    static __device__ __forceinline__ uint32_t pitch(int W) { return (uint32_t)(F16 ? W + 2 : W + 1); }
+    __device__ __forceinline__ float4 fetch(uint32_t idx) const {
+        if constexpr (F16) {
+            const apd_u2_a4 v = *(const APD_G apd_u2_a4 *)((const APD_G uint32_t *)base + idx);
+            const apd_h2 c0 = __builtin_bit_cast(apd_h2, v.x);  // {T(ix,iy), T(ix,iy+1)}
+            const apd_h2 c1 = __builtin_bit_cast(apd_h2, v.y);  // {T(ix+1,iy), T(ix+1,iy+1)}
+            return make_float4((float)c0.x, (float)c1.x, (float)c0.y, (float)c1.y);
+        } else {
+            return ((const APD_G float4 *)base)[idx];
+        }
+    }
+};
+template <bool F16>
+__device__ __forceinline__ float sample_src(const SrcTex<F16> &T, int W, int H, float x, float y) {
+    const QuadTap t = quad_tap((float)(W - 1), (float)(H - 1), SrcTex<F16>::pitch(W), x, y);
+    return bilerp(T.fetch(t.idx), t.ax, t.ay);
 }
 
 __device__ __forceinline__ float ncc_finalize(float sr, float srr, float ss, float sss, float srs, float wsum) {
@@ -362,11 +394,12 @@ __device__ __forceinline__ void build_refwin(const Args &a, int px, int py, RefW
 }
 
 // SA quadrant branch of ComputeBilateralNCCOld (APD.cu:664-719); rarely taken, kept out of line.
+template <bool F16>
 __device__ __noinline__ float ncc_old_sa(const APD_G Args *ap, int px, int py, int s, const Hom &H, uint8_t cid) {
     const APD_G Args &a = *ap;
     const int sign[8] = {1, 1, -1, -1, 1, -1, -1, 1};
     const int off[18] = {1, 1, 3, 1, 1, 3, 1, 5, 3, 3, 5, 1, 5, 3, 3, 5, 5, 5};
-    const APD_G float4 *Q = a.quad + (size_t)(s - 1) * a.qstride;
+    const SrcTex<F16> Q(a, s);
     float sr = 0.0f, srr = 0.0f, ss = 0.0f, sss = 0.0f, srs = 0.0f, wsum = 0.0f;
     for (int q = 0; q < 4; ++q) {
         for (int j = 0; j < 9; ++j) {
@@ -377,7 +410,7 @@ __device__ __noinline__ float ncc_old_sa(const APD_G Args *ap, int px, int py, i
             float r = tex_ref(a, rx, ry);
             float sx, sy;
             project(H, (float)rx, (float)ry, sx, sy);
-            float v = sample_quad(Q, a.W, a.H, sx, sy);
+            float v = sample_src(Q, a.W, a.H, sx, sy);
             sr += r; srr = fmaf(r, r, srr);
             ss += v; sss = fmaf(v, v, sss);
             srs = fmaf(r, v, srs);
@@ -388,6 +421,7 @@ __device__ __noinline__ float ncc_old_sa(const APD_G Args *ap, int px, int py, i
 }
 
 // ComputeBilateralNCCOld (APD.cu:596-721) for source view s (1..N), plane in the ref frame.
+template <bool F16>
 __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, float4 pl, const RefWin &rw) {
     const int W = a.W, H = a.H;
     Hom Hm = homography(a, s, pl);
@@ -396,11 +430,11 @@ __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, f
     if (ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f) return APD_COST_MAX;
     if (a.sa_any) {
         int pidx = clampi((int)fmaf(pty, (float)W, ptx), 0, a.HW - 1);
-        if (a.sa[pidx] != 0) return ncc_old_sa(a.self, px, py, s, Hm, a.sa[py * W + px]);
+        if (a.sa[pidx] != 0) return ncc_old_sa<F16>(a.self, px, py, s, Hm, a.sa[py * W + px]);
     }
-    const APD_G float4 *__restrict__ Q = a.quad + (size_t)(s - 1) * a.qstride;
+    const SrcTex<F16> Q(a, s);
     const float Wm1 = (float)(W - 1), Hm1 = (float)(H - 1);
-    const uint32_t W1 = (uint32_t)(W + 1);
+    const uint32_t W1 = SrcTex<F16>::pitch(W);
     float ss = 0.0f, sss = 0.0f, srs = 0.0f;
     // One window column (6 taps) per step: all 6 gathers are issued before the first is consumed.
 #pragma unroll
@@ -426,9 +460,9 @@ __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, f
         float4 q[6];
 #pragma unroll
 #ifdef APD_ABLATE_SAME_ADDR  // timing-only ablation build: every gather hits a 1 KiB footprint
-        for (int j = 0; j < 6; ++j) q[j] = Q[t[j].idx & 63];
+        for (int j = 0; j < 6; ++j) q[j] = Q.fetch(t[j].idx & 63);
 #else
-        for (int j = 0; j < 6; ++j) q[j] = Q[t[j].idx];
+        for (int j = 0; j < 6; ++j) q[j] = Q.fetch(t[j].idx);
 #endif
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
@@ -457,6 +491,7 @@ __device__ __forceinline__ int sa_at(const AT &a, int x, int y) {
 }
 
 // ComputeBilateralNCCNew + Softmax focal weighting (APD.cu:448-593, 431-446)
+template <bool F16>
 __device__ __noinline__ float ncc_new(const APD_G Args *ap, int px, int py, int s, float4 pl) {
     const APD_G Args &a = *ap;
     const int W = a.W, H = a.H;
@@ -468,7 +503,7 @@ __device__ __noinline__ float ncc_new(const APD_G Args *ap, int px, int py, int 
     project(Hm, (float)px, (float)py, ptx, pty);
     if (ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f) return APD_COST_MAX;
     if (a.weak[center] != APD_WEAK) return 0.0f;
-    const APD_G float4 *__restrict__ Q = a.quad + (size_t)(s - 1) * a.qstride;
+    const SrcTex<F16> Q(a, s);
     const APD_G short2 *anc = a.anchors + (size_t)a.amap[center] * 9;
     float sc[9];
     int ns = 0;
@@ -508,7 +543,7 @@ __device__ __noinline__ float ncc_new(const APD_G Args *ap, int px, int py, int 
                 float Y = fmaf(Hm.h[4], y, cy);
                 float Z = fmaf(Hm.h[7], y, cz);
                 float iz = 1.0f / Z;
-                float v = sample_quad(Q, W, H, X * iz, Y * iz);
+                float v = sample_src(Q, W, H, X * iz, Y * iz);
                 sr += r; srr = fmaf(r, r, srr);
                 ss += v; sss = fmaf(v, v, sss);
                 srs = fmaf(r, v, srs);

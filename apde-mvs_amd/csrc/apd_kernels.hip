@@ -87,6 +87,27 @@ __global__ __launch_bounds__(BLOCK) void k_build_quads(const float *__restrict__
     }
 }
 
+// Source images -> fp16 vertical pairs P[(iy+1)*(W+2)+(ix+1)] = {half T(ix,iy), half T(ix,iy+1)},
+// ix in [-1, W], iy in [-1, H-1], clamp-to-edge (see SrcTex in apd_device.h).
+__global__ __launch_bounds__(BLOCK) void k_build_pairs(const float *__restrict__ imgs, uint32_t *__restrict__ pairs,
+                                                     int W, int H, int N, size_t pstride) {
+    const size_t per = (size_t)(W + 2) * (H + 1);
+    const size_t total = per * N;
+    for (size_t i = blockIdx.x * (size_t)BLOCK + threadIdx.x; i < total; i += (size_t)gridDim.x * BLOCK) {
+        const int v = (int)(i / per);
+        const size_t r = i - (size_t)v * per;
+        const int iy = (int)(r / (W + 2)) - 1;
+        const int ix = (int)(r % (W + 2)) - 1;
+        const float *T = imgs + (size_t)(v + 1) * W * H;
+        const int x0 = clampi(ix, 0, W - 1);
+        const int y0 = clampi(iy, 0, H - 1), y1 = clampi(iy + 1, 0, H - 1);
+        apd_h2 h;
+        h.x = (_Float16)T[y0 * W + x0];
+        h.y = (_Float16)T[y1 * W + x0];
+        pairs[(size_t)v * pstride + r] = __builtin_bit_cast(uint32_t, h);
+    }
+}
+
 // Ordered compaction, one workgroup per image row.
 //   mode 0: colour `colour`, weak != WEAK, y < row_limit   (Strong sweep / filter pixel set)
 //   mode 1: colour `colour`, weak == WEAK, y < row_limit   (Weak sweep pixel set)
@@ -443,6 +464,7 @@ __global__ __launch_bounds__(BLOCK) void k_ransac_fit(Args a, int iter) {
 // ---------------------------------------------------------------------------------------------
 // RandomInitialization (APD.cu:919-948) + ComputeMultiViewInitialCostandSelectedViews (723-774)
 // ---------------------------------------------------------------------------------------------
+template <bool F16>
 __global__ __launch_bounds__(BLOCK) void k_random_init(Args a) {
     const int N = a.N;
     const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
@@ -467,11 +489,11 @@ __global__ __launch_bounds__(BLOCK) void k_random_init(Args a) {
     const int s = G.v + 1;
     float cv;
     if (use_new) {
-        cv = ncc_new(a.self, px, py, s, pl);
+        cv = ncc_new<F16>(a.self, px, py, s, pl);
     } else {
         RefWin rw;
         build_refwin(a, px, py, rw);
-        cv = ncc_old(a, px, py, s, pl, rw);
+        cv = ncc_old<F16>(a, px, py, s, pl, rw);
     }
     // stable top-k of the N costs (insertion sort, APD.cu:3-12, 754-769)
     const int topk_max = 4;
@@ -583,6 +605,7 @@ __device__ __forceinline__ float4 candidate(const Cands &C, int k, float4 cur0, 
 // ---------------------------------------------------------------------------------------------
 // CheckerboardPropagationStrong + PlaneHypothesisRefinementStrong (APD.cu:1098-1440, 950-1006)
 // ---------------------------------------------------------------------------------------------
+template <bool F16>
 __global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a, const int *__restrict__ list, int count, int iter) {
     const int N = a.N, W = a.W, H = a.H;
     const int wave = xcd_remap(blockIdx.x, gridDim.x) * (BLOCK / WAVE) + (threadIdx.x >> 6);
@@ -689,7 +712,7 @@ __global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a,
         float val = (h == 0 && G.v == 0) ? 2.0f : 0.0f;  // float cost_array[8][32] = {2.0f} (APD.cu:1120)
         if (fh) {
             const float4 pl = (h == 8) ? cur : a.plane[ph];
-            val = ncc_old(a, px, py, s, pl, rw);
+            val = ncc_old<F16>(a, px, py, s, pl, rw);
             if (h == 8 && geom_imp) val = fmaf(gf, geom_cost(a, px, py, s, pl), val);
         }
 #pragma unroll
@@ -760,7 +783,7 @@ __global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a,
         float dk;
         float4 t = candidate(C, k, cur0, d0, dk);
         t.w = dist2origin(cam0, px, py, dk, t);
-        float cv = ncc_old(a, px, py, s, t, rw);
+        float cv = ncc_old<F16>(a, px, py, s, t, rw);
         if (geom_imp) cv = fmaf(gf, geom_cost(a, px, py, s, t), cv);
         float tc = 0.0f;
         for (int kk = 0; kk < N; ++kk) tc = fmaf((float)__shfl(w, G.base + kk), __shfl(cv, G.base + kk), tc);
@@ -785,6 +808,7 @@ __global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a,
 // ---------------------------------------------------------------------------------------------
 // CheckerboardPropagationWeak + PlaneHypothesisRefinementWeak (APD.cu:1442-1615, 1008-1096)
 // ---------------------------------------------------------------------------------------------
+template <bool F16>
 __global__ __launch_bounds__(BLOCK) void k_sweep_weak(Args a, const int *__restrict__ list, int count, int iter) {
     const int N = a.N, W = a.W;
     const int wave = xcd_remap(blockIdx.x, gridDim.x) * (BLOCK / WAVE) + (threadIdx.x >> 6);
@@ -822,7 +846,7 @@ __global__ __launch_bounds__(BLOCK) void k_sweep_weak(Args a, const int *__restr
         float val = (h == 0 && G.v == 0) ? 2.0f : 0.0f;
         if (fh) {
             const float4 pl = (h == 8) ? cur : a.plane[ph];
-            val = ncc_new(a.self, px, py, s, pl);
+            val = ncc_new<F16>(a.self, px, py, s, pl);
             if (h == 8 && geom) val = fmaf(gf, geom_cost(a, px, py, s, pl), val);
         }
 #pragma unroll
@@ -894,7 +918,7 @@ __global__ __launch_bounds__(BLOCK) void k_sweep_weak(Args a, const int *__restr
         {
             float cv = 0.0f;
             if (w > 0) {
-                cv = ncc_new(a.self, px, py, s, fit);
+                cv = ncc_new<F16>(a.self, px, py, s, fit);
                 if (geom) cv = fmaf(gf, geom_cost(a, px, py, s, fit), cv);
             }
             float tc = 0.0f;
@@ -917,7 +941,7 @@ __global__ __launch_bounds__(BLOCK) void k_sweep_weak(Args a, const int *__restr
             t.w = dist2origin(cam0, px, py, dk, t);
             float cv = 0.0f;
             if (w > 0) {
-                cv = ncc_new(a.self, px, py, s, t);
+                cv = ncc_new<F16>(a.self, px, py, s, t);
                 if (geom) cv = fmaf(gf, geom_cost(a, px, py, s, t), cv);
             }
             float tc = 0.0f;
@@ -1006,6 +1030,7 @@ __global__ __launch_bounds__(BLOCK) void k_filter(Args a, const int *__restrict_
 
 // DepthToWeak (APD.cu:2103-2250): 61-sample disparity sweep of the selected views -> PixelState.
 // The cost curve of each pixel is staged in LDS for the peak analysis.
+template <bool F16>
 __global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
     extern __shared__ float lds_curve[];
     const int N = a.N, W = a.W, H = a.H;
@@ -1055,7 +1080,7 @@ __global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
         if (active && in_range && mine) {
             float4 t = pl;
             t.w = dist2origin(cam0, px, py, pdepth, t);
-            tc = ncc_old(a, px, py, s, t, rw);
+            tc = ncc_old<F16>(a, px, py, s, t, rw);
             if (geom) tc = fmaf(gf, geom_cost(a, px, py, s, t), tc);
         }
         float p = 0.0f;
@@ -1137,6 +1162,7 @@ __global__ __launch_bounds__(BLOCK) void k_confidence(Args a) {
 }
 
 // LocalRefine (APD.cu:2346-2432)
+template <bool F16>
 __global__ __launch_bounds__(BLOCK) void k_local_refine(Args a) {
     const int N = a.N, W = a.W;
     const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
@@ -1165,7 +1191,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_refine(Args a) {
     if (live && mine) {
         float4 t = pl;
         t.w = dist2origin(cam0, px, py, od, t);
-        tc0 = ncc_old(a, px, py, s, t, rw);
+        tc0 = ncc_old<F16>(a, px, py, s, t, rw);
         if (geom) tc0 = fmaf(gf, geom_cost(a, px, py, s, t), tc0);
     }
     float cost_now = 0.0f, base = 0.0f, wn = 0.0f;
@@ -1193,7 +1219,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_refine(Args a) {
         if (run && in_range && mine) {
             float4 t = pl;
             t.w = dist2origin(cam0, px, py, pdepth, t);
-            nv = ncc_old(a, px, py, s, t, rw);
+            nv = ncc_old<F16>(a, px, py, s, t, rw);
             if (geom) gv = gf * geom_cost(a, px, py, s, t);
         }
         float tc = 0.0f;
@@ -1346,6 +1372,13 @@ static int build_near_offsets(apd_ctx *ctx) {
 template <class T>
 static inline T devptr(const void *p) { return reinterpret_cast<T>(reinterpret_cast<uintptr_t>(p)); }
 
+// launch the fp16-pair or the fp32-quad instantiation of a sampling kernel
+#define LAUNCH_TEX(kern, grid, block, lds, stream, ...)                                            \
+    do {                                                                                         \
+        if (ctx->args.tex_f16) hipLaunchKernelGGL((kern<true>), grid, block, lds, stream, __VA_ARGS__); \
+        else hipLaunchKernelGGL((kern<false>), grid, block, lds, stream, __VA_ARGS__);            \
+    } while (0)
+
 static inline unsigned blocks_for(size_t n, int per_block) { return (unsigned)((n + per_block - 1) / per_block); }
 static inline unsigned group_blocks(int n_pixels, int N) {
     const int P = WAVE / N;
@@ -1425,10 +1458,19 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     if ((P.geom_consistency || P.use_APD) && !pb->depths) { ctx->err = "depth maps required (geom/APD)"; return APD_EINVAL; }
     const int N = NI - 1;
     const size_t HW = (size_t)W * H;
-    const size_t qstride = (size_t)(W + 1) * (H + 1);
+    // source texel storage: fp16 vertical pairs when every source texel is exact in fp16, else fp32 quads
+    bool tex_f16 = getenv("APD_TEX_F32") == nullptr;
+    for (int i = 1; i < NI && tex_f16; ++i) {
+        const float *img = pb->images[i];
+        if (!img) break;
+        for (size_t k = 0; k < (size_t)W * H; ++k) {
+            if ((float)(_Float16)img[k] != img[k]) { tex_f16 = false; break; }
+        }
+    }
+    const size_t qstride = tex_f16 ? (size_t)(W + 2) * (H + 1) : (size_t)(W + 1) * (H + 1);
     int st;
     if ((st = ensure(ctx, ctx->imgs, HW * NI * sizeof(float)))) return st;
-    if ((st = ensure(ctx, ctx->quad, qstride * N * sizeof(float4)))) return st;
+    if ((st = ensure(ctx, ctx->quad, qstride * N * (tex_f16 ? sizeof(uint32_t) : sizeof(float4))))) return st;
     if ((st = ensure(ctx, ctx->views, NI * sizeof(SrcView)))) return st;
     if ((st = ensure(ctx, ctx->cams, NI * sizeof(Cam)))) return st;
     if ((st = ensure(ctx, ctx->plane, HW * sizeof(float4)))) return st;
@@ -1531,6 +1573,8 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     a.qstride = qstride;
     a.ref = devptr<decltype(a.ref)>(ctx->imgs.p);
     a.quad = devptr<decltype(a.quad)>(ctx->quad.p);
+    a.pairs = devptr<decltype(a.pairs)>(ctx->quad.p);
+    a.tex_f16 = tex_f16 ? 1 : 0;
     a.depth = devptr<decltype(a.depth)>(need_depth ? ctx->depth.p : nullptr);
     a.views = devptr<decltype(a.views)>(ctx->views.p);
     a.cams = devptr<decltype(a.cams)>(ctx->cams.p);
@@ -1556,8 +1600,12 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     {
         const size_t total = qstride * N;
         unsigned g = (unsigned)std::min<size_t>(blocks_for(total, BLOCK), 65535u * 8u);
-        hipLaunchKernelGGL(k_build_quads, dim3(g), dim3(BLOCK), 0, s, (const float *)ctx->imgs.p,
-                           (float4 *)ctx->quad.p, W, H, N, qstride);
+        if (tex_f16)
+            hipLaunchKernelGGL(k_build_pairs, dim3(g), dim3(BLOCK), 0, s, (const float *)ctx->imgs.p,
+                               (uint32_t *)ctx->quad.p, W, H, N, qstride);
+        else
+            hipLaunchKernelGGL(k_build_quads, dim3(g), dim3(BLOCK), 0, s, (const float *)ctx->imgs.p,
+                               (float4 *)ctx->quad.p, W, H, N, qstride);
         if ((st = check_launch(ctx, "k_build_quads"))) return st;
     }
     ctx->want_curve = pb->export_reliable_curve != 0;
@@ -1640,7 +1688,7 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         }
     }
     hipEventRecord(ctx->ev[2], s);
-    hipLaunchKernelGGL(k_random_init, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), 0, s, a);
+    LAUNCH_TEX(k_random_init, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), 0, s, a);
     HIP_OK(ctx, hipMemcpyAsync(ctx->sel.p, ctx->sel2.p, (size_t)a.HW * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     if ((st = check_launch(ctx, "k_random_init"))) return st;
     hipEventRecord(ctx->ev[3], s);
@@ -1663,7 +1711,7 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             hipEventCreate(&e1);
             hipEventRecord(e0, s);
         }
-        hipLaunchKernelGGL(k_sweep_strong, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
+        LAUNCH_TEX(k_sweep_strong, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
                            (const int *)list_ptr(ctx, colour), n, iter);
         if (ctx->prof) {
             hipEventRecord(e1, s);
@@ -1677,7 +1725,7 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
         for (int colour = 0; colour < 2; ++colour) {
             const int n = ctx->cnt[2 + colour];
             if (n <= 0) continue;
-            hipLaunchKernelGGL(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
+            LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
                                (const int *)list_ptr(ctx, 2 + colour), n, iter);
         }
         if ((st = check_launch(ctx, "weak sweep"))) return st;
@@ -1703,10 +1751,10 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
     {
         const int P = WAVE / a.N;
         const size_t lds = (size_t)(BLOCK / WAVE) * P * 61 * sizeof(float);
-        hipLaunchKernelGGL(k_depth_to_weak, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), lds, s, a);
+        LAUNCH_TEX(k_depth_to_weak, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), lds, s, a);
     }
     if (a.geom || a.use_apd) hipLaunchKernelGGL(k_confidence, dim3(gpx), dim3(BLOCK), 0, s, a);
-    hipLaunchKernelGGL(k_local_refine, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), 0, s, a);
+    LAUNCH_TEX(k_local_refine, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), 0, s, a);
     if ((st = check_launch(ctx, "finish"))) return st;
     return APD_OK;
 }

@@ -11,14 +11,19 @@ ROUNDS = int(os.environ.get("AB_ROUNDS", 5))
 sc = synth.make_scene(W, H, N)
 arr = A.scene_problem(sc, 0, [j for j, _ in sc.pairs[0]][:N])
 engines = []
-for path in sys.argv[1:]:
+for spec in sys.argv[1:]:
+    path, _, opt = spec.partition(":")   # "lib.so:f32" forces the fp32 quad texel layout
+    if opt == "f32":
+        os.environ["APD_TEX_F32"] = "1"
+    else:
+        os.environ.pop("APD_TEX_F32", None)
     lib = A.load_library(path)
     e = A.Engine(0, lib)
     e.set_problem(arr)
     e.prepare()
     e.iteration(0)
     e.synchronize()
-    engines.append((os.path.basename(path), e))
+    engines.append((os.path.basename(path) + (':' + opt if opt else ''), e))
 res = {n: [] for n, _ in engines}
 for r in range(ROUNDS):
     for name, e in engines:
