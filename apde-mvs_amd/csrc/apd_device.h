@@ -330,7 +330,7 @@ __device__ __forceinline__ float bilerp(const float4 q, float ax, float ay) {
 //               downscales are), so the fp32 arithmetic after the exact conversion is unchanged.
 //  F16 = false: fp32 quads, Q[(iy+1)*(W+1) + (ix+1)] = {T00, T10, T01, T11}, 16 bytes per texel.
 typedef _Float16 apd_h2 __attribute__((ext_vector_type(2)));
-typedef uint2 apd_u2_a4 __attribute__((aligned(4)));
+struct __attribute__((aligned(4))) apd_u2_a4 { uint32_t x, y; };  // 8-byte load at 4-byte alignment
 template <bool F16>
 struct SrcTex {
     const APD_G void *base;
@@ -339,10 +339,17 @@ struct SrcTex {
         if constexpr (F16) base = (const APD_G void *)(a.pairs + (size_t)(s - 1) * a.qstride);
         else base = (const APD_G void *)(a.quad + (size_t)(s - 1) * a.qstride);
     }
+#ifdef APD_F16_QUAD  // experiment: aligned fp16 quads (8 B per texel, pitch W+1)
+    static __device__ __forceinline__ uint32_t pitch(int W) { return (uint32_t)(W + 1); }
+    __device__ __forceinline__ float4 fetch(uint32_t idx) const {
+        if constexpr (F16) {
+            const uint2 v = ((const APD_G uint2 *)base)[idx];
+#else
     static __device__ __forceinline__ uint32_t pitch(int W) { return (uint32_t)(F16 ? W + 2 : W + 1); }
     __device__ __forceinline__ float4 fetch(uint32_t idx) const {
         if constexpr (F16) {
             const apd_u2_a4 v = *(const APD_G apd_u2_a4 *)((const APD_G uint32_t *)base + idx);
+#endif
             const apd_h2 c0 = __builtin_bit_cast(apd_h2, v.x);  // {T(ix,iy), T(ix,iy+1)}
             const apd_h2 c1 = __builtin_bit_cast(apd_h2, v.y);  // {T(ix+1,iy), T(ix+1,iy+1)}
             return make_float4((float)c0.x, (float)c1.x, (float)c0.y, (float)c1.y);
@@ -369,26 +376,30 @@ __device__ __forceinline__ float ncc_finalize(float sr, float srr, float ss, flo
 }
 
 // Reference-side window of ComputeBilateralNCCOld (6x6, radius 5, step 2): fixed per pixel, so it is
-// gathered once per pixel and kept in VGPRs across all 14*N NCC evaluations of a sweep.
+// gathered once per pixel into LDS (one copy per pixel, each of the pixel's N lanes fetching a share)
+// and read back by broadcast across all 14*N NCC evaluations of a sweep.
 struct RefWin {
-    float r[36];
+    const float *r;    // 36 values in LDS, column-major (i*6 + j)
     float mean, var;   // sum_ref/36 and sum_ref_ref/36 - mean^2, same op order as the oracle
 };
-__device__ __forceinline__ void build_refwin(const Args &a, int px, int py, RefWin &w) {
+__device__ __forceinline__ void build_refwin(const Args &a, int px, int py, float *lds_r, int v, int N, RefWin &w) {
+    for (int k = v; k < 36; k += N) {
+        const int i = k / 6, j = k - 6 * (k / 6);
+        lds_r[k] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
+    }
+    // LDS operations of one wavefront execute in order: the pixel's other lanes see the writes.
+    __builtin_amdgcn_wave_barrier();
     float sr = 0.0f, srr = 0.0f;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            float r = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
-            w.r[i * 6 + j] = r;
-            sr += r;
-            srr = fmaf(r, r, srr);
-        }
+    for (int k = 0; k < 36; ++k) {
+        const float r = lds_r[k];
+        sr += r;
+        srr = fmaf(r, r, srr);
     }
     const float inv = 1.0f / 36.0f;
     sr *= inv;
     srr *= inv;
+    w.r = lds_r;
     w.mean = sr;
     w.var = fmaf(-sr, sr, srr);
 }
@@ -420,6 +431,118 @@ __device__ __noinline__ float ncc_old_sa(const APD_G Args *ap, int px, int py, i
     return ncc_finalize(sr, srr, ss, sss, srs, wsum);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fast window taps. Same arithmetic as project() + quad_tap() + bilerp(), restated for throughput:
+//   * 1/Z = v_rcp_f32 + one Newton step, r' = fma(fma(-Z, r, 1), r, r). tools/rcp_exhaustive.hip
+//     checks on gfx950 that this equals the IEEE quotient 1.0f/Z for EVERY significand and both signs
+//     over the exponent range the window guard below admits, so it is the same value, not an
+//     approximation. Windows the guard rejects (Z near 0 or huge anywhere in the window) take the
+//     IEEE path (ncc_old_ieee).
+//   * (X, Y) pairs, the 1/256 fixed-point step and the bilinear lerps use packed fp32 (v_pk_fma_f32,
+//     v_pk_mul_f32, v_pk_add_f32): per-component IEEE results identical to the scalar ops.
+//   * the tap address is a 32-bit byte offset from the (wave-uniform) texel base: the -1 of the
+//     quad index is folded into the per-view offset.
+// ---------------------------------------------------------------------------------------------
+typedef float apd_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ apd_f2 pk_fma(apd_f2 a, apd_f2 b, apd_f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ float rcp_newton(float z) {
+    const float r = __builtin_amdgcn_rcpf(z);
+    return fmaf(fmaf(-z, r, 1.0f), r, r);
+}
+// true iff every tap Z of the window [x0, x0+10] x [y0, y0+10] is provably in the range where
+// rcp_newton is exact: corners of one sign with |Z| >= max(2^-100, 2^-16 S) and S <= 2^100, S being a
+// bound on the magnitude of the terms of Z (rounding error of any tap's Z is < 2^-21 S, and Z is
+// affine, so every tap's computed Z keeps the corners' sign and |Z| >= 2^-101). NaN -> false.
+__device__ __forceinline__ bool window_rcp_ok(const Hom &Hm, float x0, float y0) {
+    const float x1 = x0 + 10.0f, y1 = y0 + 10.0f;
+    const float z00 = fmaf(Hm.h[7], y0, fmaf(Hm.h[6], x0, Hm.h[8]));
+    const float z10 = fmaf(Hm.h[7], y0, fmaf(Hm.h[6], x1, Hm.h[8]));
+    const float z01 = fmaf(Hm.h[7], y1, fmaf(Hm.h[6], x0, Hm.h[8]));
+    const float z11 = fmaf(Hm.h[7], y1, fmaf(Hm.h[6], x1, Hm.h[8]));
+    const float S = fmaf(fabsf(Hm.h[6]), fmaxf(fabsf(x0), fabsf(x1)),
+                         fmaf(fabsf(Hm.h[7]), fmaxf(fabsf(y0), fabsf(y1)), fabsf(Hm.h[8])));
+    const float lo = fmaxf(0x1p-100f, S * 0x1p-16f);
+    const float mn = fminf(fminf(z00, z10), fminf(z01, z11));
+    const float mx = fmaxf(fmaxf(z00, z10), fmaxf(z01, z11));
+    return (mn >= lo || mx <= -lo) && S <= 0x1p100f;
+}
+template <bool F16>
+struct FastTex {
+    const APD_G char *base;  // wave-uniform: a.pairs / a.quad
+    uint32_t vbase;          // byte offset of view s, minus one row and one texel of the pitch
+    uint32_t W1;             // pitch in texels
+    float Wm1, Hm1;
+    static constexpr uint32_t SHIFT = F16 ? 2u : 4u;  // log2 bytes per texel
+    template <class AT>
+    __device__ __forceinline__ FastTex(const AT &a, int s) {
+        base = F16 ? (const APD_G char *)a.pairs : (const APD_G char *)a.quad;
+        W1 = SrcTex<F16>::pitch(a.W);
+        vbase = (uint32_t)(((uint32_t)(s - 1) * (uint32_t)a.qstride - W1 - 1u) << SHIFT);
+        Wm1 = (float)(a.W - 1);
+        Hm1 = (float)(a.H - 1);
+    }
+    // one bilinear sample at (X/Z, Y/Z) given iz = 1/Z: identical to sample_src(X*iz, Y*iz)
+    struct Tap { uint32_t off; apd_f2 f; };
+    __device__ __forceinline__ Tap tap(apd_f2 XY, float iz) const {
+        apd_f2 p = XY * iz;
+        p.x = fminf(fmaxf(p.x, -1.0f), Wm1);
+        p.y = fminf(fmaxf(p.y, -1.0f), Hm1);
+        const apd_f2 q = pk_fma(p, (apd_f2){256.0f, 256.0f}, (apd_f2){512.5f, 512.5f});
+        const int qx = (int)q.x, qy = (int)q.y;
+        Tap t;
+        t.off = ((__umul24((uint32_t)qy >> 8, W1) + ((uint32_t)qx >> 8)) << SHIFT) + vbase;
+        t.f = (apd_f2){(float)(qx & 255), (float)(qy & 255)} * 0.00390625f;
+        return t;
+    }
+    __device__ __forceinline__ float sample(const Tap &t) const {
+        float4 q;
+        if constexpr (F16) {
+            const apd_u2_a4 v = *(const APD_G apd_u2_a4 *)(base + t.off);
+            const apd_h2 c0 = __builtin_bit_cast(apd_h2, v.x);
+            const apd_h2 c1 = __builtin_bit_cast(apd_h2, v.y);
+            q = make_float4((float)c0.x, (float)c1.x, (float)c0.y, (float)c1.y);
+        } else {
+            q = *(const APD_G float4 *)(base + t.off);
+        }
+        // top = fma(ax, T10 - T00, T00), bot = fma(ax, T11 - T01, T01), v = fma(ay, bot - top, top)
+        const apd_f2 lo = (apd_f2){q.x, q.z}, hi = (apd_f2){q.y, q.w};
+        const apd_f2 tb = pk_fma((apd_f2){t.f.x, t.f.x}, hi - lo, lo);
+        return fmaf(t.f.y, tb.y - tb.x, tb.x);
+    }
+};
+
+// IEEE-division statement of the ComputeBilateralNCCOld window sum (taken only for windows that
+// window_rcp_ok rejects).
+template <bool F16>
+__device__ __noinline__ apd_f2 ncc_old_ieee(const APD_G Args *ap, int px, int py, int s, const Hom &Hm,
+                                            const float *r, float *sss_out) {
+    const APD_G Args &a = *ap;
+    const SrcTex<F16> Q(a, s);
+    const float Wm1 = (float)(a.W - 1), Hm1 = (float)(a.H - 1);
+    const uint32_t W1 = SrcTex<F16>::pitch(a.W);
+    float ss = 0.0f, sss = 0.0f, srs = 0.0f;
+    for (int i = 0; i < 6; ++i) {
+        const float x = (float)(px - 5 + 2 * i);
+        const float cx = fmaf(Hm.h[0], x, Hm.h[2]);
+        const float cy = fmaf(Hm.h[3], x, Hm.h[5]);
+        const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
+        for (int j = 0; j < 6; ++j) {
+            const float y = (float)(py - 5 + 2 * j);
+            const float X = fmaf(Hm.h[1], y, cx);
+            const float Y = fmaf(Hm.h[4], y, cy);
+            const float Z = fmaf(Hm.h[7], y, cz);
+            const float iz = 1.0f / Z;
+            const QuadTap t = quad_tap(Wm1, Hm1, W1, X * iz, Y * iz);
+            const float v = bilerp(Q.fetch(t.idx), t.ax, t.ay);
+            ss += v;
+            sss = fmaf(v, v, sss);
+            srs = fmaf(r[i * 6 + j], v, srs);
+        }
+    }
+    *sss_out = sss;
+    return (apd_f2){ss, srs};
+}
+
 // ComputeBilateralNCCOld (APD.cu:596-721) for source view s (1..N), plane in the ref frame.
 template <bool F16>
 __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, float4 pl, const RefWin &rw) {
@@ -432,46 +555,39 @@ __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, f
         int pidx = clampi((int)fmaf(pty, (float)W, ptx), 0, a.HW - 1);
         if (a.sa[pidx] != 0) return ncc_old_sa<F16>(a.self, px, py, s, Hm, a.sa[py * W + px]);
     }
-    const SrcTex<F16> Q(a, s);
-    const float Wm1 = (float)(W - 1), Hm1 = (float)(H - 1);
-    const uint32_t W1 = SrcTex<F16>::pitch(W);
     float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-    // One window column (6 taps) per step: all 6 gathers are issued before the first is consumed.
+    if (window_rcp_ok(Hm, (float)(px - 5), (float)(py - 5))) {
+        const FastTex<F16> T(a, s);
+        // One window column (6 taps) per step: all 6 gathers are issued before the first is consumed.
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const float x = (float)(px - 5 + 2 * i);
-        const float cx = fmaf(Hm.h[0], x, Hm.h[2]);
-        const float cy = fmaf(Hm.h[3], x, Hm.h[5]);
-        const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
-        QuadTap t[6];
+        for (int i = 0; i < 6; ++i) {
+            const float x = (float)(px - 5 + 2 * i);
+            const apd_f2 cxy = {fmaf(Hm.h[0], x, Hm.h[2]), fmaf(Hm.h[3], x, Hm.h[5])};
+            const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
+            typename FastTex<F16>::Tap t[6];
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            const float y = (float)(py - 5 + 2 * j);
-            const float X = fmaf(Hm.h[1], y, cx);
-            const float Y = fmaf(Hm.h[4], y, cy);
-            const float Z = fmaf(Hm.h[7], y, cz);
-#ifdef APD_ABLATE_NO_DIV  // timing-only ablation build: no IEEE reciprocal
-            const float iz = Z;
-#else
-            const float iz = 1.0f / Z;
-#endif
-            t[j] = quad_tap(Wm1, Hm1, W1, X * iz, Y * iz);
+            for (int j = 0; j < 6; ++j) {
+                const float y = (float)(py - 5 + 2 * j);
+                const apd_f2 XY = pk_fma((apd_f2){Hm.h[1], Hm.h[4]}, (apd_f2){y, y}, cxy);
+                const float Z = fmaf(Hm.h[7], y, cz);
+                t[j] = T.tap(XY, rcp_newton(Z));
+            }
+            float v[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) v[j] = T.sample(t[j]);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                ss += v[j];
+                // (sss, srs) = (fma(v, v, sss), fma(r, v, srs))
+                const apd_f2 acc = pk_fma((apd_f2){v[j], rw.r[i * 6 + j]}, (apd_f2){v[j], v[j]}, (apd_f2){sss, srs});
+                sss = acc.x;
+                srs = acc.y;
+            }
         }
-        float4 q[6];
-#pragma unroll
-#ifdef APD_ABLATE_SAME_ADDR  // timing-only ablation build: every gather hits a 1 KiB footprint
-        for (int j = 0; j < 6; ++j) q[j] = Q.fetch(t[j].idx & 63);
-#else
-        for (int j = 0; j < 6; ++j) q[j] = Q.fetch(t[j].idx);
-#endif
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            const float v = bilerp(q[j], t[j].ax, t[j].ay);
-            const float r = rw.r[i * 6 + j];
-            ss += v;
-            sss = fmaf(v, v, sss);
-            srs = fmaf(r, v, srs);
-        }
+    } else {
+        const apd_f2 r = ncc_old_ieee<F16>(a.self, px, py, s, Hm, rw.r, &sss);
+        ss = r.x;
+        srs = r.y;
     }
     const float inv = 1.0f / 36.0f;
     ss *= inv; sss *= inv; srs *= inv;

@@ -61,6 +61,15 @@ __device__ __forceinline__ Group make_group(int N, int count, int wave) {
     G.gmask = (N >= 64) ? ~0ull : ((1ull << N) - 1ull);
     return G;
 }
+// Dynamic LDS of the view-group kernels: per wavefront slot, per pixel of the wave, 36 floats of
+// reference window (RefWin) [+ 61 floats of DepthToWeak cost curve].
+extern __shared__ float apd_dyn_lds[];
+__device__ __forceinline__ float *lds_slot(const Group &G, int P, int floats_per_px, int base_floats) {
+    return apd_dyn_lds + base_floats + ((threadIdx.x >> 6) * P + G.slot) * floats_per_px;
+}
+static inline size_t group_lds_bytes(int N, int floats_per_px) {
+    return (size_t)(BLOCK / WAVE) * (WAVE / N) * floats_per_px * sizeof(float);
+}
 __device__ __forceinline__ uint32_t group_bits(bool pred, const Group &G) {
     unsigned long long m = __ballot(pred);
     return (uint32_t)((m >> G.base) & G.gmask);
@@ -107,6 +116,30 @@ __global__ __launch_bounds__(BLOCK) void k_build_pairs(const float *__restrict__
         pairs[(size_t)v * pstride + r] = __builtin_bit_cast(uint32_t, h);
     }
 }
+#ifdef APD_F16_QUAD
+// experiment: aligned fp16 quads H[(iy+1)*(W+1)+(ix+1)] = {pair(ix,iy), pair(ix+1,iy)}; pstride in uint32
+__global__ __launch_bounds__(BLOCK) void k_build_hquads(const float *__restrict__ imgs, uint32_t *__restrict__ q,
+                                                      int W, int H, int N, size_t pstride) {
+    const size_t per = (size_t)(W + 1) * (H + 1);
+    const size_t total = per * N;
+    for (size_t i = blockIdx.x * (size_t)BLOCK + threadIdx.x; i < total; i += (size_t)gridDim.x * BLOCK) {
+        const int v = (int)(i / per);
+        const size_t r = i - (size_t)v * per;
+        const int iy = (int)(r / (W + 1)) - 1;
+        const int ix = (int)(r % (W + 1)) - 1;
+        const float *T = imgs + (size_t)(v + 1) * W * H;
+        const int x0 = clampi(ix, 0, W - 1), x1 = clampi(ix + 1, 0, W - 1);
+        const int y0 = clampi(iy, 0, H - 1), y1 = clampi(iy + 1, 0, H - 1);
+        apd_h2 h0, h1;
+        h0.x = (_Float16)T[y0 * W + x0];
+        h0.y = (_Float16)T[y1 * W + x0];
+        h1.x = (_Float16)T[y0 * W + x1];
+        h1.y = (_Float16)T[y1 * W + x1];
+        uint2 o = make_uint2(__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1));
+        *(uint2 *)(q + (size_t)v * pstride + 2 * r) = o;
+    }
+}
+#endif
 
 // Ordered compaction, one workgroup per image row.
 //   mode 0: colour `colour`, weak != WEAK, y < row_limit   (Strong sweep / filter pixel set)
@@ -412,7 +445,7 @@ __global__ __launch_bounds__(BLOCK) void k_ransac_fit(Args a, int iter) {
     const int W = a.W;
     const int py = c / W, px = c - py * W;
     const APD_G Cam &cam = a.cams[0];
-    const APD_G APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
+    const APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
     int sx[8], sy[8], cnt = 0;
     float s3[8][3], X[3];
     for (int i = 1; i < 9; ++i) {
@@ -492,7 +525,7 @@ __global__ __launch_bounds__(BLOCK) void k_random_init(Args a) {
         cv = ncc_new<F16>(a.self, px, py, s, pl);
     } else {
         RefWin rw;
-        build_refwin(a, px, py, rw);
+        build_refwin(a, px, py, lds_slot(G, WAVE / N, 36, 0), G.v, N, rw);
         cv = ncc_old<F16>(a, px, py, s, pl, rw);
     }
     // stable top-k of the N costs (insertion sort, APD.cu:3-12, 754-769)
@@ -694,7 +727,7 @@ __global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a,
     }
 
     RefWin rw;
-    build_refwin(a, px, py, rw);
+    build_refwin(a, px, py, lds_slot(G, WAVE / N, 36, 0), G.v, N, rw);
     const bool geom_imp = a.geom && a.impetus;
     const float gf = a.gf;
     const float4 cur = a.plane[c];
@@ -818,7 +851,7 @@ __global__ __launch_bounds__(BLOCK) void k_sweep_weak(Args a, const int *__restr
     const int py = c / W, px = c - py * W;
     const int s = G.v + 1;
     const APD_G Cam &cam0 = a.cams[0];
-    const APD_G APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
+    const APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
     const bool geom = a.geom != 0;
     const float gf = a.gf;
     const float4 cur = a.plane[c];
@@ -1032,7 +1065,6 @@ __global__ __launch_bounds__(BLOCK) void k_filter(Args a, const int *__restrict_
 // The cost curve of each pixel is staged in LDS for the peak analysis.
 template <bool F16>
 __global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
-    extern __shared__ float lds_curve[];
     const int N = a.N, W = a.W, H = a.H;
     const int P = WAVE / N;
     const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
@@ -1041,7 +1073,7 @@ __global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
     const int py = c / W, px = c - py * W;
     const int s = G.v + 1;
     const APD_G Cam &cam0 = a.cams[0];
-    float *pc = lds_curve + ((threadIdx.x >> 6) * P + G.slot) * 61;
+    float *pc = lds_slot(G, P, 61, 0);
     const bool border = px < 6 || py < 6 || px >= W - 6 || py >= H - 6;
     const float4 pl = to_ref(cam0, a.plane[c]);
     const float od = pl.w;
@@ -1069,7 +1101,7 @@ __global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
     if (active) base /= (float)valid;
     const float disp = cam0.K[0] * base / od;
     RefWin rw;
-    build_refwin(a, px, py, rw);
+    build_refwin(a, px, py, lds_slot(G, P, 36, (BLOCK / WAVE) * P * 61), G.v, N, rw);
     const bool geom = a.geom != 0;
     const float gf = a.gf;
 #pragma unroll 1
@@ -1180,7 +1212,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_refine(Args a) {
     const bool geom = a.geom != 0;
     const float gf = a.gf;
     RefWin rw;
-    build_refwin(a, px, py, rw);
+    build_refwin(a, px, py, lds_slot(G, WAVE / N, 36, 0), G.v, N, rw);
     float mydist, tc0 = 0.0f;
     {
         const APD_G Cam &sc = a.cams[s];
@@ -1294,7 +1326,7 @@ struct apd_ctx {
 static int ensure(apd_ctx *ctx, DevBuf &b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.bytes >= bytes) return APD_OK;
-    if (b.p) hipFree(b.p);
+    if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
     if (hipMalloc(&b.p, bytes) != hipSuccess) {
@@ -1417,23 +1449,23 @@ apd_ctx *apd_create(int32_t device) {
         delete ctx;
         return nullptr;
     }
-    for (auto &e : ctx->ev) hipEventCreate(&e);
+    for (auto &e : ctx->ev) (void)hipEventCreate(&e);
     return ctx;
 }
 
 void apd_destroy(apd_ctx *ctx) {
     if (!ctx) return;
-    hipSetDevice(ctx->device);
-    hipStreamSynchronize(ctx->stream);
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
     DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
                       &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs};
     for (DevBuf *b : bufs)
-        if (b->p) hipFree(b->p);
-    for (auto &e : ctx->ev) hipEventDestroy(e);
-    for (auto &pe : ctx->prof_ev) { hipEventDestroy(pe.first); hipEventDestroy(pe.second); }
-    hipStreamDestroy(ctx->stream);
+        if (b->p) (void)hipFree(b->p);
+    for (auto &e : ctx->ev) (void)hipEventDestroy(e);
+    for (auto &pe : ctx->prof_ev) { (void)hipEventDestroy(pe.first); (void)hipEventDestroy(pe.second); }
+    (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
 
@@ -1441,7 +1473,7 @@ const char *apd_last_error(const apd_ctx *ctx) { return ctx ? ctx->err.c_str() :
 
 int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     if (!ctx || !pb) return APD_EINVAL;
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     ctx->loaded = ctx->prepared = false;
     const int W = pb->width, H = pb->height, NI = pb->num_images;
     if (NI > APD_MAX_IMAGES) { ctx->err = "num_images > 32"; return APD_ETOOMANYVIEWS; }
@@ -1467,7 +1499,11 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
             if ((float)(_Float16)img[k] != img[k]) { tex_f16 = false; break; }
         }
     }
+#ifdef APD_F16_QUAD
+    const size_t qstride = tex_f16 ? 2 * (size_t)(W + 1) * (H + 1) : (size_t)(W + 1) * (H + 1);
+#else
     const size_t qstride = tex_f16 ? (size_t)(W + 2) * (H + 1) : (size_t)(W + 1) * (H + 1);
+#endif
     int st;
     if ((st = ensure(ctx, ctx->imgs, HW * NI * sizeof(float)))) return st;
     if ((st = ensure(ctx, ctx->quad, qstride * N * (tex_f16 ? sizeof(uint32_t) : sizeof(float4))))) return st;
@@ -1600,6 +1636,12 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     {
         const size_t total = qstride * N;
         unsigned g = (unsigned)std::min<size_t>(blocks_for(total, BLOCK), 65535u * 8u);
+#ifdef APD_F16_QUAD
+        if (tex_f16)
+            hipLaunchKernelGGL(k_build_hquads, dim3(g), dim3(BLOCK), 0, s, (const float *)ctx->imgs.p,
+                               (uint32_t *)ctx->quad.p, W, H, N, qstride);
+        else
+#endif
         if (tex_f16)
             hipLaunchKernelGGL(k_build_pairs, dim3(g), dim3(BLOCK), 0, s, (const float *)ctx->imgs.p,
                                (uint32_t *)ctx->quad.p, W, H, N, qstride);
@@ -1658,12 +1700,12 @@ static int *list_ptr(apd_ctx *ctx, int which) {
 
 int32_t apd_stage_prepare(apd_ctx *ctx) {
     if (!ctx || !ctx->loaded) return APD_ESTATE;
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     Args &a = ctx->args;
     hipStream_t s = ctx->stream;
     const unsigned gpx = blocks_for((size_t)a.HW, BLOCK);
     int st;
-    hipEventRecord(ctx->ev[0], s);
+    (void)hipEventRecord(ctx->ev[0], s);
     if (a.use_apd) {
         // anchors_map from the input WEAK mask (APD.cpp:627-640)
         if ((st = build_list(ctx, 2, 0, (int *)ctx->amap.p, (int *)ctx->totals.p + 4))) return st;
@@ -1672,7 +1714,7 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         hipLaunchKernelGGL(k_neighbour_update, dim3(gpx), dim3(BLOCK), 0, s, a);
         if ((st = check_launch(ctx, "anchors"))) return st;
     }
-    hipEventRecord(ctx->ev[1], s);
+    (void)hipEventRecord(ctx->ev[1], s);
     // pixel lists for the sweeps (after NeigbourUpdate)
     {
         int *tot = (int *)ctx->totals.p;
@@ -1687,18 +1729,18 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
             if ((st = build_tile_list(ctx, modes[i][0], modes[i][1], list_ptr(ctx, i), tot + i))) return st;
         }
     }
-    hipEventRecord(ctx->ev[2], s);
-    LAUNCH_TEX(k_random_init, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), 0, s, a);
+    (void)hipEventRecord(ctx->ev[2], s);
+    LAUNCH_TEX(k_random_init, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);
     HIP_OK(ctx, hipMemcpyAsync(ctx->sel.p, ctx->sel2.p, (size_t)a.HW * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     if ((st = check_launch(ctx, "k_random_init"))) return st;
-    hipEventRecord(ctx->ev[3], s);
+    (void)hipEventRecord(ctx->ev[3], s);
     ctx->prepared = true;
     return APD_OK;
 }
 
 int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
     if (!ctx || !ctx->prepared) return APD_ESTATE;
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     Args &a = ctx->args;
     hipStream_t s = ctx->stream;
     int st;
@@ -1707,14 +1749,14 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
         if (n <= 0) continue;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (ctx->prof) {
-            hipEventCreate(&e0);
-            hipEventCreate(&e1);
-            hipEventRecord(e0, s);
+            (void)hipEventCreate(&e0);
+            (void)hipEventCreate(&e1);
+            (void)hipEventRecord(e0, s);
         }
-        LAUNCH_TEX(k_sweep_strong, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
+        LAUNCH_TEX(k_sweep_strong, dim3(group_blocks(n, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a,
                            (const int *)list_ptr(ctx, colour), n, iter);
         if (ctx->prof) {
-            hipEventRecord(e1, s);
+            (void)hipEventRecord(e1, s);
             ctx->prof_ev.emplace_back(e0, e1);
             ctx->prof_pixels += n;
         }
@@ -1735,7 +1777,7 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
 
 int32_t apd_stage_finish(apd_ctx *ctx) {
     if (!ctx || !ctx->prepared) return APD_ESTATE;
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     Args a = ctx->args;
     hipStream_t s = ctx->stream;
     int st;
@@ -1750,47 +1792,48 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
     if (ctx->want_curve && ctx->curve.p) a.curve = devptr<decltype(a.curve)>(ctx->curve.p);
     {
         const int P = WAVE / a.N;
-        const size_t lds = (size_t)(BLOCK / WAVE) * P * 61 * sizeof(float);
+        const size_t lds = group_lds_bytes(a.N, 61 + 36);
+        (void)P;
         LAUNCH_TEX(k_depth_to_weak, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), lds, s, a);
     }
     if (a.geom || a.use_apd) hipLaunchKernelGGL(k_confidence, dim3(gpx), dim3(BLOCK), 0, s, a);
-    LAUNCH_TEX(k_local_refine, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), 0, s, a);
+    LAUNCH_TEX(k_local_refine, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);
     if ((st = check_launch(ctx, "finish"))) return st;
     return APD_OK;
 }
 
 int32_t apd_run_patchmatch(apd_ctx *ctx) {
     if (!ctx || !ctx->loaded) return APD_ESTATE;
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     int st;
     hipStream_t s = ctx->stream;
     if ((st = apd_stage_prepare(ctx))) return st;
     const int iters = ctx->params.max_iterations;
     for (int i = 0; i < iters; ++i) {
-        if (i < 8) hipEventRecord(ctx->ev[4 + i], s);
+        if (i < 8) (void)hipEventRecord(ctx->ev[4 + i], s);
         if ((st = apd_stage_iteration(ctx, i))) return st;
     }
-    hipEventRecord(ctx->ev[12], s);
+    (void)hipEventRecord(ctx->ev[12], s);
     if ((st = apd_stage_finish(ctx))) return st;
-    hipEventRecord(ctx->ev[13], s);
+    (void)hipEventRecord(ctx->ev[13], s);
     HIP_OK(ctx, hipStreamSynchronize(s));
     apd_timing &t = ctx->timing;
     memset(&t, 0, sizeof(t));
-    hipEventElapsedTime(&t.total_ms, ctx->ev[0], ctx->ev[13]);
-    hipEventElapsedTime(&t.anchors_ms, ctx->ev[0], ctx->ev[1]);
-    hipEventElapsedTime(&t.init_ms, ctx->ev[2], ctx->ev[3]);
-    hipEventElapsedTime(&t.sweep_ms, ctx->ev[3], ctx->ev[12]);
-    hipEventElapsedTime(&t.post_ms, ctx->ev[12], ctx->ev[13]);
+    (void)hipEventElapsedTime(&t.total_ms, ctx->ev[0], ctx->ev[13]);
+    (void)hipEventElapsedTime(&t.anchors_ms, ctx->ev[0], ctx->ev[1]);
+    (void)hipEventElapsedTime(&t.init_ms, ctx->ev[2], ctx->ev[3]);
+    (void)hipEventElapsedTime(&t.sweep_ms, ctx->ev[3], ctx->ev[12]);
+    (void)hipEventElapsedTime(&t.post_ms, ctx->ev[12], ctx->ev[13]);
     const int ni = std::min(iters, 8);
     for (int i = 0; i < ni; ++i)
-        hipEventElapsedTime(&t.iter_ms[i], ctx->ev[4 + i], (i + 1 < ni) ? ctx->ev[5 + i] : ctx->ev[12]);
+        (void)hipEventElapsedTime(&t.iter_ms[i], ctx->ev[4 + i], (i + 1 < ni) ? ctx->ev[5 + i] : ctx->ev[12]);
     t.iterations = iters;
     return APD_OK;
 }
 
 int32_t apd_synchronize(apd_ctx *ctx) {
     if (!ctx) return APD_EINVAL;
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
     return APD_OK;
 }
@@ -1798,7 +1841,7 @@ int32_t apd_synchronize(apd_ctx *ctx) {
 int32_t apd_get_results(apd_ctx *ctx, const apd_outputs *out) {
     if (!ctx || !out) return APD_EINVAL;
     if (!ctx->loaded) return APD_ESTATE;
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     hipStream_t s = ctx->stream;
     const Args &a = ctx->args;
     const size_t HW = (size_t)a.HW;
@@ -1827,9 +1870,9 @@ int32_t apd_get_timing(apd_ctx *ctx, apd_timing *timing) {
 
 int32_t apd_profile_reset(apd_ctx *ctx, int32_t enable) {
     if (!ctx) return APD_EINVAL;
-    hipSetDevice(ctx->device);
-    hipStreamSynchronize(ctx->stream);
-    for (auto &pe : ctx->prof_ev) { hipEventDestroy(pe.first); hipEventDestroy(pe.second); }
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto &pe : ctx->prof_ev) { (void)hipEventDestroy(pe.first); (void)hipEventDestroy(pe.second); }
     ctx->prof_ev.clear();
     ctx->prof_pixels = 0;
     ctx->prof = enable != 0;
@@ -1838,12 +1881,12 @@ int32_t apd_profile_reset(apd_ctx *ctx, int32_t enable) {
 
 int32_t apd_profile_query(apd_ctx *ctx, double *sweep_ms_total, int64_t *sweep_launches, int64_t *sweep_pixels) {
     if (!ctx) return APD_EINVAL;
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
     double tot = 0.0;
     for (auto &pe : ctx->prof_ev) {
         float ms = 0.0f;
-        hipEventElapsedTime(&ms, pe.first, pe.second);
+        (void)hipEventElapsedTime(&ms, pe.first, pe.second);
         tot += ms;
     }
     if (sweep_ms_total) *sweep_ms_total = tot;
