@@ -339,17 +339,10 @@ struct SrcTex {
         if constexpr (F16) base = (const APD_G void *)(a.pairs + (size_t)(s - 1) * a.qstride);
         else base = (const APD_G void *)(a.quad + (size_t)(s - 1) * a.qstride);
     }
-#ifdef APD_F16_QUAD  // experiment: aligned fp16 quads (8 B per texel, pitch W+1)
-    static __device__ __forceinline__ uint32_t pitch(int W) { return (uint32_t)(W + 1); }
-    __device__ __forceinline__ float4 fetch(uint32_t idx) const {
-        if constexpr (F16) {
-            const uint2 v = ((const APD_G uint2 *)base)[idx];
-#else
     static __device__ __forceinline__ uint32_t pitch(int W) { return (uint32_t)(F16 ? W + 2 : W + 1); }
     __device__ __forceinline__ float4 fetch(uint32_t idx) const {
         if constexpr (F16) {
             const apd_u2_a4 v = *(const APD_G apd_u2_a4 *)((const APD_G uint32_t *)base + idx);
-#endif
             const apd_h2 c0 = __builtin_bit_cast(apd_h2, v.x);  // {T(ix,iy), T(ix,iy+1)}
             const apd_h2 c1 = __builtin_bit_cast(apd_h2, v.y);  // {T(ix+1,iy), T(ix+1,iy+1)}
             return make_float4((float)c0.x, (float)c1.x, (float)c0.y, (float)c1.y);

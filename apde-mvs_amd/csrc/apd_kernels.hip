@@ -116,30 +116,6 @@ __global__ __launch_bounds__(BLOCK) void k_build_pairs(const float *__restrict__
         pairs[(size_t)v * pstride + r] = __builtin_bit_cast(uint32_t, h);
     }
 }
-#ifdef APD_F16_QUAD
-// experiment: aligned fp16 quads H[(iy+1)*(W+1)+(ix+1)] = {pair(ix,iy), pair(ix+1,iy)}; pstride in uint32
-__global__ __launch_bounds__(BLOCK) void k_build_hquads(const float *__restrict__ imgs, uint32_t *__restrict__ q,
-                                                      int W, int H, int N, size_t pstride) {
-    const size_t per = (size_t)(W + 1) * (H + 1);
-    const size_t total = per * N;
-    for (size_t i = blockIdx.x * (size_t)BLOCK + threadIdx.x; i < total; i += (size_t)gridDim.x * BLOCK) {
-        const int v = (int)(i / per);
-        const size_t r = i - (size_t)v * per;
-        const int iy = (int)(r / (W + 1)) - 1;
-        const int ix = (int)(r % (W + 1)) - 1;
-        const float *T = imgs + (size_t)(v + 1) * W * H;
-        const int x0 = clampi(ix, 0, W - 1), x1 = clampi(ix + 1, 0, W - 1);
-        const int y0 = clampi(iy, 0, H - 1), y1 = clampi(iy + 1, 0, H - 1);
-        apd_h2 h0, h1;
-        h0.x = (_Float16)T[y0 * W + x0];
-        h0.y = (_Float16)T[y1 * W + x0];
-        h1.x = (_Float16)T[y0 * W + x1];
-        h1.y = (_Float16)T[y1 * W + x1];
-        uint2 o = make_uint2(__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1));
-        *(uint2 *)(q + (size_t)v * pstride + 2 * r) = o;
-    }
-}
-#endif
 
 // Ordered compaction, one workgroup per image row.
 //   mode 0: colour `colour`, weak != WEAK, y < row_limit   (Strong sweep / filter pixel set)
@@ -1499,11 +1475,7 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
             if ((float)(_Float16)img[k] != img[k]) { tex_f16 = false; break; }
         }
     }
-#ifdef APD_F16_QUAD
-    const size_t qstride = tex_f16 ? 2 * (size_t)(W + 1) * (H + 1) : (size_t)(W + 1) * (H + 1);
-#else
     const size_t qstride = tex_f16 ? (size_t)(W + 2) * (H + 1) : (size_t)(W + 1) * (H + 1);
-#endif
     int st;
     if ((st = ensure(ctx, ctx->imgs, HW * NI * sizeof(float)))) return st;
     if ((st = ensure(ctx, ctx->quad, qstride * N * (tex_f16 ? sizeof(uint32_t) : sizeof(float4))))) return st;
@@ -1636,12 +1608,6 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     {
         const size_t total = qstride * N;
         unsigned g = (unsigned)std::min<size_t>(blocks_for(total, BLOCK), 65535u * 8u);
-#ifdef APD_F16_QUAD
-        if (tex_f16)
-            hipLaunchKernelGGL(k_build_hquads, dim3(g), dim3(BLOCK), 0, s, (const float *)ctx->imgs.p,
-                               (uint32_t *)ctx->quad.p, W, H, N, qstride);
-        else
-#endif
         if (tex_f16)
             hipLaunchKernelGGL(k_build_pairs, dim3(g), dim3(BLOCK), 0, s, (const float *)ctx->imgs.p,
                                (uint32_t *)ctx->quad.p, W, H, N, qstride);
