@@ -372,9 +372,28 @@ __device__ __forceinline__ float ncc_finalize(float sr, float srr, float ss, flo
 // gathered once per pixel into LDS (one copy per pixel, each of the pixel's N lanes fetching a share)
 // and read back by broadcast across all 14*N NCC evaluations of a sweep.
 struct RefWin {
-    const float *r;    // 36 values in LDS, column-major (i*6 + j)
+    const float *r;    // 36 values in LDS, column-major (i*6 + j), element k at r[k * stride]
     float mean, var;   // sum_ref/36 and sum_ref_ref/36 - mean^2, same op order as the oracle
 };
+// mean / variance of a reference window already in LDS (element k at r[k * RS])
+template <int RS>
+__device__ __forceinline__ RefWin refwin_from_lds(const float *r) {
+    float sr = 0.0f, srr = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 36; ++k) {
+        const float x = r[k * RS];
+        sr += x;
+        srr = fmaf(x, x, srr);
+    }
+    const float inv = 1.0f / 36.0f;
+    sr *= inv;
+    srr *= inv;
+    RefWin w;
+    w.r = r;
+    w.mean = sr;
+    w.var = fmaf(-sr, sr, srr);
+    return w;
+}
 __device__ __forceinline__ void build_refwin(const Args &a, int px, int py, float *lds_r, int v, int N, RefWin &w) {
     for (int k = v; k < 36; k += N) {
         const int i = k / 6, j = k - 6 * (k / 6);
@@ -445,7 +464,8 @@ __device__ __forceinline__ float rcp_newton(float z) {
 // true iff every tap Z of the window [x0, x0+10] x [y0, y0+10] is provably in the range where
 // rcp_newton is exact: corners of one sign with |Z| >= max(2^-100, 2^-16 S) and S <= 2^100, S being a
 // bound on the magnitude of the terms of Z (rounding error of any tap's Z is < 2^-21 S, and Z is
-// affine, so every tap's computed Z keeps the corners' sign and |Z| >= 2^-101). NaN -> false.
+// affine, so every tap's computed Z keeps the corners' sign and |Z| >= 2^-101); and |h0..h5| <= 2^100
+// so X, Y are finite. NaN -> false.
 __device__ __forceinline__ bool window_rcp_ok(const Hom &Hm, float x0, float y0) {
     const float x1 = x0 + 10.0f, y1 = y0 + 10.0f;
     const float z00 = fmaf(Hm.h[7], y0, fmaf(Hm.h[6], x0, Hm.h[8]));
@@ -457,12 +477,29 @@ __device__ __forceinline__ bool window_rcp_ok(const Hom &Hm, float x0, float y0)
     const float lo = fmaxf(0x1p-100f, S * 0x1p-16f);
     const float mn = fminf(fminf(z00, z10), fminf(z01, z11));
     const float mx = fmaxf(fmaxf(z00, z10), fmaxf(z01, z11));
-    return (mn >= lo || mx <= -lo) && S <= 0x1p100f;
+    // X and Y finite at every tap (so X/Z is never NaN and the med3 clamp below is exact)
+    const float hm = fmaxf(fmaxf(fmaxf(fabsf(Hm.h[0]), fabsf(Hm.h[1])), fmaxf(fabsf(Hm.h[2]), fabsf(Hm.h[3]))),
+                           fmaxf(fabsf(Hm.h[4]), fabsf(Hm.h[5])));
+    return (mn >= lo || mx <= -lo) && S <= 0x1p100f && hm <= 0x1p100f;
 }
-template <bool F16>
+// v_fma_mix_f32 with both fp16 operands taken from the low (lo) / high (hi) halves: fma(a, (float)b,
+// (float)c) in fp32 with exact fp16->fp32 conversions. Written as inline asm because the SLP
+// vectoriser otherwise converts all four halves and packs the two FMAs (more instructions).
+__device__ __forceinline__ float fma_mix_lo(float a, apd_h2 b, apd_h2 c) {
+    float d;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ float fma_mix_hi(float a, apd_h2 b, apd_h2 c) {
+    float d;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[0,1,1]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+// UNI: the source view is wave-uniform (view-major kernels) -> its base folds into the SGPR pointer.
+template <bool F16, bool UNI>
 struct FastTex {
-    const APD_G char *base;  // wave-uniform: a.pairs / a.quad
-    uint32_t vbase;          // byte offset of view s, minus one row and one texel of the pitch
+    const APD_G char *base;  // wave-uniform: a.pairs / a.quad (+ the view's offset when UNI)
+    uint32_t vbase;          // byte offset of view s (0 when UNI), minus one row and one texel of the pitch
     uint32_t W1;             // pitch in texels
     float Wm1, Hm1;
     static constexpr uint32_t SHIFT = F16 ? 2u : 4u;  // log2 bytes per texel
@@ -470,16 +507,25 @@ struct FastTex {
     __device__ __forceinline__ FastTex(const AT &a, int s) {
         base = F16 ? (const APD_G char *)a.pairs : (const APD_G char *)a.quad;
         W1 = SrcTex<F16>::pitch(a.W);
-        vbase = (uint32_t)(((uint32_t)(s - 1) * (uint32_t)a.qstride - W1 - 1u) << SHIFT);
+        const uint32_t vb = (uint32_t)(((uint32_t)(s - 1) * (uint32_t)a.qstride - W1 - 1u) << SHIFT);
+        if constexpr (UNI) {
+            base = (const APD_G char *)((F16 ? (const APD_G char *)a.pairs : (const APD_G char *)a.quad) +
+                                        ((int64_t)(s - 1) * (int64_t)a.qstride - (int64_t)W1 - 1) * (1 << SHIFT));
+            vbase = 0u;
+        } else {
+            vbase = vb;
+        }
         Wm1 = (float)(a.W - 1);
         Hm1 = (float)(a.H - 1);
     }
-    // one bilinear sample at (X/Z, Y/Z) given iz = 1/Z: identical to sample_src(X*iz, Y*iz)
+    // one bilinear sample at (X/Z, Y/Z) given iz = 1/Z: identical to sample_src(X*iz, Y*iz).
+    // Clamp with v_med3_f32: equal to fminf(fmaxf(x, -1), Wm1) for every non-NaN x (window_rcp_ok
+    // guarantees X, Y finite and Z finite non-zero, so X*iz is never NaN).
     struct Tap { uint32_t off; apd_f2 f; };
     __device__ __forceinline__ Tap tap(apd_f2 XY, float iz) const {
         apd_f2 p = XY * iz;
-        p.x = fminf(fmaxf(p.x, -1.0f), Wm1);
-        p.y = fminf(fmaxf(p.y, -1.0f), Hm1);
+        p.x = __builtin_amdgcn_fmed3f(p.x, -1.0f, Wm1);
+        p.y = __builtin_amdgcn_fmed3f(p.y, -1.0f, Hm1);
         const apd_f2 q = pk_fma(p, (apd_f2){256.0f, 256.0f}, (apd_f2){512.5f, 512.5f});
         const int qx = (int)q.x, qy = (int)q.y;
         Tap t;
@@ -488,19 +534,25 @@ struct FastTex {
         return t;
     }
     __device__ __forceinline__ float sample(const Tap &t) const {
-        float4 q;
         if constexpr (F16) {
+            // F16 storage is only selected for quarter-integer texels in [0, 256) (see apd_set_problem):
+            // the horizontal differences T10-T00, T11-T01 are then exact in fp16, so they are taken with
+            // one v_pk_add_f16 and fed to v_fma_mix_f32 (fp16 operands converted exactly) -- the same
+            // fp32 values and FMAs as bilerp() on the converted texels.
             const apd_u2_a4 v = *(const APD_G apd_u2_a4 *)(base + t.off);
-            const apd_h2 c0 = __builtin_bit_cast(apd_h2, v.x);
-            const apd_h2 c1 = __builtin_bit_cast(apd_h2, v.y);
-            q = make_float4((float)c0.x, (float)c1.x, (float)c0.y, (float)c1.y);
+            const apd_h2 c0 = __builtin_bit_cast(apd_h2, v.x);  // {T00, T01}
+            const apd_h2 c1 = __builtin_bit_cast(apd_h2, v.y);  // {T10, T11}
+            const apd_h2 dd = c1 - c0;
+            const float top = fma_mix_lo(t.f.x, dd, c0);  // fma(ax, T10 - T00, T00)
+            const float bot = fma_mix_hi(t.f.x, dd, c0);  // fma(ax, T11 - T01, T01)
+            return fmaf(t.f.y, bot - top, top);
         } else {
-            q = *(const APD_G float4 *)(base + t.off);
+            const float4 q = *(const APD_G float4 *)(base + t.off);
+            // top = fma(ax, T10 - T00, T00), bot = fma(ax, T11 - T01, T01), v = fma(ay, bot - top, top)
+            const apd_f2 lo = (apd_f2){q.x, q.z}, hi = (apd_f2){q.y, q.w};
+            const apd_f2 tb = pk_fma((apd_f2){t.f.x, t.f.x}, hi - lo, lo);
+            return fmaf(t.f.y, tb.y - tb.x, tb.x);
         }
-        // top = fma(ax, T10 - T00, T00), bot = fma(ax, T11 - T01, T01), v = fma(ay, bot - top, top)
-        const apd_f2 lo = (apd_f2){q.x, q.z}, hi = (apd_f2){q.y, q.w};
-        const apd_f2 tb = pk_fma((apd_f2){t.f.x, t.f.x}, hi - lo, lo);
-        return fmaf(t.f.y, tb.y - tb.x, tb.x);
     }
 };
 
@@ -508,7 +560,7 @@ struct FastTex {
 // window_rcp_ok rejects).
 template <bool F16>
 __device__ __noinline__ apd_f2 ncc_old_ieee(const APD_G Args *ap, int px, int py, int s, const Hom &Hm,
-                                            const float *r, float *sss_out) {
+                                            const float *r, int rs, float *sss_out) {
     const APD_G Args &a = *ap;
     const SrcTex<F16> Q(a, s);
     const float Wm1 = (float)(a.W - 1), Hm1 = (float)(a.H - 1);
@@ -529,7 +581,7 @@ __device__ __noinline__ apd_f2 ncc_old_ieee(const APD_G Args *ap, int px, int py
             const float v = bilerp(Q.fetch(t.idx), t.ax, t.ay);
             ss += v;
             sss = fmaf(v, v, sss);
-            srs = fmaf(r[i * 6 + j], v, srs);
+            srs = fmaf(r[(i * 6 + j) * rs], v, srs);
         }
     }
     *sss_out = sss;
@@ -537,7 +589,8 @@ __device__ __noinline__ apd_f2 ncc_old_ieee(const APD_G Args *ap, int px, int py
 }
 
 // ComputeBilateralNCCOld (APD.cu:596-721) for source view s (1..N), plane in the ref frame.
-template <bool F16>
+// RS = LDS stride of the reference window (1: per-pixel contiguous; 64: [k][pixel] layout).
+template <bool F16, int RS = 1>
 __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, float4 pl, const RefWin &rw) {
     const int W = a.W, H = a.H;
     Hom Hm = homography(a, s, pl);
@@ -550,14 +603,14 @@ __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, f
     }
     float ss = 0.0f, sss = 0.0f, srs = 0.0f;
     if (window_rcp_ok(Hm, (float)(px - 5), (float)(py - 5))) {
-        const FastTex<F16> T(a, s);
+        const FastTex<F16, (RS > 1)> T(a, s);
         // One window column (6 taps) per step: all 6 gathers are issued before the first is consumed.
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const float x = (float)(px - 5 + 2 * i);
             const apd_f2 cxy = {fmaf(Hm.h[0], x, Hm.h[2]), fmaf(Hm.h[3], x, Hm.h[5])};
             const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
-            typename FastTex<F16>::Tap t[6];
+            typename FastTex<F16, (RS > 1)>::Tap t[6];
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
                 const float y = (float)(py - 5 + 2 * j);
@@ -572,13 +625,13 @@ __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, f
             for (int j = 0; j < 6; ++j) {
                 ss += v[j];
                 // (sss, srs) = (fma(v, v, sss), fma(r, v, srs))
-                const apd_f2 acc = pk_fma((apd_f2){v[j], rw.r[i * 6 + j]}, (apd_f2){v[j], v[j]}, (apd_f2){sss, srs});
+                const apd_f2 acc = pk_fma((apd_f2){v[j], rw.r[(i * 6 + j) * RS]}, (apd_f2){v[j], v[j]}, (apd_f2){sss, srs});
                 sss = acc.x;
                 srs = acc.y;
             }
         }
     } else {
-        const apd_f2 r = ncc_old_ieee<F16>(a.self, px, py, s, Hm, rw.r, &sss);
+        const apd_f2 r = ncc_old_ieee<F16>(a.self, px, py, s, Hm, rw.r, RS, &sss);
         ss = r.x;
         srs = r.y;
     }

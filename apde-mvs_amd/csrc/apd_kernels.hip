@@ -815,6 +815,268 @@ __global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a,
 }
 
 // ---------------------------------------------------------------------------------------------
+// View-major Strong sweep (same function as k_sweep_strong, different work decomposition).
+// A workgroup of VM_WAVES waves owns VM_P = 64 consecutive pixels of the (tile-ordered) list and
+// runs the pixel's work in phases separated by workgroup barriers, each phase with the lane shape
+// that suits it:
+//   P0  lane = (pixel, direction): adaptive-checkerboard scan of one of the 8 directions; the 9
+//       hypothesis planes, their validity and the 6x6 reference window go to LDS.
+//   P1  lane = pixel, wave = (hypothesis, view) task: every gather instruction of a wave samples ONE
+//       source image around 64 neighbouring pixels (compact footprint, L1 reuse across window
+//       columns and across the wave's successive tasks); costs -> LDS [h][v][pixel].
+//   P2  lane = (pixel, view) groups, as in k_sweep_strong: joint view selection with the in-order
+//       CDF and 15 draws, weighted hypothesis costs, argmin, refinement candidates (RNG order
+//       unchanged); candidates, weights and the running state -> LDS.
+//   P3  lane = pixel, wave = (candidate, view) task: refinement NCC (+ geometric) -> LDS.
+//   P4  lane = pixel: in-order weighted candidate costs, acceptance, writes.
+// ---------------------------------------------------------------------------------------------
+#define VM_WAVES 8
+#define VM_BLOCK (VM_WAVES * WAVE)
+#define VM_P 64
+struct VmLds {  // static part; the cost table [9][N][64] follows (dynamic)
+    float refw[36 * VM_P];       // [k][p]
+    float4 hyp[9 * VM_P];        // [h][p]: 8 propagated + current
+    int npos[8 * VM_P];          // [d][p]: neighbour index, -1 = invalid
+    float4 cand[5 * VM_P];       // [k][p]: refinement candidates (t.w = distance)
+    float4 pnow[VM_P];
+    float st[4 * VM_P];          // depth_now, cost_now, cost_init, weight_norm
+};
+static inline size_t vm_lds_bytes(int N) {
+    return sizeof(VmLds) + (size_t)9 * N * VM_P * sizeof(float) + (size_t)N * VM_P * sizeof(int);
+}
+
+// One direction of the adaptive checkerboard (APD.cu:1127-1316): d = 2*dir + far, dir in
+// {up, down, left, right}, in the order of pos[]/flag[] of k_sweep_strong.
+__device__ __forceinline__ int scan_direction(const APD_G float *__restrict__ cost, int d, int c, int px, int py,
+                                              int W, int H) {
+    const int dir = d >> 1, far = d & 1;
+    // unit step toward the neighbour, and the distance to the border along it
+    const int sx = dir == 2 ? -1 : (dir == 3 ? 1 : 0);
+    const int sy = dir == 0 ? -1 : (dir == 1 ? 1 : 0);
+    const int du = dir == 0 ? py : (dir == 1 ? H - 1 - py : (dir == 2 ? px : W - 1 - px));
+    const int step = sy * W + sx;
+    if (far) {
+        if (!(du > 2)) return -1;
+        int best = c + 3 * step;
+        float cmin = cost[best];
+        for (int i = 1; i < 11; ++i)
+            if (du > 2 + 2 * i) {
+                const int t = c + (3 + 2 * i) * step;
+                const float v = cost[t];
+                if (v < cmin) { cmin = v; best = t; }
+            }
+        return best;
+    }
+    if (!(du > 0)) return -1;
+    // perpendicular axis: x for up/down (first -x then +x), y for left/right (first -y then +y)
+    const bool vert = dir < 2;
+    const int vstep = vert ? 1 : W;
+    const int dneg = vert ? px : py;                       // distance to the border on the - side
+    const int dpos = vert ? W - 1 - px : H - 1 - py;       // ... on the + side
+    int best = c + step;
+    float cmin = cost[best];
+    for (int i = 0; i < 3; ++i) {
+        if (du > 1 + i && dneg > i) {
+            const int t = c + (i + 2) * step - (i + 1) * vstep;
+            const float v = cost[t];
+            if (v < cmin) { cmin = v; best = t; }
+        }
+        if (du > 1 + i && dpos > i) {
+            const int t = c + (i + 2) * step + (i + 1) * vstep;
+            const float v = cost[t];
+            if (v < cmin) { cmin = v; best = t; }
+        }
+    }
+    return best;
+}
+
+template <bool F16>
+__global__ __launch_bounds__(VM_BLOCK, 4) void k_sweep_strong_vm(Args a, const int *__restrict__ list, int count,
+                                                                  int iter) {
+    const int N = a.N, W = a.W, H = a.H;
+    VmLds &L = *reinterpret_cast<VmLds *>(apd_dyn_lds);
+    float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64], later [5][N][64]
+    int *wts = reinterpret_cast<int *>(costL + 9 * N * VM_P);            // [N][64]
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int first = blk * VM_P;
+    const int np = min(VM_P, count - first);
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
+    const APD_G Cam &cam0 = a.cams[0];
+    const bool geom_imp = a.geom && a.impetus;
+    const float gf = a.gf;
+
+    // ---- P0: lane = (pixel, direction)
+    {
+        const int p = lane, d = wave;
+        if (p < np) {
+            const int c = list[first + p];
+            const int py = c / W, px = c - py * W;
+            const int q = scan_direction(a.cost, d, c, px, py, W, H);
+            L.npos[d * VM_P + p] = q;
+            if (q >= 0) L.hyp[d * VM_P + p] = a.plane[q];
+            if (d == 0) L.hyp[8 * VM_P + p] = a.plane[c];
+            for (int k = d; k < 36; k += VM_WAVES) {
+                const int i = k / 6, j = k - 6 * (k / 6);
+                L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- P1: lane = pixel, wave = (hypothesis, view) tasks
+    const int p1 = lane;
+    const bool pv1 = p1 < np;
+    int c1 = 0, px1 = 0, py1 = 0;
+    if (pv1) { c1 = list[first + p1]; py1 = c1 / W; px1 = c1 - py1 * W; }
+    const RefWin rw = refwin_from_lds<VM_P>(&L.refw[p1]);
+    for (int t = wave; t < 9 * N; t += VM_WAVES) {
+        const int h = t / N, v = t - h * N;
+        float val = (h == 0 && v == 0) ? 2.0f : 0.0f;  // float cost_array[8][32] = {2.0f} (APD.cu:1120)
+        const bool fh = h == 8 || L.npos[h * VM_P + p1] >= 0;
+        if (pv1 && fh) {
+            const float4 pl = L.hyp[h * VM_P + p1];
+            val = ncc_old<F16, VM_P>(a, px1, py1, v + 1, pl, rw);
+            if (h == 8 && geom_imp) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
+        }
+        costL[t * VM_P + p1] = val;
+    }
+    __syncthreads();
+
+    // ---- P2: lane = (pixel, view) groups; rounds of VM_WAVES * (64/N) pixels
+    const int Gp = WAVE / N;
+    const int ppr = VM_WAVES * Gp;
+    for (int r0 = 0; r0 < np; r0 += ppr) {
+        int g = lane / N;
+        const bool lane_ok = g < Gp;
+        int v = lane - g * N;
+        if (!lane_ok) { g = 0; v = (lane - Gp * N) % N; }
+        Group G;
+        G.v = v; G.base = g * N; G.slot = g; G.li = 0;
+        G.gmask = (N >= 64) ? ~0ull : ((1ull << N) - 1ull);
+        const int pr = r0 + wave * Gp + g;
+        G.valid = lane_ok && pr < np;
+        const int p = min(pr, np - 1);
+        const int c = list[first + p];
+        const int py = c / W, px = c - py * W;
+        float ca[8];
+#pragma unroll
+        for (int h = 0; h < 8; ++h) ca[h] = costL[(h * N + v) * VM_P + p];
+        const float cv_now = costL[(8 * N + v) * VM_P + p];
+        // view selection priors from the 4 direct neighbours (APD.cu:1323-1337)
+        float prior = 0.0f;
+        {
+            const int nb[4] = {c - W, c + W, c - 1, c + 1};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (L.npos[(2 * i) * VM_P + p] >= 0) prior += ((a.sel[nb[i]] >> v) & 1u) ? 0.9f : 0.1f;
+        }
+        Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c, ord_strong(iter));
+        const int w = view_selection(ca, prior, iter, rg, G, N);
+        const uint32_t tsel = group_bits(w > 0, G);
+        float fc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        float wn = 0.0f, cost_now = 0.0f;
+        for (int k = 0; k < N; ++k) {
+            const int wk = __shfl(w, G.base + k);
+            const float fwk = (float)wk;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float ck = __shfl(ca[j], G.base + k);
+                if (wk > 0) fc[j] = fmaf(fwk, ck, fc[j]);
+            }
+            if (wk > 0) wn += fwk;
+            cost_now = fmaf(fwk, __shfl(cv_now, G.base + k), cost_now);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fc[j] /= wn;
+        cost_now /= wn;
+        const float cost_init = cost_now;
+        int mi = 0;
+        {
+            float m = fc[0];
+#pragma unroll
+            for (int j = 1; j < 8; ++j) if (fc[j] <= m) { m = fc[j]; mi = j; }
+        }
+        const float4 cur = L.hyp[8 * VM_P + p];
+        float depth_now = depth_from_plane(cam0, cur, px, py);
+        float4 pnow = cur;
+        {
+            float fcm = fc[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) if (mi == k) fcm = fc[k];
+            if (L.npos[mi * VM_P + p] >= 0) {
+                const float4 cand = L.hyp[mi * VM_P + p];
+                const float db = depth_from_plane(cam0, cand, px, py);
+                if (db >= a.dmin && db <= a.dmax && fcm < cost_now) {
+                    depth_now = db; pnow = cand; cost_now = fcm;
+                    if (G.valid && G.v == 0) a.sel[c] = tsel;
+                }
+            }
+        }
+        // PlaneHypothesisRefinementStrong candidates (APD.cu:950-980)
+        const Cands C = refine_candidates(a, px, py, rg, pnow, depth_now);
+        if (G.valid) {
+            wts[v * VM_P + p] = w;
+            if (G.v == 0) {
+#pragma unroll 1
+                for (int k = 0; k < 5; ++k) {
+                    float dk;
+                    float4 t = candidate(C, k, pnow, depth_now, dk);
+                    t.w = dist2origin(cam0, px, py, dk, t);
+                    L.cand[k * VM_P + p] = t;
+                }
+                L.pnow[p] = pnow;
+                L.st[0 * VM_P + p] = depth_now;
+                L.st[1 * VM_P + p] = cost_now;
+                L.st[2 * VM_P + p] = cost_init;
+                L.st[3 * VM_P + p] = wn;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- P3: lane = pixel, wave = (candidate, view) tasks
+    for (int t = wave; t < 5 * N; t += VM_WAVES) {
+        const int k = t / N, v = t - k * N;
+        float cv = 0.0f;
+        if (pv1) {
+            const float4 tp = L.cand[k * VM_P + p1];
+            cv = ncc_old<F16, VM_P>(a, px1, py1, v + 1, tp, rw);
+            if (geom_imp) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
+        }
+        costL[t * VM_P + p1] = cv;
+    }
+    __syncthreads();
+
+    // ---- P4: weighted candidate costs in view order, acceptance, writes
+    if (pv1) {
+        const int p = p1, c = c1;
+        for (int v = wave; v < N; v += VM_WAVES) a.vw[(size_t)v * a.HW + c] = (uint8_t)wts[v * VM_P + p];
+        if (wave == 0) {
+            float cost_now = L.st[1 * VM_P + p];
+            const float cost_init = L.st[2 * VM_P + p], wn = L.st[3 * VM_P + p];
+            float4 pnow = L.pnow[p];
+#pragma unroll 1
+            for (int k = 0; k < 5; ++k) {
+                const float4 t = L.cand[k * VM_P + p];
+                float tc = 0.0f;
+                for (int kk = 0; kk < N; ++kk) tc = fmaf((float)wts[kk * VM_P + p], costL[(k * N + kk) * VM_P + p], tc);
+                tc /= wn;
+                const float db = depth_from_plane(cam0, t, px1, py1);
+                if (db >= a.dmin && db <= a.dmax && tc < cost_now) { pnow = t; cost_now = tc; }
+            }
+            if (a.state == APD_REFINE_INIT) {
+                if ((double)cost_now < (double)cost_init - 0.1) { a.cost[c] = cost_now; a.plane[c] = pnow; }
+                else a.cost[c] = cost_init;
+            } else {
+                a.cost[c] = cost_now;
+                a.plane[c] = pnow;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // CheckerboardPropagationWeak + PlaneHypothesisRefinementWeak (APD.cu:1442-1615, 1008-1096)
 // ---------------------------------------------------------------------------------------------
 template <bool F16>
@@ -1276,6 +1538,7 @@ struct apd_ctx {
     int n_near = 0;
     Args args{};
     bool loaded = false, prepared = false;
+    bool sweep_vm = true;          // view-major Strong sweep (APD_SWEEP_LANES=1 selects k_sweep_strong)
     int weak_count = 0;
     int cnt[4] = {0, 0, 0, 0};     // strong black, strong red, weak black, weak red
     size_t list_cap = 0;
@@ -1426,6 +1689,12 @@ apd_ctx *apd_create(int32_t device) {
         return nullptr;
     }
     for (auto &e : ctx->ev) (void)hipEventCreate(&e);
+    ctx->sweep_vm = getenv("APD_SWEEP_LANES") == nullptr;
+    // the view-major sweep's LDS grows with N (> 64 KiB from N = 15 on); gfx950 has 160 KiB per CU
+    (void)hipFuncSetAttribute((const void *)k_sweep_strong_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)vm_lds_bytes(APD_MAX_IMAGES - 1));
+    (void)hipFuncSetAttribute((const void *)k_sweep_strong_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)vm_lds_bytes(APD_MAX_IMAGES - 1));
     return ctx;
 }
 
@@ -1466,13 +1735,16 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     if ((P.geom_consistency || P.use_APD) && !pb->depths) { ctx->err = "depth maps required (geom/APD)"; return APD_EINVAL; }
     const int N = NI - 1;
     const size_t HW = (size_t)W * H;
-    // source texel storage: fp16 vertical pairs when every source texel is exact in fp16, else fp32 quads
+    // source texel storage: fp16 vertical pairs when every source texel is a quarter-integer in
+    // [0, 256) (8-bit images and their INTER_LINEAR 2^-k downscales are): such texels AND their
+    // horizontal differences are exact in fp16 (FastTex::sample relies on both). Else fp32 quads.
     bool tex_f16 = getenv("APD_TEX_F32") == nullptr;
     for (int i = 1; i < NI && tex_f16; ++i) {
         const float *img = pb->images[i];
         if (!img) break;
         for (size_t k = 0; k < (size_t)W * H; ++k) {
-            if ((float)(_Float16)img[k] != img[k]) { tex_f16 = false; break; }
+            const float q = img[k] * 4.0f;
+            if (!(q >= 0.0f && q < 1024.0f) || q != (float)(int)q) { tex_f16 = false; break; }
         }
     }
     const size_t qstride = tex_f16 ? (size_t)(W + 2) * (H + 1) : (size_t)(W + 1) * (H + 1);
@@ -1719,8 +1991,12 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             (void)hipEventCreate(&e1);
             (void)hipEventRecord(e0, s);
         }
-        LAUNCH_TEX(k_sweep_strong, dim3(group_blocks(n, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a,
-                           (const int *)list_ptr(ctx, colour), n, iter);
+        if (ctx->sweep_vm)
+            LAUNCH_TEX(k_sweep_strong_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), vm_lds_bytes(a.N), s,
+                       a, (const int *)list_ptr(ctx, colour), n, iter);
+        else
+            LAUNCH_TEX(k_sweep_strong, dim3(group_blocks(n, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a,
+                       (const int *)list_ptr(ctx, colour), n, iter);
         if (ctx->prof) {
             (void)hipEventRecord(e1, s);
             ctx->prof_ev.emplace_back(e0, e1);
