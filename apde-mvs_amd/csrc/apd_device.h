@@ -10,6 +10,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #define APD_COST_MAX 2.0f
 #define APD_WEAK 0
@@ -533,13 +534,14 @@ struct FastTex {
         t.f = (apd_f2){(float)(qx & 255), (float)(qy & 255)} * 0.00390625f;
         return t;
     }
-    __device__ __forceinline__ float sample(const Tap &t) const {
+    using Raw = typename std::conditional<F16, apd_u2_a4, float4>::type;
+    __device__ __forceinline__ Raw load(const Tap &t) const { return *(const APD_G Raw *)(base + t.off); }
+    __device__ __forceinline__ float finish(const Tap &t, const Raw &v) const {
         if constexpr (F16) {
             // F16 storage is only selected for quarter-integer texels in [0, 256) (see apd_set_problem):
             // the horizontal differences T10-T00, T11-T01 are then exact in fp16, so they are taken with
             // one v_pk_add_f16 and fed to v_fma_mix_f32 (fp16 operands converted exactly) -- the same
             // fp32 values and FMAs as bilerp() on the converted texels.
-            const apd_u2_a4 v = *(const APD_G apd_u2_a4 *)(base + t.off);
             const apd_h2 c0 = __builtin_bit_cast(apd_h2, v.x);  // {T00, T01}
             const apd_h2 c1 = __builtin_bit_cast(apd_h2, v.y);  // {T10, T11}
             const apd_h2 dd = c1 - c0;
@@ -547,13 +549,14 @@ struct FastTex {
             const float bot = fma_mix_hi(t.f.x, dd, c0);  // fma(ax, T11 - T01, T01)
             return fmaf(t.f.y, bot - top, top);
         } else {
-            const float4 q = *(const APD_G float4 *)(base + t.off);
+            const float4 q = v;
             // top = fma(ax, T10 - T00, T00), bot = fma(ax, T11 - T01, T01), v = fma(ay, bot - top, top)
             const apd_f2 lo = (apd_f2){q.x, q.z}, hi = (apd_f2){q.y, q.w};
             const apd_f2 tb = pk_fma((apd_f2){t.f.x, t.f.x}, hi - lo, lo);
             return fmaf(t.f.y, tb.y - tb.x, tb.x);
         }
     }
+    __device__ __forceinline__ float sample(const Tap &t) const { return finish(t, load(t)); }
 };
 
 // IEEE-division statement of the ComputeBilateralNCCOld window sum (taken only for windows that
@@ -602,15 +605,16 @@ __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, f
         if (a.sa[pidx] != 0) return ncc_old_sa<F16>(a.self, px, py, s, Hm, a.sa[py * W + px]);
     }
     float ss = 0.0f, sss = 0.0f, srs = 0.0f;
+#ifdef APD_ABLATE_NCC  // timing-only build: skeleton without the window sums
+    return fabsf(Hm.h[0] + Hm.h[8]) * 0.001f;
+#endif
     if (window_rcp_ok(Hm, (float)(px - 5), (float)(py - 5))) {
         const FastTex<F16, (RS > 1)> T(a, s);
-        // One window column (6 taps) per step: all 6 gathers are issued before the first is consumed.
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
+        using FT = FastTex<F16, (RS > 1)>;
+        auto column = [&](int i, typename FT::Tap *t) {
             const float x = (float)(px - 5 + 2 * i);
             const apd_f2 cxy = {fmaf(Hm.h[0], x, Hm.h[2]), fmaf(Hm.h[3], x, Hm.h[5])};
             const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
-            typename FastTex<F16, (RS > 1)>::Tap t[6];
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
                 const float y = (float)(py - 5 + 2 * j);
@@ -618,18 +622,52 @@ __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, f
                 const float Z = fmaf(Hm.h[7], y, cz);
                 t[j] = T.tap(XY, rcp_newton(Z));
             }
-            float v[6];
-#pragma unroll
-            for (int j = 0; j < 6; ++j) v[j] = T.sample(t[j]);
+        };
+        auto consume = [&](int i, const typename FT::Tap *t, const typename FT::Raw *q) {
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
-                ss += v[j];
+                const float v = T.finish(t[j], q[j]);
+                ss += v;
                 // (sss, srs) = (fma(v, v, sss), fma(r, v, srs))
-                const apd_f2 acc = pk_fma((apd_f2){v[j], rw.r[(i * 6 + j) * RS]}, (apd_f2){v[j], v[j]}, (apd_f2){sss, srs});
+                const apd_f2 acc = pk_fma((apd_f2){v, rw.r[(i * 6 + j) * RS]}, (apd_f2){v, v}, (apd_f2){sss, srs});
                 sss = acc.x;
                 srs = acc.y;
             }
+        };
+#ifndef APD_NCC_NOPIPE
+        // software pipeline: column i+1's gathers are in flight while column i is consumed
+        typename FT::Tap ta[6], tb[6];
+        typename FT::Raw qa[6], qb[6];
+        column(0, ta);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) qa[j] = T.load(ta[j]);
+#pragma unroll
+        for (int i = 0; i < 6; i += 2) {
+            if (i + 1 < 6) {
+                column(i + 1, tb);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) qb[j] = T.load(tb[j]);
+            }
+            consume(i, ta, qa);
+            if (i + 2 < 6) {
+                column(i + 2, ta);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) qa[j] = T.load(ta[j]);
+            }
+            if (i + 1 < 6) consume(i + 1, tb, qb);
         }
+#else
+        // One window column (6 taps) per step: all 6 gathers are issued before the first is consumed.
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            typename FT::Tap t[6];
+            typename FT::Raw q[6];
+            column(i, t);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) q[j] = T.load(t[j]);
+            consume(i, t, q);
+        }
+#endif
     } else {
         const apd_f2 r = ncc_old_ieee<F16>(a.self, px, py, s, Hm, rw.r, RS, &sss);
         ss = r.x;

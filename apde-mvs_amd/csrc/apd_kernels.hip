@@ -891,7 +891,10 @@ __device__ __forceinline__ int scan_direction(const APD_G float *__restrict__ co
 }
 
 template <bool F16>
-__global__ __launch_bounds__(VM_BLOCK, 4) void k_sweep_strong_vm(Args a, const int *__restrict__ list, int count,
+#ifndef VM_MINW
+#define VM_MINW 4  // waves per SIMD -> VGPR budget 512 / VM_MINW
+#endif
+__global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, const int *__restrict__ list, int count,
                                                                   int iter) {
     const int N = a.N, W = a.W, H = a.H;
     VmLds &L = *reinterpret_cast<VmLds *>(apd_dyn_lds);
