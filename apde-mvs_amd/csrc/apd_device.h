@@ -60,6 +60,7 @@ struct Args {
     const APD_G float4 *quad;              // source images 1..N in quad layout, view v at (v-1)*qstride
     const APD_G uint32_t *pairs;           // or in fp16 vertical-pair layout (tex_f16), same stride
     int tex_f16;
+    int force_slow;                        // test hook: route every NCC-Old window through ncc_old_slow
     const APD_G float *depth;              // [N+1][H*W] depth maps (geom / APD)
     const APD_G SrcView *views;            // [N+1]
     const APD_G Cam *cams;                 // [N+1]
@@ -419,7 +420,7 @@ __device__ __forceinline__ void build_refwin(const Args &a, int px, int py, floa
 
 // SA quadrant branch of ComputeBilateralNCCOld (APD.cu:664-719); rarely taken, kept out of line.
 template <bool F16>
-__device__ __noinline__ float ncc_old_sa(const APD_G Args *ap, int px, int py, int s, const Hom &H, uint8_t cid) {
+__device__ __forceinline__ float ncc_old_sa(const APD_G Args *ap, int px, int py, int s, const Hom &H, uint8_t cid) {
     const APD_G Args &a = *ap;
     const int sign[8] = {1, 1, -1, -1, 1, -1, -1, 1};
     const int off[18] = {1, 1, 3, 1, 1, 3, 1, 5, 3, 3, 5, 1, 5, 3, 3, 5, 5, 5};
@@ -562,8 +563,8 @@ struct FastTex {
 // IEEE-division statement of the ComputeBilateralNCCOld window sum (taken only for windows that
 // window_rcp_ok rejects).
 template <bool F16>
-__device__ __noinline__ apd_f2 ncc_old_ieee(const APD_G Args *ap, int px, int py, int s, const Hom &Hm,
-                                            const float *r, int rs, float *sss_out) {
+__device__ __forceinline__ apd_f2 ncc_old_ieee(const APD_G Args *ap, int px, int py, int s, const Hom &Hm,
+                                               const float *r, int rs, float *sss_out) {
     const APD_G Args &a = *ap;
     const SrcTex<F16> Q(a, s);
     const float Wm1 = (float)(a.W - 1), Hm1 = (float)(a.H - 1);
@@ -591,24 +592,63 @@ __device__ __noinline__ apd_f2 ncc_old_ieee(const APD_G Args *ap, int px, int py
     return (apd_f2){ss, srs};
 }
 
-// ComputeBilateralNCCOld (APD.cu:596-721) for source view s (1..N), plane in the ref frame.
+__device__ __forceinline__ float ncc_old_finish(float ss, float sss, float srs, float mean, float var) {
+    const float inv = 1.0f / 36.0f;
+    ss *= inv; sss *= inv; srs *= inv;
+    float var_src = fmaf(-ss, ss, sss);
+    if (var < 1e-5f || var_src < 1e-5f) return APD_COST_MAX;
+    float covar = fmaf(-mean, ss, srs);
+    float vrs = sqrtf(var * var_src);
+    return fmaxf(0.0f, fminf(APD_COST_MAX, 1.0f - covar / vrs));
+}
+
+// Out-of-line ComputeBilateralNCCOld for the windows ncc_old_fast hands back: the SA quadrant
+// variant, or windows whose taps need the IEEE reciprocal. Everything arrives by value (the
+// homography is recomputed from the plane), so the hot path never spills a homography to the stack.
+template <bool F16>
+__device__ __noinline__ float ncc_old_slow(const APD_G Args *ap, int px, int py, int s, float4 pl, const float *r,
+                                           int rs, float mean, float var) {
+    const APD_G Args &a = *ap;
+    const Hom Hm = homography(a, s, pl);
+    float ptx, pty;
+    project(Hm, (float)px, (float)py, ptx, pty);
+    if (ptx >= (float)a.W || ptx < 0.0f || pty >= (float)a.H || pty < 0.0f) return APD_COST_MAX;
+    if (a.sa_any) {
+        int pidx = clampi((int)fmaf(pty, (float)a.W, ptx), 0, a.HW - 1);
+        if (a.sa[pidx] != 0) return ncc_old_sa<F16>(ap, px, py, s, Hm, a.sa[py * a.W + px]);
+    }
+    float sss;
+    const apd_f2 rr = ncc_old_ieee<F16>(ap, px, py, s, Hm, r, rs, &sss);
+    return ncc_old_finish(rr.x, sss, rr.y, mean, var);
+}
+
+// ComputeBilateralNCCOld (APD.cu:596-721) for source view s (1..N), plane in the ref frame: the
+// call-free fast path. Returns the cost, or sets `slow` when the window needs ncc_old_slow (SA mask
+// hit at the projected centre, or a Z the Newton reciprocal is not proven for); the returned value
+// is then meaningless (the taps ran on a dummy homography that keeps every address in bounds).
 // RS = LDS stride of the reference window (1: per-pixel contiguous; 64: [k][pixel] layout).
 template <bool F16, int RS = 1>
-__device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, float4 pl, const RefWin &rw) {
+__device__ __forceinline__ float ncc_old_fast(const Args &a, int px, int py, int s, float4 pl, const RefWin &rw,
+                                              bool &slow) {
     const int W = a.W, H = a.H;
     Hom Hm = homography(a, s, pl);
     float ptx, pty;
     project(Hm, (float)px, (float)py, ptx, pty);
+    slow = false;
     if (ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f) return APD_COST_MAX;
     if (a.sa_any) {
         int pidx = clampi((int)fmaf(pty, (float)W, ptx), 0, a.HW - 1);
-        if (a.sa[pidx] != 0) return ncc_old_sa<F16>(a.self, px, py, s, Hm, a.sa[py * W + px]);
+        if (a.sa[pidx] != 0) slow = true;
     }
-    float ss = 0.0f, sss = 0.0f, srs = 0.0f;
 #ifdef APD_ABLATE_NCC  // timing-only build: skeleton without the window sums
     return fabsf(Hm.h[0] + Hm.h[8]) * 0.001f;
 #endif
-    if (window_rcp_ok(Hm, (float)(px - 5), (float)(py - 5))) {
+    if (!window_rcp_ok(Hm, (float)(px - 5), (float)(py - 5)) || a.force_slow) slow = true;
+    if (slow) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Hm.h[k] = (k == 8) ? 1.0f : 0.0f;  // every tap -> texel (0, 0)
+    }
+    float ss = 0.0f, sss = 0.0f, srs = 0.0f;
         const FastTex<F16, (RS > 1)> T(a, s);
         using FT = FastTex<F16, (RS > 1)>;
         auto column = [&](int i, typename FT::Tap *t) {
@@ -668,18 +708,15 @@ __device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, f
             consume(i, t, q);
         }
 #endif
-    } else {
-        const apd_f2 r = ncc_old_ieee<F16>(a.self, px, py, s, Hm, rw.r, RS, &sss);
-        ss = r.x;
-        srs = r.y;
-    }
-    const float inv = 1.0f / 36.0f;
-    ss *= inv; sss *= inv; srs *= inv;
-    float var_src = fmaf(-ss, ss, sss);
-    if (rw.var < 1e-5f || var_src < 1e-5f) return APD_COST_MAX;
-    float covar = fmaf(-rw.mean, ss, srs);
-    float vrs = sqrtf(rw.var * var_src);
-    return fmaxf(0.0f, fminf(APD_COST_MAX, 1.0f - covar / vrs));
+    return ncc_old_finish(ss, sss, srs, rw.mean, rw.var);
+}
+
+template <bool F16, int RS = 1>
+__device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, float4 pl, const RefWin &rw) {
+    bool slow;
+    const float v = ncc_old_fast<F16, RS>(a, px, py, s, pl, rw, slow);
+    if (__builtin_expect(slow, 0)) return ncc_old_slow<F16>(a.self, px, py, s, pl, rw.r, RS, rw.mean, rw.var);
+    return v;
 }
 
 // sa label at a possibly out-of-image linear index (same rule as the oracle's sa_at)

@@ -933,15 +933,29 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     int c1 = 0, px1 = 0, py1 = 0;
     if (pv1) { c1 = list[first + p1]; py1 = c1 / W; px1 = c1 - py1 * W; }
     const RefWin rw = refwin_from_lds<VM_P>(&L.refw[p1]);
-    for (int t = wave; t < 9 * N; t += VM_WAVES) {
+    // tasks whose window needs the out-of-line path are collected in `defer` (bit k = k-th task of
+    // this wave) and evaluated after the loop, so the hot loop holds no call.
+    uint64_t defer = 0;
+    for (int t = wave, k = 0; t < 9 * N; t += VM_WAVES, ++k) {
         const int h = t / N, v = t - h * N;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;  // float cost_array[8][32] = {2.0f} (APD.cu:1120)
         const bool fh = h == 8 || L.npos[h * VM_P + p1] >= 0;
         if (pv1 && fh) {
             const float4 pl = L.hyp[h * VM_P + p1];
-            val = ncc_old<F16, VM_P>(a, px1, py1, v + 1, pl, rw);
+            bool slow;
+            val = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, pl, rw, slow);
+            if (slow) defer |= 1ull << k;
             if (h == 8 && geom_imp) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
         }
+        costL[t * VM_P + p1] = val;
+    }
+    while (defer) {
+        const int k = __builtin_ctzll(defer);
+        defer &= defer - 1;
+        const int t = wave + k * VM_WAVES, h = t / N, v = t - h * N;
+        const float4 pl = L.hyp[h * VM_P + p1];
+        float val = ncc_old_slow<F16>(a.self, px1, py1, v + 1, pl, rw.r, VM_P, rw.mean, rw.var);
+        if (h == 8 && geom_imp) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
         costL[t * VM_P + p1] = val;
     }
     __syncthreads();
@@ -1039,14 +1053,26 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     __syncthreads();
 
     // ---- P3: lane = pixel, wave = (candidate, view) tasks
-    for (int t = wave; t < 5 * N; t += VM_WAVES) {
+    defer = 0;
+    for (int t = wave, kt = 0; t < 5 * N; t += VM_WAVES, ++kt) {
         const int k = t / N, v = t - k * N;
         float cv = 0.0f;
         if (pv1) {
             const float4 tp = L.cand[k * VM_P + p1];
-            cv = ncc_old<F16, VM_P>(a, px1, py1, v + 1, tp, rw);
+            bool slow;
+            cv = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, tp, rw, slow);
+            if (slow) defer |= 1ull << kt;
             if (geom_imp) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
         }
+        costL[t * VM_P + p1] = cv;
+    }
+    while (defer) {
+        const int kt = __builtin_ctzll(defer);
+        defer &= defer - 1;
+        const int t = wave + kt * VM_WAVES, k = t / N, v = t - k * N;
+        const float4 tp = L.cand[k * VM_P + p1];
+        float cv = ncc_old_slow<F16>(a.self, px1, py1, v + 1, tp, rw.r, VM_P, rw.mean, rw.var);
+        if (geom_imp) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
         costL[t * VM_P + p1] = cv;
     }
     __syncthreads();
@@ -1858,6 +1884,7 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     a.quad = devptr<decltype(a.quad)>(ctx->quad.p);
     a.pairs = devptr<decltype(a.pairs)>(ctx->quad.p);
     a.tex_f16 = tex_f16 ? 1 : 0;
+    a.force_slow = getenv("APD_FORCE_SLOW_NCC") != nullptr;  // test hook (tests/test_gpu_parity.py)
     a.depth = devptr<decltype(a.depth)>(need_depth ? ctx->depth.p : nullptr);
     a.views = devptr<decltype(a.views)>(ctx->views.p);
     a.cams = devptr<decltype(a.cams)>(ctx->cams.p);
