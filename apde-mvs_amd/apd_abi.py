@@ -155,7 +155,9 @@ class Outputs:
         self.costs = np.zeros((height, width), np.float32)
         self.selected_views = np.zeros((height, width), np.uint32)
         self.view_weights = np.zeros((num_src, height, width), np.uint8)
-        self.anchors = np.zeros((max(max_weak, 1), ANCHOR_NUM, 2), np.int16)
+        # anchors are only requested when the caller sizes them (weak_count <= max_weak): the library
+        # writes weak_count * 9 entries, so an undersized buffer must never be handed over
+        self.anchors = np.zeros((max_weak, ANCHOR_NUM, 2), np.int16) if max_weak > 0 else None
         self.weak_count = np.zeros(1, np.int32)
         self.reliable_curve = np.zeros((hw, 61), np.float32) if want_curve else None
 
@@ -167,7 +169,7 @@ class Outputs:
         o.costs = _ptr(self.costs, C.c_float)
         o.selected_views = _ptr(self.selected_views, C.c_uint32)
         o.view_weights = _ptr(self.view_weights, C.c_uint8)
-        o.anchors = _ptr(self.anchors, C.c_int16)
+        o.anchors = _ptr(self.anchors, C.c_int16)  # NULL when not sized
         o.weak_count = _ptr(self.weak_count, C.c_int32)
         o.reliable_curve = _ptr(self.reliable_curve, C.c_float)
         return o

@@ -1,0 +1,633 @@
+// apd_main.cpp — the `apd` depth binary: drop-in for the reference's `APD` executable (main.cpp),
+// driving libapd_hip.so through the C ABI of include/apd_hip.h.
+//
+// Same flags, defaults, bool-word parsing, exit codes and stdout lines as main.cpp:9-40 / 210-400
+// (run.py:104-119 builds the command line), the same per-problem host work as
+// APD::InuputInitialization (APD.cpp:501-685) and ProcessProblem (main.cpp:148-191), and the same
+// round schedule (main.cpp:290-367). Additions (all optional):
+//   --gpus LIST          comma-separated HIP devices; views of a pass are dealt to the devices by a
+//                        dynamic work queue (one thread + one apd_ctx per device)
+//   --ordering MODE      sequential (reference order: a view sees the current pass's depth maps of
+//                        the views processed before it) | jacobi (every view of a pass reads the
+//                        previous pass's maps; required for > 1 GPU, results independent of the
+//                        device count and of the processing order)
+//   --seed N             base of the deterministic per-problem RNG seed
+// Fusion (RunFusion*, APD.cpp:962-1608) is outside this engine's scope.
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iomanip>
+#include <iostream>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/apd_hip.h"
+#include "image.h"
+#include "io.h"
+
+using namespace apdhost;
+
+namespace {
+
+std::mutex g_print;
+#define SAY(expr)                                      \
+    do {                                               \
+        std::lock_guard<std::mutex> _g(g_print);       \
+        std::cout << expr << std::endl;                \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------------
+// arguments (boost::program_options semantics of main.cpp:6-40)
+// ------------------------------------------------------------------------------------------------
+struct Opt {
+    const char *name, *shortname, *defval, *help;
+    bool is_bool;
+};
+const Opt kOpts[] = {
+    {"dense_folder", "d", nullptr, "path to dense folder", false},
+    {"gpu_index", "g", "0", "gpu index", false},
+    {"dataset", "D", "DTU", "dataset name, DTU, ETH3D or Tanks and Temples", false},
+    {"only_fuse", "f", "false", "only fuse depths", true},
+    {"no_fuse", "F", "false", "skip fuse", true},
+    {"memory_cache", "m", "true", "use memory cache", true},
+    {"use_sa", "s", "true", "use segment anything results", true},
+    {"use_impetus", "i", "true", "use impetus", true},
+    {"weak_filter", "w", "true", "use weak filter", true},
+    {"flush", nullptr, "false", "Flush mat to disk", true},
+    {"export_anchor", "n", "false", "Export anchor points to disk", true},
+    {"export_curve", "r", "false", "Export reliable curve to disk", true},
+    {"export_color", "c", "true", "Export ply with color", true},
+    {"gpus", nullptr, "", "comma-separated HIP devices (default: gpu_index)", false},
+    {"ordering", nullptr, "", "sequential | jacobi (default: sequential on 1 GPU, jacobi on more)", false},
+    {"seed", nullptr, "24301", "base RNG seed of the deterministic PatchMatch RNG", false},
+};
+
+void usage() {
+    std::cout << "Allowed options:\n";
+    for (const Opt &o : kOpts) {
+        std::string n = std::string("  ") + (o.shortname ? std::string("-") + o.shortname + " [ --" : "--") + o.name +
+                        (o.shortname ? " ]" : "") + " arg";
+        std::cout << std::left << std::setw(34) << n << o.help;
+        if (o.defval && *o.defval) std::cout << " (=" << o.defval << ")";
+        std::cout << "\n";
+    }
+    std::cout << "  -h [ --help ]                   produce help message\n";
+}
+
+bool parse_bool(const std::string &v, bool &b) {
+    std::string s;
+    for (char c : v) s += (char)tolower(c);
+    if (s == "true" || s == "1" || s == "yes" || s == "on") { b = true; return true; }
+    if (s == "false" || s == "0" || s == "no" || s == "off") { b = false; return true; }
+    return false;
+}
+
+std::map<std::string, std::string> parse_args(int argc, char **argv) {
+    std::map<std::string, std::string> vals;
+    for (const Opt &o : kOpts)
+        if (o.defval) vals[o.name] = o.defval;
+    auto fail = [](const std::string &msg) {
+        std::cout << "Error: " << msg << std::endl;
+        usage();
+        exit(-1);
+    };
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        if (a == "-h" || a == "--help") {
+            usage();
+            exit(0);
+        }
+        const Opt *opt = nullptr;
+        std::string value;
+        bool have_value = false;
+        if (a.rfind("--", 0) == 0) {
+            std::string n = a.substr(2);
+            const size_t eq = n.find('=');
+            if (eq != std::string::npos) { value = n.substr(eq + 1); n = n.substr(0, eq); have_value = true; }
+            for (const Opt &o : kOpts) if (n == o.name) opt = &o;
+        } else if (a.size() >= 2 && a[0] == '-') {
+            const std::string n = a.substr(1, 1);
+            for (const Opt &o : kOpts) if (o.shortname && n == o.shortname) opt = &o;
+            if (a.size() > 2) { value = a.substr(2); have_value = true; }
+        }
+        if (!opt) fail("unrecognised option '" + a + "'");
+        if (!have_value) {
+            if (i + 1 >= argc) fail(std::string("the required argument for option '--") + opt->name + "' is missing");
+            value = argv[++i];
+        }
+        if (opt->is_bool) {
+            bool b;
+            if (!parse_bool(value, b))
+                fail(std::string("the argument ('") + value + "') for option '--" + opt->name + "' is invalid");
+        }
+        vals[opt->name] = value;
+    }
+    if (!vals.count("dense_folder")) fail("the option '--dense_folder' is required but missing");
+    return vals;
+}
+
+bool as_bool(const std::map<std::string, std::string> &v, const char *k) {
+    bool b = false;
+    parse_bool(v.at(k), b);
+    return b;
+}
+
+// ------------------------------------------------------------------------------------------------
+// per-problem state (main.h:80-115)
+// ------------------------------------------------------------------------------------------------
+struct Job {
+    Problem pb;
+    apd_params params{};
+    int scale_size = 1;
+    int iteration = 0;
+    bool export_anchor = false, export_curve = false;
+    long used_ms = 0;
+};
+
+struct Pending {  // Jacobi ordering: outputs committed at the end of the pass
+    std::string path;
+    Mat mat;
+};
+
+struct Driver {
+    std::string dense;
+    bool use_sa = true, flush = false;
+    uint64_t seed = 24301;
+    bool jacobi = false;
+    MatStore *store = nullptr;
+    std::mutex pend_mu;
+    std::vector<Pending> pending;
+
+    void emit(const std::string &path, const Mat &m) {
+        if (jacobi) {
+            std::lock_guard<std::mutex> g(pend_mu);
+            pending.push_back({path, m});
+        } else {
+            store->write(path, m, flush);
+        }
+    }
+    void commit() {
+        for (auto &p : pending) store->write(p.path, p.mat, flush);
+        pending.clear();
+    }
+
+    // APD::InuputInitialization + CudaSpaceInitialization + RunPatchMatch + ProcessProblem
+    bool process(apd_ctx *ctx, Job &job);
+};
+
+bool load_image(const std::string &path, std::vector<float> &img, int &w, int &h) {
+    Gray8 g;
+    std::string err;
+    if (!read_gray8(path, g, err)) {
+        SAY("Error opening file: \"" << path << "\" (" << err << ")");
+        return false;
+    }
+    w = g.width;
+    h = g.height;
+    img.resize(g.px.size());
+    for (size_t i = 0; i < g.px.size(); ++i) img[i] = (float)g.px[i];  // convertTo(CV_32FC1)
+    return true;
+}
+
+bool Driver::process(apd_ctx *ctx, Job &job) {
+    const Problem &pb = job.pb;
+    const std::string result_folder = dense + "/APD/" + format_index(pb.ref_image_id);
+    SAY("Processing image: " << format_index(pb.ref_image_id) << "...");
+    const auto start = std::chrono::steady_clock::now();
+    // ---- images (APD.cpp:508-533)
+    std::vector<std::vector<float>> images;
+    std::vector<int> ids{pb.ref_image_id};
+    ids.insert(ids.end(), pb.src_image_ids.begin(), pb.src_image_ids.end());
+    int width = 0, height = 0;
+    for (size_t i = 0; i < ids.size(); ++i) {
+        std::vector<float> img;
+        int w, h;
+        if (!load_image(dense + "/images/" + format_index(ids[i]) + pb.img_ext, img, w, h)) return false;
+        if (i == 0) { width = w; height = h; }
+        images.push_back(std::move(img));
+    }
+    if (images.size() > APD_MAX_IMAGES) {
+        SAY("Can't process so much images: " << images.size());
+        exit(EXIT_FAILURE);
+    }
+    const int NI = (int)images.size();
+    // ---- cameras (APD.cpp:536-556)
+    std::vector<apd_camera> cams(NI);
+    for (int i = 0; i < NI; ++i) {
+        if (!read_camera(dense + "/cams/" + format_index(ids[i]) + "_cam.txt", cams[i])) {
+            SAY("Error opening file: " << dense << "/cams/" << format_index(ids[i]) << "_cam.txt");
+            return false;
+        }
+        cams[i].width = width;
+        cams[i].height = height;
+    }
+    apd_params P = job.params;
+    P.depth_min = cams[0].depth_min * 0.6f;
+    P.depth_max = cams[0].depth_max * 1.2f;
+    P.num_images = NI;
+    {
+        std::lock_guard<std::mutex> g(g_print);
+        std::cout << "Read images and camera done\n";
+        std::cout << "Depth range: " << P.depth_min << " " << P.depth_max << std::endl;
+        std::cout << "Num images: " << P.num_images << std::endl;
+    }
+    // ---- scale (APD.cpp:562-590)
+    if (job.scale_size != 1) {
+        for (int i = 0; i < NI; ++i) {
+            const float factor = 1.0f / (float)job.scale_size;
+            const int src_w = (i == 0) ? width : cams[i].width, src_h = (i == 0) ? height : cams[i].height;
+            const int new_cols = (int)std::round(src_w * factor);
+            const int new_rows = (int)std::round(src_h * factor);
+            const float scale_x = new_cols / (float)src_w, scale_y = new_rows / (float)src_h;
+            std::vector<float> dst((size_t)new_cols * new_rows);
+            resize_linear_f32(images[i].data(), src_w, src_h, dst.data(), new_cols, new_rows);
+            images[i].swap(dst);
+            cams[i].K[0] *= scale_x;
+            cams[i].K[2] *= scale_x;
+            cams[i].K[4] *= scale_y;
+            cams[i].K[5] *= scale_y;
+            cams[i].width = new_cols;
+            cams[i].height = new_rows;
+        }
+        width = cams[0].width;
+        height = cams[0].height;
+        SAY("Scale images and cameras done");
+    }
+    SAY("Image size: " << width << " * " << height);
+    const size_t HW = (size_t)width * height;
+    auto fit = [&](Mat m) { return (m.cols != width || m.rows != height) ? resize_nearest(m, width, height) : m; };
+    // ---- priors (APD.cpp:592-684)
+    std::vector<Mat> depths;
+    if (P.geom_consistency || P.use_APD) {
+        Mat d;
+        store->read(result_folder + "/depths.bin", d);
+        depths.push_back(fit(d));
+        for (int id : pb.src_image_ids) {
+            Mat s;
+            store->read(dense + "/APD/" + format_index(id) + "/depths.bin", s);
+            depths.push_back(fit(s));
+        }
+        for (auto &m : depths)
+            if (m.empty() || m.type != CV_32FC1) { SAY("Error: missing depth prior"); return false; }
+    }
+    Mat weak, conf, sa, anchors_map;
+    int weak_count = 0;
+    if (P.use_APD) {
+        store->read(result_folder + "/weak.bin", weak);
+        store->read(result_folder + "/confidence.bin", conf);
+        if (weak.empty() || conf.empty()) { SAY("Error: missing weak/confidence prior"); return false; }
+        if (weak.cols != width || weak.rows != height) { SAY("resize weak info to target size"); weak = fit(weak); }
+        if (conf.cols != width || conf.rows != height) { SAY("resize confidence to target size"); conf = fit(conf); }
+        anchors_map = Mat(height, width, CV_32SC1);
+        for (size_t i = 0; i < HW; ++i) anchors_map.ptr<int32_t>()[i] = weak.ptr<uint8_t>()[i] == APD_WEAK ? weak_count++ : -1;
+        if (P.use_sa) {
+            const std::string sa_dir = dense + "/sa_masks";
+            if (file_exists(sa_dir)) {
+                store->read(sa_dir + "/" + format_index(pb.ref_image_id) + ".bin", sa);
+                if (!sa.empty() && (sa.cols != width || sa.rows != height)) { SAY("resize sa mask to target size"); sa = fit(sa); }
+            } else {
+                SAY("Can't find sa mask folder: \"" << sa_dir << "\"");
+            }
+        }
+        SAY("Weak count: " << weak_count << " / " << HW << " = " << (float)weak_count / (float)HW * 100 << "%");
+    }
+    std::vector<float> init_planes;
+    if (P.state != APD_FIRST_INIT) {
+        Mat d, n;
+        store->read(result_folder + "/depths.bin", d);
+        store->read(result_folder + "/normals.bin", n);
+        if (d.empty() || n.empty()) { SAY("Error: missing depth/normal prior"); return false; }
+        if (d.cols != width || d.rows != height || n.cols != width || n.rows != height) {
+            SAY("resize depth and normal to target size");
+            d = fit(d);
+            n = fit(n);
+        }
+        init_planes.resize(HW * 4);
+        for (size_t i = 0; i < HW; ++i) {
+            init_planes[4 * i + 0] = n.ptr<float>()[3 * i + 0];
+            init_planes[4 * i + 1] = n.ptr<float>()[3 * i + 1];
+            init_planes[4 * i + 2] = n.ptr<float>()[3 * i + 2];
+            init_planes[4 * i + 3] = d.ptr<float>()[i];
+        }
+    }
+    // ---- device (CudaSpaceInitialization + RunPatchMatch)
+    std::vector<const float *> img_ptrs(NI), dep_ptrs(NI);
+    for (int i = 0; i < NI; ++i) img_ptrs[i] = images[i].data();
+    for (size_t i = 0; i < depths.size(); ++i) dep_ptrs[i] = depths[i].ptr<float>();
+    apd_problem prob{};
+    prob.width = width;
+    prob.height = height;
+    prob.num_images = NI;
+    prob.images = img_ptrs.data();
+    prob.cameras = cams.data();
+    prob.params = P;
+    prob.depths = depths.empty() ? nullptr : dep_ptrs.data();
+    prob.init_planes = init_planes.empty() ? nullptr : init_planes.data();
+    prob.weak_info = P.use_APD ? weak.ptr<uint8_t>() : nullptr;
+    prob.confidence = P.use_APD ? conf.ptr<uint8_t>() : nullptr;
+    prob.sa_mask = (P.use_APD && !sa.empty()) ? sa.ptr<uint8_t>() : nullptr;
+    prob.seed = seed ^ ((uint64_t)(uint32_t)job.iteration << 32) ^ (uint64_t)(uint32_t)pb.ref_image_id;
+    prob.export_reliable_curve = job.export_curve ? 1 : 0;
+    int st = apd_set_problem(ctx, &prob);
+    if (st != APD_OK) { SAY("apd_set_problem failed: " << apd_last_error(ctx)); return false; }
+    const auto t0 = std::chrono::steady_clock::now();
+    st = apd_run_patchmatch(ctx);
+    const auto t1 = std::chrono::steady_clock::now();
+    if (st != APD_OK) { SAY("apd_run_patchmatch failed: " << apd_last_error(ctx)); return false; }
+    const long ms = (long)std::chrono::duration_cast<std::chrono::milliseconds>(t1 - t0).count();
+    {
+        std::lock_guard<std::mutex> g(g_print);
+        printf("RunPatchMatch time: %ld ms\n", ms);
+        fflush(stdout);
+    }
+    job.used_ms += ms;
+    // ---- results
+    std::vector<float> planes(HW * 4);
+    Mat depth(height, width, CV_32FC1), normal(height, width, CV_32FC3), states(height, width, CV_8UC1),
+        confidence(height, width, CV_8UC1);
+    std::vector<int16_t> anchors;
+    std::vector<float> curve;
+    int32_t wc = 0;
+    apd_outputs out{};
+    out.planes = planes.data();
+    out.weak_info = states.ptr<uint8_t>();
+    out.confidence = confidence.ptr<uint8_t>();
+    out.weak_count = &wc;
+    if (job.export_anchor && P.use_APD) {
+        anchors.resize((size_t)std::max(weak_count, 1) * APD_ANCHOR_NUM * 2);
+        out.anchors = anchors.data();
+    }
+    if (job.export_curve) {
+        curve.resize(HW * APD_CURVE_SAMPLES);
+        out.reliable_curve = curve.data();
+    }
+    st = apd_get_results(ctx, &out);
+    if (st != APD_OK) { SAY("apd_get_results failed: " << apd_last_error(ctx)); return false; }
+    if (!(P.geom_consistency || P.use_APD)) memset(confidence.data.data(), 1, confidence.data.size());
+    apd_epilogue(width, height, planes.data(), P.depth_min, P.depth_max, depth.ptr<float>(), normal.ptr<float>(),
+                 states.ptr<uint8_t>());
+    // ---- exports (APD.cu:2614-2626, 2649-2660); written immediately, they are not priors
+    if (job.export_anchor && P.use_APD) {
+        write_binmat_file(result_folder + "/anchors_map.bin", anchors_map);
+        FILE *fa = fopen((result_folder + "/anchors.bin").c_str(), "wb");
+        if (fa) {
+            const int32_t n = wc, k = APD_ANCHOR_NUM;
+            fwrite(&n, 4, 1, fa);
+            fwrite(&k, 4, 1, fa);
+            fwrite(anchors.data(), sizeof(int16_t) * 2, (size_t)wc * APD_ANCHOR_NUM, fa);
+            fclose(fa);
+        }
+    }
+    if (job.export_curve) {
+        FILE *fc = fopen((result_folder + "/reliable_curve.bin").c_str(), "wb");
+        if (fc) {
+            const int32_t w32 = width, h32 = height, ns = APD_CURVE_SAMPLES;
+            fwrite(&w32, 4, 1, fc);
+            fwrite(&h32, 4, 1, fc);
+            fwrite(&ns, 4, 1, fc);
+            fwrite(curve.data(), sizeof(float), curve.size(), fc);
+            fclose(fc);
+        }
+    }
+    emit(result_folder + "/depths.bin", depth);
+    emit(result_folder + "/normals.bin", normal);
+    emit(result_folder + "/weak.bin", states);
+    if (P.geom_consistency || P.use_APD) emit(result_folder + "/confidence.bin", confidence);
+    const auto end = std::chrono::steady_clock::now();
+    {
+        std::lock_guard<std::mutex> g(g_print);
+        std::cout << "Processing image: " << format_index(pb.ref_image_id) << " done!" << std::endl;
+        std::cout << "Cost time: " << std::chrono::duration_cast<std::chrono::milliseconds>(end - start).count()
+                  << " ms" << std::endl;
+    }
+    return true;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    auto vm = parse_args(argc, argv);
+    const std::string dense = vm["dense_folder"];
+    const int gpu_index = std::atoi(vm["gpu_index"].c_str());
+    const std::string dataset = vm["dataset"];
+    const bool only_fuse = as_bool(vm, "only_fuse");
+    const bool no_fuse = as_bool(vm, "no_fuse");
+    bool use_memory_cache = as_bool(vm, "memory_cache");
+    const bool use_sa = as_bool(vm, "use_sa");
+    const bool use_impetus = as_bool(vm, "use_impetus");
+    const bool weak_filter = as_bool(vm, "weak_filter");
+    bool flush = as_bool(vm, "flush");
+    const bool export_anchor = as_bool(vm, "export_anchor");
+    const bool export_curve = as_bool(vm, "export_curve");
+    const bool export_color = as_bool(vm, "export_color");
+    if (only_fuse) use_memory_cache = false;
+    if (no_fuse) flush = true;
+    std::vector<int> gpus;
+    {
+        std::stringstream ss(vm["gpus"]);
+        std::string tok;
+        while (std::getline(ss, tok, ',')) if (!tok.empty()) gpus.push_back(std::atoi(tok.c_str()));
+        if (gpus.empty()) gpus.push_back(gpu_index);
+    }
+    std::string ordering = vm["ordering"];
+    if (ordering.empty()) ordering = gpus.size() > 1 ? "jacobi" : "sequential";
+    if (ordering != "sequential" && ordering != "jacobi") {
+        std::cout << "Error: --ordering must be sequential or jacobi" << std::endl;
+        return -1;
+    }
+    if (gpus.size() > 1 && ordering != "jacobi") {
+        std::cout << "Error: more than one GPU requires --ordering jacobi" << std::endl;
+        return -1;
+    }
+    std::cout << "========================== Config ==========================" << std::endl;
+    std::cout << "dense_folder : " << dense << std::endl;
+    std::cout << "gpu_index    : " << gpu_index << std::endl;
+    std::cout << "dataset      : " << dataset << std::endl;
+    std::cout << "only_fuse    : " << only_fuse << std::endl;
+    std::cout << "no_fuse      : " << no_fuse << std::endl;
+    std::cout << "memory_cache : " << use_memory_cache << std::endl;
+    std::cout << "use_sa       : " << use_sa << std::endl;
+    std::cout << "use_impetus  : " << use_impetus << std::endl;
+    std::cout << "weak_filter  : " << weak_filter << std::endl;
+    std::cout << "flush        : " << flush << std::endl;
+    std::cout << "export_anchor: " << export_anchor << std::endl;
+    std::cout << "export_curve : " << export_curve << std::endl;
+    std::cout << "export_color : " << export_color << std::endl;
+    std::cout << "gpus         : " << vm["gpus"] << std::endl;
+    std::cout << "ordering     : " << ordering << std::endl;
+    std::cout << "============================================================" << std::endl;
+    if (use_memory_cache) printf("Use memory cache!\n");
+    MatStore store(use_memory_cache);
+    make_dir(dense + "/APD");
+    std::vector<Problem> problems;
+    std::string err;
+    if (!read_pair_file(dense, problems, err)) {
+        std::cout << "Error: " << err << std::endl;
+        return -1;
+    }
+    for (auto &p : problems) make_dir(dense + "/APD/" + format_index(p.ref_image_id));
+    // CheckImages (main.cpp:104-127) + ComputeRoundNum (main.cpp:129-146)
+    int W0 = 0, H0 = 0;
+    for (size_t i = 0; i < problems.size(); ++i) {
+        Gray8 g;
+        if (!read_gray8(dense + "/images/" + format_index(problems[i].ref_image_id) + problems[i].img_ext, g, err) ||
+            (i > 0 && (g.width != W0 || g.height != H0))) {
+            std::cout << "Images may error, check it!\n";
+            return EXIT_FAILURE;
+        }
+        W0 = g.width;
+        H0 = g.height;
+    }
+    if (problems.empty()) {
+        std::cout << "Images may error, check it!\n";
+        return EXIT_FAILURE;
+    }
+    std::cout << "There are " << problems.size() << " problems needed to be processed!" << std::endl;
+    if (only_fuse) {
+        std::cout << "Fusion is outside this engine (DESIGN.md section 8): nothing to do for --only_fuse" << std::endl;
+        return EXIT_FAILURE;
+    }
+    int max_size = std::max(W0, H0), round_num = 1;
+    while (max_size > 800) {
+        max_size /= 2;
+        round_num++;
+    }
+    std::cout << "Round nums: " << round_num << std::endl;
+    const float geom_factor = (dataset == "TaT_a" || dataset == "TaT_i") ? 0.05f : 0.2f;
+
+    Driver drv;
+    drv.dense = dense;
+    drv.use_sa = use_sa;
+    drv.flush = flush;
+    drv.seed = std::strtoull(vm["seed"].c_str(), nullptr, 10);
+    drv.jacobi = ordering == "jacobi";
+    drv.store = &store;
+    std::vector<apd_ctx *> ctxs;
+    for (int d : gpus) {
+        apd_ctx *c = apd_create(d);
+        if (!c) {
+            std::cout << "apd_create(" << d << ") failed: " << apd_last_error(nullptr) << std::endl;
+            return EXIT_FAILURE;
+        }
+        ctxs.push_back(c);
+    }
+    std::vector<Job> jobs(problems.size());
+    for (size_t i = 0; i < problems.size(); ++i) jobs[i].pb = problems[i];
+    bool ok = true;
+    // one pass over all views: dynamic work queue over the devices
+    auto run_pass = [&]() {
+        std::atomic<size_t> next{0};
+        std::atomic<bool> good{true};
+        auto worker = [&](apd_ctx *ctx) {
+            for (size_t k; good && (k = next.fetch_add(1)) < jobs.size();)
+                if (!drv.process(ctx, jobs[k])) good = false;
+        };
+        if (ctxs.size() == 1) {
+            worker(ctxs[0]);
+        } else {
+            std::vector<std::thread> th;
+            for (apd_ctx *c : ctxs) th.emplace_back(worker, c);
+            for (auto &t : th) t.join();
+        }
+        drv.commit();
+        return (bool)good;
+    };
+    auto base_params = [&]() {
+        apd_params p{};
+        p.max_iterations = 3;
+        p.top_k = 4;
+        p.use_impetus = use_impetus;
+        p.strong_radius = 5;
+        p.strong_increment = 2;
+        p.weak_radius = 5;
+        p.weak_increment = 5;
+        p.use_sa = use_sa;
+        p.weak_peak_radius = 6;
+        p.rotate_time = 4;
+        p.ransac_threshold = 0.005f;
+        p.geom_factor = geom_factor;
+        return p;
+    };
+    // round schedule (main.cpp:290-367)
+    int iteration_index = 0;
+    const int geom_iteration = 3;
+    const auto start = std::chrono::steady_clock::now();
+    for (int i = 0; i < round_num && ok; ++i) {
+        std::cout << "========================== Round " << i << " ==========================" << std::endl;
+        std::cout << "======== iteration " << iteration_index << "========" << std::endl;
+        for (auto &job : jobs) {
+            apd_params p = base_params();
+            if (i == 0) {
+                p.state = APD_FIRST_INIT;
+                p.use_APD = 0;
+            } else {
+                p.state = APD_REFINE_INIT;
+                p.use_APD = 1;
+                p.ransac_threshold = (float)(0.01 - i * 0.00125);
+                p.rotate_time = std::min((int)std::pow(2, i), 4);
+            }
+            p.geom_consistency = 0;
+            p.weak_peak_radius = 6;
+            job.params = p;
+            job.iteration = iteration_index;
+            job.scale_size = (int)std::pow(2, round_num - 1 - i);
+        }
+        ok = run_pass();
+        iteration_index++;
+        for (int j = 0; j < geom_iteration && ok; ++j) {
+            std::cout << "======== iteration " << iteration_index << "========" << std::endl;
+            const bool is_last = (i == round_num - 1 && j == geom_iteration - 1);
+            for (auto &job : jobs) {
+                apd_params p = base_params();
+                p.state = APD_REFINE_ITER;
+                if (i == 0) {
+                    p.use_APD = 0;
+                } else {
+                    p.use_APD = 1;
+                    p.ransac_threshold = (float)(0.01 - i * 0.00125);
+                    p.rotate_time = std::min((int)std::pow(2, i), 4);
+                }
+                p.geom_consistency = 1;
+                p.weak_peak_radius = std::max(4 - 2 * j, 2);
+                job.params = p;
+                job.export_anchor = is_last && export_anchor;
+                job.export_curve = is_last && export_curve;
+                job.iteration = iteration_index;
+                job.scale_size = (int)std::pow(2, round_num - 1 - i);
+            }
+            ok = run_pass();
+            iteration_index++;
+        }
+        std::cout << "=============================================================" << std::endl;
+    }
+    for (apd_ctx *c : ctxs) apd_destroy(c);
+    if (!ok) return EXIT_FAILURE;
+    const auto end = std::chrono::steady_clock::now();
+    std::cout << "Cost time: " << std::chrono::duration_cast<std::chrono::milliseconds>(end - start).count() << " ms"
+              << std::endl;
+    long avg = 0;
+    for (auto &j : jobs) avg += j.used_ms;
+    avg /= (long)jobs.size();
+    std::cout << "Average used time: " << avg << " ms" << std::endl;
+    if (use_memory_cache && flush) {
+        printf("Write memory cache to disk!\n");
+        store.flush_all();
+        printf("All done!\n");
+    }
+    if (no_fuse) {
+        printf("Skip fusion, all done!\n");
+        return EXIT_SUCCESS;
+    }
+    std::cout << "Run fusion\n";
+    std::cout << "Fusion is outside this engine (DESIGN.md section 8); depth maps are in " << dense << "/APD"
+              << std::endl;
+    std::cout << "All done\n";
+    return EXIT_SUCCESS;
+}

@@ -1,0 +1,29 @@
+// capi.cpp — C entry points over the host helpers, for the CPU tests (tests/test_host.py) only.
+#include <cstring>
+#include <string>
+
+#include "image.h"
+#include "io.h"
+
+using namespace apdhost;
+
+extern "C" {
+// decode an image file to gray; returns width*height (copied into out if out_cap suffices) or < 0
+long apdhost_read_gray8(const char *path, unsigned char *out, long out_cap, int *w, int *h) {
+    Gray8 g;
+    std::string err;
+    if (!read_gray8(path, g, err)) return -1;
+    *w = g.width;
+    *h = g.height;
+    const long n = (long)g.px.size();
+    if (out && out_cap >= n) memcpy(out, g.px.data(), n);
+    return n;
+}
+void apdhost_resize_linear_f32(const float *src, int sw, int sh, float *dst, int dw, int dh) {
+    resize_linear_f32(src, sw, sh, dst, dw, dh);
+}
+void apdhost_resize_nearest(const void *src, int sw, int sh, void *dst, int dw, int dh, int elem) {
+    resize_nearest(src, sw, sh, dst, dw, dh, elem);
+}
+int apdhost_read_camera(const char *path, apd_camera *cam) { return read_camera(path, *cam) ? 0 : -1; }
+}

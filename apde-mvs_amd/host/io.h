@@ -1,0 +1,67 @@
+// io.h — on-disk contract of the reference's depth binary, restated without OpenCV/Boost:
+// bin-mat files (APD.cpp:18-83), MVSNet cam.txt (APD.cpp:85-135), pair.txt (main.cpp:44-102),
+// and the MemoryCache write-back semantics (APD.cpp:3-16, main.cpp:381-393).
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/apd_hip.h"
+
+namespace apdhost {
+
+// OpenCV type codes used by the reference's bin-mat files
+enum { CV_8UC1 = 0, CV_32SC1 = 4, CV_32FC1 = 5, CV_32FC3 = 21 };
+int cv_elem_size(int type);
+
+struct Mat {
+    int rows = 0, cols = 0, type = CV_8UC1;
+    std::vector<uint8_t> data;  // row-major, rows * cols * elem bytes
+    Mat() = default;
+    Mat(int r, int c, int t) : rows(r), cols(c), type(t), data((size_t)r * c * cv_elem_size(t)) {}
+    template <class T> T *ptr() { return reinterpret_cast<T *>(data.data()); }
+    template <class T> const T *ptr() const { return reinterpret_cast<const T *>(data.data()); }
+    bool empty() const { return rows == 0 || cols == 0; }
+};
+Mat resize_nearest(const Mat &m, int w, int h);
+
+// MemoryCache (APD.cpp:3-16): when enabled, bin-mat writes land in memory and reach the disk only
+// when flushed; reads check the cache first. Thread-safe.
+class MatStore {
+public:
+    explicit MatStore(bool cache) : cache_(cache) {}
+    bool read(const std::string &path, Mat &m);                    // ReadBinMat   APD.cpp:18-56
+    bool write(const std::string &path, const Mat &m, bool flush);  // WriteBinMat  APD.cpp:58-83
+    void flush_all();                                              // main.cpp:381-393
+    bool cached() const { return cache_; }
+
+private:
+    bool cache_;
+    std::mutex mu_;
+    std::map<std::string, Mat> mats_;
+};
+
+bool read_binmat_file(const std::string &path, Mat &m);
+bool write_binmat_file(const std::string &path, const Mat &m);
+
+// ReadCamera (APD.cpp:85-135): extrinsic 4x4 (last row ignored), intrinsic 3x3, depth_min interval
+// [depth_num depth_max] with the depth_num = 192 fallback; centre c = -R^T t in double.
+bool read_camera(const std::string &path, apd_camera &cam);
+
+struct Problem {  // main.h:102-115
+    int ref_image_id = 0;
+    std::vector<int> src_image_ids;
+    std::string img_ext;
+};
+// GenerateSampleList (main.cpp:44-102): sources with score <= 0 are dropped; the image extension
+// is the first of .jpg .png .jpeg .JPG .PNG .JPEG present for the reference image.
+bool read_pair_file(const std::string &dense_folder, std::vector<Problem> &problems, std::string &err);
+
+std::string format_index(int id);  // ToFormatIndex: %08d
+bool file_exists(const std::string &p);
+bool make_dir(const std::string &p);
+
+}  // namespace apdhost

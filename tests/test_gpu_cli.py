@@ -1,0 +1,99 @@
+"""GPU: the `apd` binary (apde-mvs_amd/host) over a synthetic MVSNet scan, whole reference schedule.
+
+The scan is 1000x750 with 5 views, so main.cpp's schedule has 2 rounds: FIRST_INIT + 3 geometric
+passes at 500x375, then REFINE_INIT with APD (anchors, RANSAC, weak sweep, SA masks) + 3 geometric
+APD passes at full size. Every view's final depths.bin / normals.bin / weak.bin / confidence.bin must
+equal, bit for bit, the same schedule restated in Python (tests/host_schedule.py) driving the HIP
+library directly -- which the parity tests tie to the oracle. This checks the whole host side:
+image decode + resize, cam parsing, K scaling, prior resizing, anchors map, epilogue, bin-mat
+files, seeds, and the sequential vs jacobi pass orderings (jacobi on two device contexts).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import apd_abi as A
+import host_schedule as HS
+import synth
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+APD_BIN = os.path.join(REPO, "apde-mvs_amd", "host", "build", "apd")
+
+
+@pytest.fixture(scope="module")
+def engine():
+    lib = A.load_library()
+    if lib.apd_device_count() < 1:
+        pytest.fail("no HIP device visible")
+    eng = A.Engine(0, lib)
+    yield eng
+    eng.close()
+
+
+@pytest.fixture(scope="module")
+def scan(tmp_path_factory):
+    sc = synth.make_scene(1000, 750, 4, seed=7)
+    folder = str(tmp_path_factory.mktemp("scan"))
+    HS.write_dense_folder(sc, folder, ext=".png", masks=True)
+    return folder
+
+
+def run_engine(engine):
+    def fn(arr):
+        engine.set_problem(arr)
+        engine.run()
+        return engine.results(A.Outputs(arr.width, arr.height, len(arr.images) - 1))
+    return fn
+
+
+def check_outputs(folder, expected):
+    for ref, exp in expected.items():
+        d = os.path.join(folder, "APD", f"{ref:08d}")
+        depth = synth.read_bin_mat(os.path.join(d, "depths.bin"))
+        normal = synth.read_bin_mat(os.path.join(d, "normals.bin"))
+        weak = synth.read_bin_mat(os.path.join(d, "weak.bin"))
+        conf = synth.read_bin_mat(os.path.join(d, "confidence.bin"))
+        assert np.array_equal(depth.view(np.uint32), exp["depth"].view(np.uint32)), f"depth of view {ref}"
+        assert np.array_equal(normal.view(np.uint32), exp["normal"].view(np.uint32)), f"normal of view {ref}"
+        assert np.array_equal(weak, exp["weak"]), f"weak of view {ref}"
+        assert np.array_equal(conf, exp["conf"]), f"confidence of view {ref}"
+        assert (depth > 0).mean() > 0.5
+
+
+@pytest.mark.parametrize("ordering,gpus", [("sequential", "0"), ("jacobi", "0,0")])
+def test_cli_matches_schedule(scan, engine, ordering, gpus, tmp_path):
+    import shutil
+    folder = str(tmp_path / "run")
+    shutil.copytree(scan, folder)
+    r = subprocess.run([APD_BIN, "--dense_folder", folder, "--dataset", "ETH3D", "--no_fuse", "true",
+                        "--memory_cache", "false", "--gpus", gpus, "--ordering", ordering],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "Round nums: 2" in r.stdout
+    assert r.stdout.count("RunPatchMatch time:") == 5 * 8
+    expected = HS.run_schedule(folder, run_engine(engine), ordering=ordering)
+    check_outputs(folder, expected)
+
+
+def test_cli_memory_cache_flush(scan, tmp_path):
+    """--memory_cache true: nothing reaches the disk until the final flush (--no_fuse forces it)."""
+    import shutil
+    folder = str(tmp_path / "run")
+    shutil.copytree(scan, folder)
+    r = subprocess.run([APD_BIN, "--dense_folder", folder, "--no_fuse", "true", "--memory_cache", "true",
+                        "--export_anchor", "true", "--export_curve", "true"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "Write memory cache to disk!" in r.stdout
+    d = os.path.join(folder, "APD", "00000000")
+    for f in ("depths.bin", "normals.bin", "weak.bin", "confidence.bin", "anchors.bin", "anchors_map.bin",
+              "reliable_curve.bin"):
+        assert os.path.exists(os.path.join(d, f)), f
+    hdr = np.fromfile(os.path.join(d, "reliable_curve.bin"), np.int32, 3)
+    assert list(hdr) == [1000, 750, 61]
+    am = synth.read_bin_mat(os.path.join(d, "anchors_map.bin"))
+    n_weak, k = np.fromfile(os.path.join(d, "anchors.bin"), np.int32, 2)
+    assert k == 9 and n_weak == int((am >= 0).sum())
