@@ -1,0 +1,90 @@
+"""CPU (gloo, world_size 2): the view-sharded scan runner (apde-mvs_amd/scan_runner.py).
+
+Two ranks each process half of the views of every pass and exchange the new depth maps with one
+torch.distributed all-gather per pass. The files they write must equal, bit for bit, the Jacobi
+schedule restated in tests/host_schedule.py on one process -- with the CPU oracle standing in for the
+HIP engine (test infrastructure; the runner itself only takes a run_fn). A 1-rank run must give the
+same files, i.e. the result does not depend on the number of ranks.
+"""
+import os
+import shutil
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import host_schedule as HS
+import oracle_lib
+import synth
+
+
+def _oracle_fn():
+    lib = oracle_lib.load()
+    return lambda arr: oracle_lib.run(lib, arr, nthreads=2)
+
+
+def _rank_main(rank, world, folder, port):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.join(os.path.dirname(here), "apde-mvs_amd")]
+    import torch.distributed as dist
+    import scan_runner as SR
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    SR.run_scan(folder, _oracle_fn(), rank, world, SR.Exchange(world, rank, None))
+    dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def scan(tmp_path_factory):
+    sc = synth.make_scene(128, 96, 3, seed=11)
+    folder = str(tmp_path_factory.mktemp("scan"))
+    HS.write_dense_folder(sc, folder, ext=".png", masks=True)
+    expected = HS.run_schedule(folder, _oracle_fn(), ordering="jacobi")
+    return folder, expected
+
+
+def _check(folder, expected):
+    for ref, exp in expected.items():
+        d = os.path.join(folder, "APD", f"{ref:08d}")
+        for name, key in (("depths.bin", "depth"), ("normals.bin", "normal"), ("weak.bin", "weak"),
+                          ("confidence.bin", "conf")):
+            got = synth.read_bin_mat(os.path.join(d, name))
+            e = exp[key]
+            if e.dtype == np.float32:
+                assert np.array_equal(got.view(np.uint32), e.view(np.uint32)), (ref, name)
+            else:
+                assert np.array_equal(got, e), (ref, name)
+
+
+def test_two_ranks_equal_single_process_jacobi(scan, tmp_path):
+    folder, expected = scan
+    run = str(tmp_path / "run")
+    shutil.copytree(folder, run)
+    port = 29500 + (os.getpid() % 2000)
+    mp.spawn(_rank_main, args=(2, run, port), nprocs=2, join=True)
+    _check(run, expected)
+
+
+def test_one_rank_equals_jacobi(scan, tmp_path):
+    import scan_runner as SR
+    folder, expected = scan
+    run = str(tmp_path / "run")
+    shutil.copytree(folder, run)
+    SR.run_scan(run, _oracle_fn(), 0, 1, None)
+    _check(run, expected)
+
+
+def test_runner_matches_restated_host_io(scan):
+    """The runner's C++-backed decode/resize/camera path agrees with the Python restatement."""
+    import scan_runner as SR
+    folder, _ = scan
+    host = SR.HostLib()
+    img = host.read_gray(os.path.join(folder, "images", "00000000.png")).astype(np.float32)
+    from PIL import Image
+    assert np.array_equal(img, np.asarray(Image.open(os.path.join(folder, "images", "00000000.png")), np.float32))
+    assert np.array_equal(host.resize_linear(img, 64, 48), HS.resize_linear(img, 64, 48))
+    cam = host.read_camera(os.path.join(folder, "cams", "00000001_cam.txt"))
+    exp = HS.read_cam(os.path.join(folder, "cams", "00000001_cam.txt"))
+    for k in ("K", "R", "t", "c"):
+        assert np.array_equal(cam[k], exp[k])
