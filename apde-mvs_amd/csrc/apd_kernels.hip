@@ -1057,7 +1057,9 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     for (int t = wave, kt = 0; t < 5 * N; t += VM_WAVES, ++kt) {
         const int k = t / N, v = t - k * N;
         float cv = 0.0f;
-        if (pv1) {
+        // a view with sampled weight 0 contributes fmaf(0, cv, tc) == tc for every finite cv (costs are
+        // clamped to [0, 2]), so its refinement NCCs are skipped without changing any result
+        if (pv1 && wts[v * VM_P + p1] > 0) {
             const float4 tp = L.cand[k * VM_P + p1];
             bool slow;
             cv = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, tp, rw, slow);
@@ -1330,6 +1332,162 @@ __global__ __launch_bounds__(BLOCK) void k_filter(Args a, const int *__restrict_
 
 // DepthToWeak (APD.cu:2103-2250): 61-sample disparity sweep of the selected views -> PixelState.
 // The cost curve of each pixel is staged in LDS for the peak analysis.
+// ---------------------------------------------------------------------------------------------
+// View-major DepthToWeak (same function as k_depth_to_weak): a workgroup owns a 64-pixel row strip;
+// the 61 x N (depth sample, view) NCC tasks run with lane = pixel and one source view per wave task,
+// in chunks whose costs go to an LDS table; then the in-order weighted view sums per (pixel, depth)
+// and the peak analysis. Waves skip every task none of their pixels selected (selected_views is
+// spatially coherent), which the lanes = views layout could not.
+// ---------------------------------------------------------------------------------------------
+#define DW_CHUNK_BYTES 32768
+struct DwLds {
+    float refw[36 * VM_P];
+    float pc[61 * VM_P];        // cost curve per pixel [d][p]
+    float4 pl[VM_P];            // ref-frame plane
+    float base[VM_P], disp[VM_P], wn[VM_P];
+    uint32_t sel[VM_P];
+    int active[VM_P];
+};
+static inline int dw_chunk(int N) { return std::max(1, std::min(61, DW_CHUNK_BYTES / (N * VM_P * (int)sizeof(float)))); }
+static inline size_t dw_lds_bytes(int N) {
+    return sizeof(DwLds) + (size_t)dw_chunk(N) * N * VM_P * sizeof(float) + (size_t)N * VM_P * sizeof(int);
+}
+template <bool F16>
+__global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, int chunk) {
+    const int N = a.N, W = a.W, H = a.H;
+    DwLds &L = *reinterpret_cast<DwLds *>(apd_dyn_lds);
+    float *tcL = reinterpret_cast<float *>(&L + 1);           // [chunk][N][64]
+    int *wts = reinterpret_cast<int *>(tcL + chunk * N * VM_P); // [N][64]
+    const int first = blockIdx.x * VM_P;
+    const int np = min(VM_P, a.HW - first);
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
+    const APD_G Cam &cam0 = a.cams[0];
+    const int p = lane;
+    const bool pv = p < np;
+    const int c = first + min(p, np - 1);
+    const int py = c / W, px = c - py * W;
+    // ---- P0: per-pixel inputs, view weights, reference window
+    if (pv) {
+        if (wave == 0) {
+            L.pl[p] = to_ref(cam0, a.plane[c]);
+            L.sel[p] = a.sel[c];
+        }
+        for (int v = wave; v < N; v += VM_WAVES) wts[v * VM_P + p] = a.vw[(size_t)v * a.HW + c];
+        for (int k = wave; k < 36; k += VM_WAVES) {
+            const int i = k / 6, j = k - 6 * (k / 6);
+            L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
+        }
+    }
+    __syncthreads();
+    if (wave == 0 && pv) {  // baseline / weight norm over the selected views, in view order
+        const uint32_t sv = L.sel[p];
+        float base = 0.0f, wn = 0.0f;
+        int valid = 0;
+        for (int k = 0; k < N; ++k) {
+            const APD_G Cam &sc = a.cams[k + 1];
+            const float d0 = cam0.c[0] - sc.c[0], d1 = cam0.c[1] - sc.c[1], d2 = cam0.c[2] - sc.c[2];
+            const float dk = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+            if ((sv >> k) & 1u) { wn += (float)wts[k * VM_P + p]; base += dk; valid++; }
+        }
+        const float od = L.pl[p].w;
+        const bool border = px < 6 || py < 6 || px >= W - 6 || py >= H - 6;
+        const bool active = !(border || od == 0) && valid != 0;
+        if (active) base /= (float)valid;
+        L.base[p] = base;
+        L.wn[p] = wn;
+        L.disp[p] = cam0.K[0] * base / od;
+        L.active[p] = active;
+    }
+    __syncthreads();
+    const RefWin rw = refwin_from_lds<VM_P>(&L.refw[p]);
+    const bool act = pv && L.active[p] != 0;
+    const float base = L.base[p], disp = L.disp[p], wn = L.wn[p];
+    const uint32_t sv = L.sel[p];
+    const float4 pl = L.pl[p];
+    const bool geom = a.geom != 0;
+    const float gf = a.gf;
+    for (int d0 = 0; d0 < 61; d0 += chunk) {
+        const int dc = min(chunk, 61 - d0);
+        // ---- P1: (depth, view) tasks, lane = pixel
+        uint64_t defer = 0;
+        for (int t = wave, k = 0; t < dc * N; t += VM_WAVES, ++k) {
+            const int dd = t / N, v = t - dd * N;
+            const int d = d0 + dd;
+            const float pdepth = cam0.K[0] * base / (disp + (float)(d - 30));
+            const bool in_range = !(pdepth < a.dmin || pdepth > a.dmax);
+            float tc = 0.0f;
+            if (act && in_range && ((sv >> v) & 1u)) {
+                float4 tp = pl;
+                tp.w = dist2origin(cam0, px, py, pdepth, tp);
+                bool slow;
+                tc = ncc_old_fast<F16, VM_P>(a, px, py, v + 1, tp, rw, slow);
+                if (slow) defer |= 1ull << k;
+                if (geom) tc = fmaf(gf, geom_cost(a, px, py, v + 1, tp), tc);
+            }
+            tcL[t * VM_P + p] = tc;
+        }
+        while (defer) {
+            const int k = __builtin_ctzll(defer);
+            defer &= defer - 1;
+            const int t = wave + k * VM_WAVES, dd = t / N, v = t - dd * N;
+            const float pdepth = cam0.K[0] * base / (disp + (float)(d0 + dd - 30));
+            float4 tp = pl;
+            tp.w = dist2origin(cam0, px, py, pdepth, tp);
+            float tc = ncc_old_slow<F16>(a.self, px, py, v + 1, tp, rw.r, VM_P, rw.mean, rw.var);
+            if (geom) tc = fmaf(gf, geom_cost(a, px, py, v + 1, tp), tc);
+            tcL[t * VM_P + p] = tc;
+        }
+        __syncthreads();
+        // ---- P2: in-order weighted view sums per (pixel, depth)
+        for (int dd = wave; dd < dc; dd += VM_WAVES) {
+            const int d = d0 + dd;
+            const float pdepth = cam0.K[0] * base / (disp + (float)(d - 30));
+            const bool in_range = !(pdepth < a.dmin || pdepth > a.dmax);
+            float pval = 0.0f;
+            for (int k = 0; k < N; ++k)
+                if ((sv >> k) & 1u) pval = fmaf(tcL[(dd * N + k) * VM_P + p], (float)wts[k * VM_P + p], pval);
+            pval /= wn;
+            const float val = in_range ? ((2.0f > pval) ? pval : 2.0f) : 2.0f;
+            L.pc[d * VM_P + p] = val;
+            if (a.curve && act) a.curve[(size_t)c * 61 + d] = val;
+        }
+        __syncthreads();
+    }
+    // ---- P3: peak analysis (APD.cu:2200-2248)
+    if (wave == 0 && pv) {
+        int state = APD_UNKNOWN;
+        if (act) {
+            const float *pc = &L.pc[p];
+            int cnt = 0, min_peak = 0;
+            float min_cost = 2.0f;
+            uint64_t peaks = 0;
+            for (int i = 2; i < 59; ++i) {
+                const float ci = pc[i * VM_P];
+                if (pc[(i - 1) * VM_P] > ci && pc[(i + 1) * VM_P] > ci) {
+                    peaks |= 1ull << i;
+                    cnt++;
+                    if (ci < min_cost) { min_peak = i; min_cost = ci; }
+                }
+            }
+            if (abs(min_peak - 30) > a.peak_radius || pc[min_peak * VM_P] > 0.5f) {
+                state = APD_WEAK;
+            } else if (cnt == 1) {
+                state = (pc[min_peak * VM_P] <= 0.15f) ? APD_STRONG : APD_WEAK;
+            } else {
+                float var = 0.0f;
+                for (int i = 2; i < 59; ++i) {
+                    if (((peaks >> i) & 1ull) && i != min_peak) { float dd = pc[i * VM_P] - min_cost; var = fmaf(dd, dd, var); }
+                }
+                var = sqrtf(var);
+                var /= (float)(cnt - 1);
+                state = (var > 0.2f) ? APD_STRONG : APD_WEAK;
+            }
+        }
+        a.weak[c] = (uint8_t)state;
+    }
+}
+
 template <bool F16>
 __global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
     const int N = a.N, W = a.W, H = a.H;
@@ -1721,9 +1879,13 @@ apd_ctx *apd_create(int32_t device) {
     ctx->sweep_vm = getenv("APD_SWEEP_LANES") == nullptr;
     // the view-major sweep's LDS grows with N (> 64 KiB from N = 15 on); gfx950 has 160 KiB per CU
     (void)hipFuncSetAttribute((const void *)k_sweep_strong_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)vm_lds_bytes(APD_MAX_IMAGES - 1));
+                              160 * 1024);
     (void)hipFuncSetAttribute((const void *)k_sweep_strong_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)vm_lds_bytes(APD_MAX_IMAGES - 1));
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_depth_to_weak_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_depth_to_weak_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     return ctx;
 }
 
@@ -2063,10 +2225,13 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
     }
     if (ctx->want_curve && ctx->curve.p) a.curve = devptr<decltype(a.curve)>(ctx->curve.p);
     {
-        const int P = WAVE / a.N;
-        const size_t lds = group_lds_bytes(a.N, 61 + 36);
-        (void)P;
-        LAUNCH_TEX(k_depth_to_weak, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), lds, s, a);
+        if (ctx->sweep_vm) {
+            LAUNCH_TEX(k_depth_to_weak_vm, dim3(blocks_for((size_t)a.HW, VM_P)), dim3(VM_BLOCK), dw_lds_bytes(a.N), s,
+                       a, dw_chunk(a.N));
+        } else {
+            const size_t lds = group_lds_bytes(a.N, 61 + 36);
+            LAUNCH_TEX(k_depth_to_weak, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), lds, s, a);
+        }
     }
     if (a.geom || a.use_apd) hipLaunchKernelGGL(k_confidence, dim3(gpx), dim3(BLOCK), 0, s, a);
     LAUNCH_TEX(k_local_refine, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);

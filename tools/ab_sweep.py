@@ -12,14 +12,19 @@ sc = synth.make_scene(W, H, N)
 arr = A.scene_problem(sc, 0, [j for j, _ in sc.pairs[0]][:N])
 engines = []
 for spec in sys.argv[1:]:
-    path, _, opt = spec.partition(":")   # "lib.so:f32" forces the fp32 quad texel layout
+    path, _, opt = spec.partition(":")   # "lib.so:f32" = fp32 quad texels; "lib.so:ENV=VAL,..." = env at create
+    envs = {}
     if opt == "f32":
-        os.environ["APD_TEX_F32"] = "1"
-    else:
-        os.environ.pop("APD_TEX_F32", None)
+        envs["APD_TEX_F32"] = "1"
+    elif opt:
+        envs = dict(kv.split("=", 1) for kv in opt.split(","))
+    for k, v in envs.items():
+        os.environ[k] = v
     lib = A.load_library(path)
     e = A.Engine(0, lib)
     e.set_problem(arr)
+    for k in envs:
+        os.environ.pop(k, None)
     e.prepare()
     e.iteration(0)
     e.synchronize()
