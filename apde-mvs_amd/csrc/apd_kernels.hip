@@ -186,18 +186,20 @@ __global__ __launch_bounds__(BLOCK) void k_list_fill(Args a, int mode, int colou
 // change any result (pixels of one colour are independent), only locality: pixels are listed by
 // 16x16 tiles, and inside a tile by 4x4 micro-tiles (8 same-colour pixels = one wavefront at N=8),
 // so a wavefront's and a workgroup's NCC windows overlap in the source images.
-#define TILE 16
-__device__ __forceinline__ void tile_pixel(int tile, int tiles_x, int k, int &x, int &y) {
-    const int micro = k >> 4, inner = k & 15;
-    const int lx = ((micro & 3) << 2) + (inner & 3);
-    const int ly = ((micro >> 2) << 2) + (inner >> 2);
-    x = (tile % tiles_x) * TILE + lx;
-    y = (tile / tiles_x) * TILE + ly;
+// List tiles: tw x th = 256 positions, visited in 4x4 micro-tiles (row-major inside the tile); a
+// sweep workgroup's 64 list entries are then a tw x th/2 region of one colour.
+#define TILE_POS 256
+__device__ __forceinline__ void tile_pixel(int tile, int tiles_x, int tw, int k, int &x, int &y) {
+    const int micro = k >> 4, inner = k & 15, mx = tw >> 2;
+    const int lx = ((micro % mx) << 2) + (inner & 3);
+    const int ly = ((micro / mx) << 2) + (inner >> 2);
+    x = (tile % tiles_x) * tw + lx;
+    y = (tile / tiles_x) * (TILE_POS / tw) + ly;
 }
-__global__ __launch_bounds__(BLOCK) void k_tile_count(Args a, int mode, int colour, int tiles_x,
+__global__ __launch_bounds__(BLOCK) void k_tile_count(Args a, int mode, int colour, int tiles_x, int tw,
                                                     int *__restrict__ counts) {
     int x, y;
-    tile_pixel(blockIdx.x, tiles_x, threadIdx.x, x, y);
+    tile_pixel(blockIdx.x, tiles_x, tw, threadIdx.x, x, y);
     const bool p = x < a.W && y < a.H && list_pred(a, mode, colour, x, y);
     __shared__ int wsum[BLOCK / WAVE];
     const int c = __popcll(__ballot(p));
@@ -205,10 +207,10 @@ __global__ __launch_bounds__(BLOCK) void k_tile_count(Args a, int mode, int colo
     __syncthreads();
     if (threadIdx.x == 0) counts[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
-__global__ __launch_bounds__(BLOCK) void k_tile_fill(Args a, int mode, int colour, int tiles_x,
+__global__ __launch_bounds__(BLOCK) void k_tile_fill(Args a, int mode, int colour, int tiles_x, int tw,
                                                    const int *__restrict__ offs, int *__restrict__ out) {
     int x, y;
-    tile_pixel(blockIdx.x, tiles_x, threadIdx.x, x, y);
+    tile_pixel(blockIdx.x, tiles_x, tw, threadIdx.x, x, y);
     const bool p = x < a.W && y < a.H && list_pred(a, mode, colour, x, y);
     __shared__ int wcnt[BLOCK / WAVE];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1353,20 +1355,23 @@ static inline size_t dw_lds_bytes(int N) {
     return sizeof(DwLds) + (size_t)dw_chunk(N) * N * VM_P * sizeof(float) + (size_t)N * VM_P * sizeof(int);
 }
 template <bool F16>
-__global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, int chunk) {
+__global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, int chunk, int tw) {
     const int N = a.N, W = a.W, H = a.H;
     DwLds &L = *reinterpret_cast<DwLds *>(apd_dyn_lds);
     float *tcL = reinterpret_cast<float *>(&L + 1);           // [chunk][N][64]
     int *wts = reinterpret_cast<int *>(tcL + chunk * N * VM_P); // [N][64]
-    const int first = blockIdx.x * VM_P;
-    const int np = min(VM_P, a.HW - first);
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
     const APD_G Cam &cam0 = a.cams[0];
     const int p = lane;
-    const bool pv = p < np;
-    const int c = first + min(p, np - 1);
-    const int py = c / W, px = c - py * W;
+    // the workgroup's pixels: a tw x (64/tw) tile (XCD-aware tile order); pixels outside the image idle
+    const int th = VM_P / tw, tiles_x = (W + tw - 1) / tw;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int tx = blk % tiles_x, ty = blk / tiles_x;
+    const int gx = tx * tw + (p % tw), gy = ty * th + (p / tw);
+    const bool pv = gx < W && gy < H;
+    const int px = min(gx, W - 1), py = min(gy, H - 1);
+    const int c = py * W + px;
     // ---- P0: per-pixel inputs, view weights, reference window
     if (pv) {
         if (wave == 0) {
@@ -1726,6 +1731,8 @@ struct apd_ctx {
     Args args{};
     bool loaded = false, prepared = false;
     bool sweep_vm = true;          // view-major Strong sweep (APD_SWEEP_LANES=1 selects k_sweep_strong)
+    int dw_tile_w = 8;             // DepthToWeak pixel tile width (64 / tile height); APD_DW_TILE_W
+    int tile_w = 8;                // sweep list tile width (tile = tile_w x 256/tile_w positions); APD_TILE_W
     int weak_count = 0;
     int cnt[4] = {0, 0, 0, 0};     // strong black, strong red, weak black, weak red
     size_t list_cap = 0;
@@ -1877,6 +1884,11 @@ apd_ctx *apd_create(int32_t device) {
     }
     for (auto &e : ctx->ev) (void)hipEventCreate(&e);
     ctx->sweep_vm = getenv("APD_SWEEP_LANES") == nullptr;
+    if (const char *e = getenv("APD_DW_TILE_W")) ctx->dw_tile_w = std::max(1, std::min(64, atoi(e)));
+    if (const char *e = getenv("APD_TILE_W")) {
+        const int t = atoi(e);
+        if (t == 4 || t == 8 || t == 16 || t == 32 || t == 64) ctx->tile_w = t;
+    }
     // the view-major sweep's LDS grows with N (> 64 KiB from N = 15 on); gfx950 has 160 KiB per CU
     (void)hipFuncSetAttribute((const void *)k_sweep_strong_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
@@ -1953,7 +1965,7 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     if ((st = ensure(ctx, ctx->conf, HW))) return st;
     if ((st = ensure(ctx, ctx->sa, HW))) return st;
     if ((st = ensure(ctx, ctx->lists, (HW + 8) * sizeof(int)))) return st;
-    const size_t units = std::max<size_t>((size_t)H, (size_t)((W + TILE - 1) / TILE) * ((H + TILE - 1) / TILE));
+    const size_t units = std::max<size_t>((size_t)H, (size_t)(W + 3) / 4 * ((H + 3) / 4));  // any tile shape
     if ((st = ensure(ctx, ctx->rowcnt, units * sizeof(int)))) return st;
     if ((st = ensure(ctx, ctx->rowoff, units * sizeof(int)))) return st;
     if ((st = ensure(ctx, ctx->totals, 8 * sizeof(int)))) return st;
@@ -2094,17 +2106,19 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
 // Sweep lists (modes 0/1) in tile order: count per tile, scan, fill.
 static void tile_count_scan(apd_ctx *ctx, int mode, int colour, int *total_dev) {
     Args &a = ctx->args;
-    const int tx = (a.W + TILE - 1) / TILE, ty = (a.H + TILE - 1) / TILE;
-    hipLaunchKernelGGL(k_tile_count, dim3(tx * ty), dim3(BLOCK), 0, ctx->stream, a, mode, colour, tx,
+    const int tw = ctx->tile_w, th = TILE_POS / tw;
+    const int tx = (a.W + tw - 1) / tw, ty = (a.H + th - 1) / th;
+    hipLaunchKernelGGL(k_tile_count, dim3(tx * ty), dim3(BLOCK), 0, ctx->stream, a, mode, colour, tx, tw,
                        (int *)ctx->rowcnt.p);
     hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(1024), 0, ctx->stream, (const int *)ctx->rowcnt.p, tx * ty,
                        (int *)ctx->rowoff.p, total_dev);
 }
 static int build_tile_list(apd_ctx *ctx, int mode, int colour, int *out, int *total_dev) {
     Args &a = ctx->args;
-    const int tx = (a.W + TILE - 1) / TILE, ty = (a.H + TILE - 1) / TILE;
+    const int tw = ctx->tile_w, th = TILE_POS / tw;
+    const int tx = (a.W + tw - 1) / tw, ty = (a.H + th - 1) / th;
     tile_count_scan(ctx, mode, colour, total_dev);
-    hipLaunchKernelGGL(k_tile_fill, dim3(tx * ty), dim3(BLOCK), 0, ctx->stream, a, mode, colour, tx,
+    hipLaunchKernelGGL(k_tile_fill, dim3(tx * ty), dim3(BLOCK), 0, ctx->stream, a, mode, colour, tx, tw,
                        (const int *)ctx->rowoff.p, out);
     return check_launch(ctx, "tile list build");
 }
@@ -2226,8 +2240,9 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
     if (ctx->want_curve && ctx->curve.p) a.curve = devptr<decltype(a.curve)>(ctx->curve.p);
     {
         if (ctx->sweep_vm) {
-            LAUNCH_TEX(k_depth_to_weak_vm, dim3(blocks_for((size_t)a.HW, VM_P)), dim3(VM_BLOCK), dw_lds_bytes(a.N), s,
-                       a, dw_chunk(a.N));
+            const int tw = ctx->dw_tile_w, th = VM_P / tw;
+            const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
+            LAUNCH_TEX(k_depth_to_weak_vm, dim3(nb), dim3(VM_BLOCK), dw_lds_bytes(a.N), s, a, dw_chunk(a.N), tw);
         } else {
             const size_t lds = group_lds_bytes(a.N, 61 + 36);
             LAUNCH_TEX(k_depth_to_weak, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), lds, s, a);
