@@ -832,7 +832,9 @@ __global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a,
 //   P3  lane = pixel, wave = (candidate, view) task: refinement NCC (+ geometric) -> LDS.
 //   P4  lane = pixel: in-order weighted candidate costs, acceptance, writes.
 // ---------------------------------------------------------------------------------------------
-#define VM_WAVES 8
+#ifndef VM_WAVES
+#define VM_WAVES 4  // 4-wave workgroups: 3 per CU at <= 170 VGPRs (the sweep needs ~154 without spills)
+#endif
 #define VM_BLOCK (VM_WAVES * WAVE)
 #define VM_P 64
 struct VmLds {  // static part; the cost table [9][N][64] follows (dynamic)
@@ -894,7 +896,7 @@ __device__ __forceinline__ int scan_direction(const APD_G float *__restrict__ co
 
 template <bool F16>
 #ifndef VM_MINW
-#define VM_MINW 4  // waves per SIMD -> VGPR budget 512 / VM_MINW
+#define VM_MINW 3  // waves per SIMD -> VGPR budget 512 / VM_MINW
 #endif
 __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, const int *__restrict__ list, int count,
                                                                   int iter) {
@@ -913,15 +915,17 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 
     // ---- P0: lane = (pixel, direction)
     {
-        const int p = lane, d = wave;
+        const int p = lane;
         if (p < np) {
             const int c = list[first + p];
             const int py = c / W, px = c - py * W;
-            const int q = scan_direction(a.cost, d, c, px, py, W, H);
-            L.npos[d * VM_P + p] = q;
-            if (q >= 0) L.hyp[d * VM_P + p] = a.plane[q];
-            if (d == 0) L.hyp[8 * VM_P + p] = a.plane[c];
-            for (int k = d; k < 36; k += VM_WAVES) {
+            for (int d = wave; d < 8; d += VM_WAVES) {
+                const int q = scan_direction(a.cost, d, c, px, py, W, H);
+                L.npos[d * VM_P + p] = q;
+                if (q >= 0) L.hyp[d * VM_P + p] = a.plane[q];
+            }
+            if (wave == 0) L.hyp[8 * VM_P + p] = a.plane[c];
+            for (int k = wave; k < 36; k += VM_WAVES) {
                 const int i = k / 6, j = k - 6 * (k / 6);
                 L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
             }
@@ -937,7 +941,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     const RefWin rw = refwin_from_lds<VM_P>(&L.refw[p1]);
     // tasks whose window needs the out-of-line path are collected in `defer` (bit k = k-th task of
     // this wave) and evaluated after the loop, so the hot loop holds no call.
-    uint64_t defer = 0;
+    uint64_t defer[2] = {0, 0};  // up to 128 tasks per wave (9 * 31 / VM_WAVES)
     for (int t = wave, k = 0; t < 9 * N; t += VM_WAVES, ++k) {
         const int h = t / N, v = t - h * N;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;  // float cost_array[8][32] = {2.0f} (APD.cu:1120)
@@ -946,14 +950,15 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
             const float4 pl = L.hyp[h * VM_P + p1];
             bool slow;
             val = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, pl, rw, slow);
-            if (slow) defer |= 1ull << k;
+            if (slow) defer[k >> 6] |= 1ull << (k & 63);
             if (h == 8 && geom_imp) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
         }
         costL[t * VM_P + p1] = val;
     }
-    while (defer) {
-        const int k = __builtin_ctzll(defer);
-        defer &= defer - 1;
+    for (int w2 = 0; w2 < 2; ++w2)
+    while (defer[w2]) {
+        const int k = __builtin_ctzll(defer[w2]) + 64 * w2;
+        defer[w2] &= defer[w2] - 1;
         const int t = wave + k * VM_WAVES, h = t / N, v = t - h * N;
         const float4 pl = L.hyp[h * VM_P + p1];
         float val = ncc_old_slow<F16>(a.self, px1, py1, v + 1, pl, rw.r, VM_P, rw.mean, rw.var);
@@ -1055,7 +1060,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     __syncthreads();
 
     // ---- P3: lane = pixel, wave = (candidate, view) tasks
-    defer = 0;
+    defer[0] = defer[1] = 0;
     for (int t = wave, kt = 0; t < 5 * N; t += VM_WAVES, ++kt) {
         const int k = t / N, v = t - k * N;
         float cv = 0.0f;
@@ -1065,14 +1070,15 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
             const float4 tp = L.cand[k * VM_P + p1];
             bool slow;
             cv = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, tp, rw, slow);
-            if (slow) defer |= 1ull << kt;
+            if (slow) defer[kt >> 6] |= 1ull << (kt & 63);
             if (geom_imp) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
         }
         costL[t * VM_P + p1] = cv;
     }
-    while (defer) {
-        const int kt = __builtin_ctzll(defer);
-        defer &= defer - 1;
+    for (int w2 = 0; w2 < 2; ++w2)
+    while (defer[w2]) {
+        const int kt = __builtin_ctzll(defer[w2]) + 64 * w2;
+        defer[w2] &= defer[w2] - 1;
         const int t = wave + kt * VM_WAVES, k = t / N, v = t - k * N;
         const float4 tp = L.cand[k * VM_P + p1];
         float cv = ncc_old_slow<F16>(a.self, px1, py1, v + 1, tp, rw.r, VM_P, rw.mean, rw.var);
