@@ -1499,6 +1499,279 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
     }
 }
 
+// Pixel tile of a view-major pixel kernel (RandomInit / DepthToWeak / LocalRefine): tw x 64/tw pixels
+// of the image in XCD-aware tile order; lanes outside the image idle.
+struct TilePix {
+    int px, py, c;
+    bool pv;
+};
+__device__ __forceinline__ TilePix tile_pix(const Args &a, int tw, int lane) {
+    const int th = VM_P / tw, tiles_x = (a.W + tw - 1) / tw;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int gx = (blk % tiles_x) * tw + (lane % tw), gy = (blk / tiles_x) * th + (lane / tw);
+    TilePix t;
+    t.pv = gx < a.W && gy < a.H;
+    t.px = min(gx, a.W - 1);
+    t.py = min(gy, a.H - 1);
+    t.c = t.py * a.W + t.px;
+    return t;
+}
+
+// ---------------------------------------------------------------------------------------------
+// View-major RandomInitialization + ComputeMultiViewInitialCostandSelectedViews (same function as
+// k_random_init): per-pixel plane (RNG draws in one lane), then the N per-view costs as wave tasks,
+// then the stable top-k of the N costs per pixel.
+// ---------------------------------------------------------------------------------------------
+struct RiLds {
+    float refw[36 * VM_P];
+    float4 pl[VM_P];
+};
+static inline size_t ri_lds_bytes(int N) { return sizeof(RiLds) + (size_t)N * VM_P * sizeof(float); }
+template <bool F16>
+__global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, int tw) {
+    const int N = a.N;
+    RiLds &L = *reinterpret_cast<RiLds *>(apd_dyn_lds);
+    float *cvL = reinterpret_cast<float *>(&L + 1);  // [N][64]
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (WAVE - 1);
+    const TilePix T = tile_pix(a, tw, lane);
+    const int p = lane, px = T.px, py = T.py, c = T.c;
+    const APD_G Cam &cam = a.cams[0];
+    if (T.pv) {
+        if (wave == 0) {
+            float4 pl;
+            if (a.state == APD_FIRST_INIT) {
+                Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_INIT);
+                float depth = g.uniform() * (a.dmax - a.dmin) + a.dmin;
+                pl = random_normal(cam, px, py, g, depth);
+                pl.w = dist2origin(cam, px, py, depth, pl);
+            } else {
+                pl = to_ref(cam, a.plane[c]);
+                float depth = pl.w;
+                pl.w = dist2origin(cam, px, py, depth, pl);
+            }
+            L.pl[p] = pl;
+        }
+        for (int k = wave; k < 36; k += VM_WAVES) {
+            const int i = k / 6, j = k - 6 * (k / 6);
+            L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
+        }
+    }
+    __syncthreads();
+    const RefWin rw = refwin_from_lds<VM_P>(&L.refw[p]);
+    const bool use_new = a.use_apd && a.weak[c] == APD_WEAK;
+    const float4 pl = L.pl[p];
+    uint64_t defer = 0;
+    for (int v = wave, k = 0; v < N; v += VM_WAVES, ++k) {
+        float cv = 0.0f;
+        if (T.pv) {
+            if (use_new) {
+                cv = ncc_new<F16>(a.self, px, py, v + 1, pl);
+            } else {
+                bool slow;
+                cv = ncc_old_fast<F16, VM_P>(a, px, py, v + 1, pl, rw, slow);
+                if (slow) defer |= 1ull << k;
+            }
+        }
+        cvL[v * VM_P + p] = cv;
+    }
+    while (defer) {
+        const int k = __builtin_ctzll(defer);
+        defer &= defer - 1;
+        const int v = wave + k * VM_WAVES;
+        cvL[v * VM_P + p] = ncc_old_slow<F16>(a.self, px, py, v + 1, pl, rw.r, VM_P, rw.mean, rw.var);
+    }
+    __syncthreads();
+    if (wave == 0 && T.pv) {
+        // stable top-k of the N costs (insertion sort, APD.cu:3-12, 754-769)
+        const int topk_max = 4;
+        float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+        int nt = 0, nvalid = 0;
+        for (int k = 0; k < N; ++k) {
+            const float x = cvL[k * VM_P + p];
+            if (x < APD_COST_MAX) nvalid++;
+            int q = (nt > 0 && t0 <= x) + (nt > 1 && t1 <= x) + (nt > 2 && t2 <= x) + (nt > 3 && t3 <= x);
+            if (q < topk_max) {
+                if (q <= 2) t3 = t2;
+                if (q <= 1) t2 = t1;
+                if (q <= 0) t1 = t0;
+                if (q == 0) t0 = x;
+                else if (q == 1) t1 = x;
+                else if (q == 2) t2 = x;
+                else t3 = x;
+                if (nt < topk_max) nt++;
+            }
+        }
+        const int top_k = min(nvalid, a.top_k);
+        const float thr = top_k <= 1 ? t0 : (top_k == 2 ? t1 : (top_k == 3 ? t2 : t3));
+        float cost_out = APD_COST_MAX;
+        uint32_t sv = 0;
+        if (top_k > 0) {
+            float sum = 0.0f;
+            sum += t0;
+            if (top_k > 1) sum += t1;
+            if (top_k > 2) sum += t2;
+            if (top_k > 3) sum += t3;
+            cost_out = sum / (float)top_k;
+            for (int k = 0; k < N; ++k) if (cvL[k * VM_P + p] <= thr) sv |= 1u << k;
+        }
+        a.plane[c] = pl;
+        a.cost[c] = cost_out;
+        a.sel_next[c] = sv;  // launch-start snapshot semantics (oracle k_random_init)
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// View-major LocalRefine (same function as k_local_refine, APD.cu:2346-2432): the current-depth costs
+// as N wave tasks, then the +-5 disparity candidates as (candidate, view) tasks in LDS chunks, with
+// the in-order weighted sums (NCC and geometric terms weighted separately, as the reference adds them).
+// ---------------------------------------------------------------------------------------------
+struct LrLds {
+    float refw[36 * VM_P];
+    float4 pl[VM_P];
+    float base[VM_P], disp[VM_P], wn[VM_P], cost_now[VM_P];
+    uint32_t sel[VM_P];
+    int run[VM_P];
+};
+static inline int lr_chunk(int N) { return std::max(1, std::min(11, 32768 / (2 * N * VM_P * (int)sizeof(float)))); }
+static inline size_t lr_lds_bytes(int N) {
+    return sizeof(LrLds) + (size_t)(2 * lr_chunk(N) + 1) * N * VM_P * sizeof(float) + (size_t)N * VM_P * sizeof(int);
+}
+template <bool F16>
+__global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, int chunk, int tw) {
+    const int N = a.N;
+    LrLds &L = *reinterpret_cast<LrLds *>(apd_dyn_lds);
+    float *t0L = reinterpret_cast<float *>(&L + 1);   // [N][64] current-depth costs
+    float *nvL = t0L + N * VM_P;                      // [chunk][N][64] NCC
+    float *gvL = nvL + chunk * N * VM_P;              // [chunk][N][64] gf * geometric
+    int *wts = reinterpret_cast<int *>(gvL + chunk * N * VM_P);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (WAVE - 1);
+    const TilePix T = tile_pix(a, tw, lane);
+    const int p = lane, px = T.px, py = T.py, c = T.c;
+    const APD_G Cam &cam0 = a.cams[0];
+    const bool geom = a.geom != 0;
+    const float gf = a.gf;
+    if (T.pv) {
+        if (wave == 0) {
+            L.pl[p] = to_ref(cam0, a.plane[c]);
+            L.sel[p] = a.sel[c];
+        }
+        for (int v = wave; v < N; v += VM_WAVES) wts[v * VM_P + p] = a.vw[(size_t)v * a.HW + c];
+        for (int k = wave; k < 36; k += VM_WAVES) {
+            const int i = k / 6, j = k - 6 * (k / 6);
+            L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
+        }
+    }
+    __syncthreads();
+    const RefWin rw = refwin_from_lds<VM_P>(&L.refw[p]);
+    const float4 pl = L.pl[p];
+    const float od = pl.w;
+    const uint32_t sv = L.sel[p];
+    const bool live = T.pv && od != 0;
+    // ---- current-depth costs, one task per view
+    {
+        uint64_t defer = 0;
+        for (int v = wave, k = 0; v < N; v += VM_WAVES, ++k) {
+            float tc0 = 0.0f;
+            if (live && ((sv >> v) & 1u)) {
+                float4 t = pl;
+                t.w = dist2origin(cam0, px, py, od, t);
+                bool slow;
+                tc0 = ncc_old_fast<F16, VM_P>(a, px, py, v + 1, t, rw, slow);
+                if (slow) defer |= 1ull << k;
+                if (geom) tc0 = fmaf(gf, geom_cost(a, px, py, v + 1, t), tc0);
+            }
+            t0L[v * VM_P + p] = tc0;
+        }
+        while (defer) {
+            const int k = __builtin_ctzll(defer);
+            defer &= defer - 1;
+            const int v = wave + k * VM_WAVES;
+            float4 t = pl;
+            t.w = dist2origin(cam0, px, py, od, t);
+            float tc0 = ncc_old_slow<F16>(a.self, px, py, v + 1, t, rw.r, VM_P, rw.mean, rw.var);
+            if (geom) tc0 = fmaf(gf, geom_cost(a, px, py, v + 1, t), tc0);
+            t0L[v * VM_P + p] = tc0;
+        }
+    }
+    __syncthreads();
+    if (wave == 0 && T.pv) {
+        float cost_now = 0.0f, base = 0.0f, wn = 0.0f;
+        int valid = 0;
+        for (int k = 0; k < N; ++k) {
+            const APD_G Cam &sc = a.cams[k + 1];
+            const float d0 = cam0.c[0] - sc.c[0], d1 = cam0.c[1] - sc.c[1], d2 = cam0.c[2] - sc.c[2];
+            const float dk = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+            if ((sv >> k) & 1u) {
+                const float wk = (float)wts[k * VM_P + p];
+                cost_now = fmaf(t0L[k * VM_P + p], wk, cost_now);
+                wn += wk;
+                base += dk;
+                valid++;
+            }
+        }
+        const bool run = live && !(wn == 0 || valid == 0);
+        if (run) { cost_now /= wn; base /= (float)valid; }
+        L.cost_now[p] = cost_now;
+        L.base[p] = base;
+        L.wn[p] = wn;
+        L.disp[p] = cam0.K[0] * base / od;
+        L.run[p] = run;
+    }
+    __syncthreads();
+    const bool run = T.pv && L.run[p] != 0;
+    const float base = L.base[p], disp = L.disp[p], wn = L.wn[p];
+    float min_cost = 2.0f, best = od;  // tracked by wave 0's lane of the pixel
+    for (int d0 = 0; d0 < 11; d0 += chunk) {
+        const int dc = min(chunk, 11 - d0);
+        uint64_t defer = 0;
+        for (int t = wave, k = 0; t < dc * N; t += VM_WAVES, ++k) {
+            const int dd = t / N, v = t - dd * N;
+            const int d = d0 + dd - 5;
+            const float pdepth = cam0.K[0] * base / (disp + (float)d);
+            const bool in_range = !(pdepth < a.dmin || pdepth > a.dmax);
+            float nv = 0.0f, gv = 0.0f;
+            if (run && in_range && ((sv >> v) & 1u)) {
+                float4 tp = pl;
+                tp.w = dist2origin(cam0, px, py, pdepth, tp);
+                bool slow;
+                nv = ncc_old_fast<F16, VM_P>(a, px, py, v + 1, tp, rw, slow);
+                if (slow) defer |= 1ull << k;
+                if (geom) gv = gf * geom_cost(a, px, py, v + 1, tp);
+            }
+            nvL[t * VM_P + p] = nv;
+            gvL[t * VM_P + p] = gv;
+        }
+        while (defer) {
+            const int k = __builtin_ctzll(defer);
+            defer &= defer - 1;
+            const int t = wave + k * VM_WAVES, dd = t / N, v = t - dd * N;
+            const float pdepth = cam0.K[0] * base / (disp + (float)(d0 + dd - 5));
+            float4 tp = pl;
+            tp.w = dist2origin(cam0, px, py, pdepth, tp);
+            nvL[t * VM_P + p] = ncc_old_slow<F16>(a.self, px, py, v + 1, tp, rw.r, VM_P, rw.mean, rw.var);
+        }
+        __syncthreads();
+        if (wave == 0 && T.pv) {
+            for (int dd = 0; dd < dc; ++dd) {
+                const float pdepth = cam0.K[0] * base / (disp + (float)(d0 + dd - 5));
+                const bool in_range = !(pdepth < a.dmin || pdepth > a.dmax);
+                float tc = 0.0f;
+                for (int k = 0; k < N; ++k) {
+                    if ((sv >> k) & 1u) {
+                        const float wk = (float)wts[k * VM_P + p];
+                        tc = fmaf(nvL[(dd * N + k) * VM_P + p], wk, tc);
+                        if (geom) tc = fmaf(gvL[(dd * N + k) * VM_P + p], wk, tc);
+                    }
+                }
+                tc /= wn;
+                if (run && in_range && tc < min_cost) { min_cost = tc; best = pdepth; }
+            }
+        }
+        __syncthreads();
+    }
+    if (wave == 0 && run && (double)(L.cost_now[p] - min_cost) > 0.1) a.plane[c].w = best;
+}
+
 template <bool F16>
 __global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
     const int N = a.N, W = a.W, H = a.H;
@@ -1904,6 +2177,14 @@ apd_ctx *apd_create(int32_t device) {
                               160 * 1024);
     (void)hipFuncSetAttribute((const void *)k_depth_to_weak_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_local_refine_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_local_refine_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_random_init_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_random_init_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     return ctx;
 }
 
@@ -2180,7 +2461,13 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         }
     }
     (void)hipEventRecord(ctx->ev[2], s);
-    LAUNCH_TEX(k_random_init, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);
+    if (ctx->sweep_vm) {
+        const int tw = ctx->dw_tile_w, th = VM_P / tw;
+        const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
+        LAUNCH_TEX(k_random_init_vm, dim3(nb), dim3(VM_BLOCK), ri_lds_bytes(a.N), s, a, tw);
+    } else {
+        LAUNCH_TEX(k_random_init, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);
+    }
     HIP_OK(ctx, hipMemcpyAsync(ctx->sel.p, ctx->sel2.p, (size_t)a.HW * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     if ((st = check_launch(ctx, "k_random_init"))) return st;
     (void)hipEventRecord(ctx->ev[3], s);
@@ -2255,7 +2542,13 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
         }
     }
     if (a.geom || a.use_apd) hipLaunchKernelGGL(k_confidence, dim3(gpx), dim3(BLOCK), 0, s, a);
-    LAUNCH_TEX(k_local_refine, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);
+    if (ctx->sweep_vm) {
+        const int tw = ctx->dw_tile_w, th = VM_P / tw;
+        const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
+        LAUNCH_TEX(k_local_refine_vm, dim3(nb), dim3(VM_BLOCK), lr_lds_bytes(a.N), s, a, lr_chunk(a.N), tw);
+    } else {
+        LAUNCH_TEX(k_local_refine, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);
+    }
     if ((st = check_launch(ctx, "finish"))) return st;
     return APD_OK;
 }
