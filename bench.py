@@ -102,7 +102,8 @@ def main():
         import torch
         import torch.distributed as tdist
 
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # nccl == RCCL on ROCm; APD_BENCH_BACKEND=gloo rehearses the N>1 path with several ranks on one GPU
+        backend = os.environ.get("APD_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local_rank)
         tdist.init_process_group(backend=backend)
@@ -121,7 +122,9 @@ def main():
     srcs = [j for j, _ in sc.pairs[ref]][:N]
     arr = A.scene_problem(sc, ref, srcs, seed=0x5EED ^ ref)
 
-    eng = A.Engine(local_rank)
+    lib = A.load_library()
+    device = local_rank % max(1, lib.apd_device_count())
+    eng = A.Engine(device, lib)
     eng.set_problem(arr)
     eng.prepare()
     eng.synchronize()
@@ -134,6 +137,8 @@ def main():
         if dist:
             torch, tdist, backend = dist
             tdist.barrier()
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
 
     eng.profile_reset(True)
     barrier()
@@ -149,7 +154,7 @@ def main():
     eng.profile_reset(False)
     if dist:
         torch, tdist, backend = dist
-        dev = torch.device("cuda", local_rank) if backend == "nccl" else torch.device("cpu")
+        dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
