@@ -1116,6 +1116,484 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 }
 
 // ---------------------------------------------------------------------------------------------
+// View-major Weak sweep (same function as k_sweep_weak). The reference side of
+// ComputeBilateralNCCNew -- the anchors' windows (6x6 centre patch, 3x3 anchor patches), their SA
+// tap masks and their (sr, srr, wsum) moments -- does not depend on the view or the plane, so it is
+// built once per pixel in LDS; each (plane, view) task then only projects and samples the source.
+//   P0  per pixel: anchors, hypothesis planes (STRONG anchors + current), fit plane, NCC-New ref data
+//   P1  (hypothesis, view) tasks, lane = pixel: NCC-New (+ geometric for the current plane)
+//   P2  lane = (pixel, view): view selection, geometric hypothesis terms, argmin + acceptance
+//   P3  fit-plane tasks for views with weight > 0
+//   P4  lane = pixel: fit acceptance, the 5 refinement candidates (RNG continues from P2)
+//   P5  (candidate, view) tasks for views with weight > 0
+//   P6  lane = pixel: acceptance, writes
+// ---------------------------------------------------------------------------------------------
+struct WvLds {
+    float rref[108 * VM_P];      // [tap][p]: window 0 taps 0..35 (6x6, step 2), anchor k taps 36+9(k-1).. (3x3, step 5)
+    float wsr[9 * VM_P], wsrr[9 * VM_P], wsum[9 * VM_P];  // per window moments over its valid taps
+    uint64_t tmask0[VM_P];       // SA tap masks (all ones without SA)
+    uint32_t tmask[8 * VM_P];
+    int anc[9 * VM_P];           // packed (x, y) of anchors 0..8, -1 = none
+    uint32_t awin[VM_P];         // bit k: window k is evaluated (anchor present and SA label matches)
+    float4 hyp[9 * VM_P];        // [h][p]: anchor planes 1..8 (if STRONG) + current
+    int npos[8 * VM_P];          // anchor pixel index (or -1)
+    uint32_t hflag[VM_P];        // bit h: hypothesis h present (anchor STRONG)
+    float4 fit[VM_P];
+    float4 cand[5 * VM_P];
+    float4 pnow[VM_P];
+    float st[5 * VM_P];          // depth_now, cost_now, cost_init, weight norm, refine (fit normal != 0)
+    uint32_t rng_n[VM_P];
+};
+static inline size_t wv_lds_bytes(int N) {
+    return sizeof(WvLds) + (size_t)9 * N * VM_P * sizeof(float) + (size_t)N * VM_P * sizeof(int);
+}
+__device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
+    const long idx = (long)y * a.W + x;
+    if (idx < 0 || idx >= a.HW) return -1;
+    return a.sa[idx];
+}
+// One NCC-New window of pixel slot p against source view s: taps (ax - 5 + inc*i, ay - 5 + inc*j),
+// i outer, j inner, skipping taps outside the SA mask; the reference's moments come from WvLds.
+// `fast` = window_rcp_ok for this lane (Newton reciprocal + packed taps); otherwise the IEEE
+// statement. Every lane of the wave executes the same instruction stream; lanes that do not need
+// this window (`live` false) run on a parked homography and discard the sums.
+template <bool F16, int NW, int INC>
+__device__ __forceinline__ void ncc_new_window(const Args &a, const WvLds &L, int p, int tap0, uint64_t mask,
+                                               const Hom &Hm, int ax, int ay, bool live, bool fast,
+                                               const FastTex<F16, true> &T, const SrcTex<F16> &Q, float &ss,
+                                               float &sss, float &srs) {
+    const uint64_t fm = __ballot(live && fast), sm = __ballot(live && !fast);
+    if (fm) {
+        Hom Hp = Hm;
+        if (!(live && fast)) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) Hp.h[k] = (k == 8) ? 1.0f : 0.0f;
+        }
+        float vs[NW * NW];
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const float x = (float)(ax - 5 + INC * i);
+            const apd_f2 cxy = {fmaf(Hp.h[0], x, Hp.h[2]), fmaf(Hp.h[3], x, Hp.h[5])};
+            const float cz = fmaf(Hp.h[6], x, Hp.h[8]);
+            typename FastTex<F16, true>::Tap t[NW];
+            typename FastTex<F16, true>::Raw q[NW];
+#pragma unroll
+            for (int j = 0; j < NW; ++j) {
+                const float y = (float)(ay - 5 + INC * j);
+                const apd_f2 XY = pk_fma((apd_f2){Hp.h[1], Hp.h[4]}, (apd_f2){y, y}, cxy);
+                const float Z = fmaf(Hp.h[7], y, cz);
+                t[j] = T.tap(XY, rcp_newton(Z));
+            }
+#pragma unroll
+            for (int j = 0; j < NW; ++j) q[j] = T.load(t[j]);
+#pragma unroll
+            for (int j = 0; j < NW; ++j) vs[i * NW + j] = T.finish(t[j], q[j]);
+        }
+        if (live && fast) {
+#pragma unroll
+            for (int tk = 0; tk < NW * NW; ++tk) {
+                if (!((mask >> tk) & 1ull)) continue;
+                const float v = vs[tk];
+                const float r = L.rref[(tap0 + tk) * VM_P + p];
+                ss += v;
+                sss = fmaf(v, v, sss);
+                srs = fmaf(r, v, srs);
+            }
+        }
+    }
+    if (sm && live && !fast) {
+        const float Wm1 = (float)(a.W - 1), Hm1 = (float)(a.H - 1);
+        const uint32_t W1 = SrcTex<F16>::pitch(a.W);
+        for (int i = 0; i < NW; ++i) {
+            const float x = (float)(ax - 5 + INC * i);
+            const float cx = fmaf(Hm.h[0], x, Hm.h[2]);
+            const float cy = fmaf(Hm.h[3], x, Hm.h[5]);
+            const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
+            for (int j = 0; j < NW; ++j) {
+                const int tk = i * NW + j;
+                if (!((mask >> tk) & 1ull)) continue;
+                const float y = (float)(ay - 5 + INC * j);
+                const float X = fmaf(Hm.h[1], y, cx);
+                const float Y = fmaf(Hm.h[4], y, cy);
+                const float Z = fmaf(Hm.h[7], y, cz);
+                const float iz = 1.0f / Z;
+                const QuadTap t = quad_tap(Wm1, Hm1, W1, X * iz, Y * iz);
+                const float v = bilerp(Q.fetch(t.idx), t.ax, t.ay);
+                const float r = L.rref[(tap0 + tk) * VM_P + p];
+                ss += v;
+                sss = fmaf(v, v, sss);
+                srs = fmaf(r, v, srs);
+            }
+        }
+    }
+}
+
+// ComputeBilateralNCCNew + Softmax focal weighting (APD.cu:448-593, 431-446) for pixel slot p, source
+// view s, plane pl, with the reference side from WvLds. Called by every lane of the wave (converged);
+// `want` = the lane evaluates this task. Same operations, in the same order, as ncc_new.
+template <bool F16>
+__device__ __forceinline__ float ncc_new_vm(const Args &a, const WvLds &L, int p, int px, int py, int s, float4 pl,
+                                            bool want) {
+    const int W = a.W, H = a.H;
+    const Hom Hm = homography(a, s, pl);
+    float ptx, pty;
+    project(Hm, (float)px, (float)py, ptx, pty);
+    bool alive = want && !(ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f);
+    const FastTex<F16, true> T(a, s);
+    const SrcTex<F16> Q(a, s);
+    const uint32_t awin = L.awin[p];
+    float sc[9];
+    int ns = 0;
+    float center_cost = 0.0f, strong_weight = 0.0f;
+    bool dead = !alive;  // COST_MAX (centre or centre-anchor projected out of the image)
+#pragma unroll 1
+    for (int k = 0; k < 9; ++k) {
+        const int pk = L.anc[k * VM_P + p];
+        const bool has = alive && pk >= 0 && ((awin >> k) & 1u);
+        const int ax = has ? (pk & 0xFFFF) : px, ay = has ? (pk >> 16) : py;
+        bool live = has;
+        if (has) {
+            float asx, asy;
+            project(Hm, (float)ax, (float)ay, asx, asy);
+            if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) {
+                live = false;
+                if (k != 0) {
+                    if ((a.sel[ax + ay * W] >> (s - 1)) & 1u) {
+#pragma unroll
+                        for (int t = 0; t < 9; ++t) if (t == ns) sc[t] = APD_COST_MAX;
+                        ns++;
+                        strong_weight += 1.0f;
+                    }
+                } else {
+                    dead = true;
+                    alive = false;
+                }
+            }
+        }
+        if (!__ballot(live)) continue;
+        const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
+        float ss = 0.0f, sss = 0.0f, srs = 0.0f;
+        if (k == 0)
+            ncc_new_window<F16, 6, 2>(a, L, p, 0, L.tmask0[p], Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+        else
+            ncc_new_window<F16, 3, 5>(a, L, p, 36 + 9 * (k - 1), (uint64_t)L.tmask[(k - 1) * VM_P + p], Hm, ax, ay,
+                                      live, fast, T, Q, ss, sss, srs);
+        if (!live) continue;
+        const float wsum = L.wsum[k * VM_P + p];
+        if (wsum == 0.0f) continue;
+        const float c = ncc_finalize(L.wsr[k * VM_P + p], L.wsrr[k * VM_P + p], ss, sss, srs, wsum);
+        if (k == 0) {
+            center_cost = c;
+        } else {
+#pragma unroll
+            for (int t = 0; t < 9; ++t) if (t == ns) sc[t] = c;
+            ns++;
+            strong_weight += 1.0f;
+        }
+    }
+    if (dead) return APD_COST_MAX;
+    if (strong_weight <= 1e-6f) return center_cost;
+    float mx = -1e10f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) if (t < ns && sc[t] > mx) mx = sc[t];
+    float e[9];
+    float sum = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        if (t < ns) { e[t] = d_expf(sc[t] - mx); sum += e[t]; }
+    }
+    float acc = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        if (t < ns) { float w = e[t] / sum; acc = fmaf(w, sc[t], acc); }
+    }
+    acc = (acc > APD_COST_MAX) ? APD_COST_MAX : acc;
+    return (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
+}
+
+template <bool F16>
+__global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
+                                                                int iter) {
+    const int N = a.N, W = a.W;
+    WvLds &L = *reinterpret_cast<WvLds *>(apd_dyn_lds);
+    float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64], later [5][N][64]
+    int *wts = reinterpret_cast<int *>(costL + 9 * N * VM_P);            // [N][64]
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int first = blk * VM_P;
+    const int np = min(VM_P, count - first);
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
+    const APD_G Cam &cam0 = a.cams[0];
+    const bool geom = a.geom != 0;
+    const float gf = a.gf;
+    const int p1 = lane;
+    const bool pv1 = p1 < np;
+    const int c1 = list[first + min(p1, np - 1)];
+    const int py1 = c1 / W, px1 = c1 - py1 * W;
+
+    // ---- P0: anchors, planes, NCC-New reference data
+    if (pv1) {
+        const APD_G short2 *anc = a.anchors + (size_t)a.amap[c1] * 9;
+        const int cid = a.sa_any ? a.sa[c1] : 0;
+        const bool use_sa = cid != 0;
+        if (wave == 0) {
+            uint32_t hflag = 0, awin = 0;
+            for (int k = 0; k < 9; ++k) {
+                const short2 ap = anc[k];
+                const bool ok = !(ap.x == -1 || ap.y == -1);
+                L.anc[k * VM_P + p1] = ok ? ((int)(uint16_t)ap.x | ((int)ap.y << 16)) : -1;
+                if (ok && !(use_sa && sa_at_dev(a, ap.x, ap.y) != cid)) awin |= 1u << k;
+                if (k >= 1) {
+                    const int q = ok ? ap.x + ap.y * W : -1;
+                    L.npos[(k - 1) * VM_P + p1] = q;
+                    if (ok && a.weak[q] == APD_STRONG) {
+                        hflag |= 1u << (k - 1);
+                        L.hyp[(k - 1) * VM_P + p1] = a.plane[q];
+                    }
+                }
+            }
+            L.hflag[p1] = hflag;
+            L.awin[p1] = awin;
+            L.hyp[8 * VM_P + p1] = a.plane[c1];
+            L.fit[p1] = a.fit[c1];
+        }
+        // reference windows: wave w builds windows w, w + VM_WAVES, ... (tap order = the reference's)
+        for (int k = wave; k < 9; k += VM_WAVES) {
+            const short2 ap = anc[k];
+            if (ap.x == -1 || ap.y == -1) continue;
+            const int ax = ap.x, ay = ap.y;
+            const int n1 = (k == 0) ? 6 : 3, inc = (k == 0) ? 2 : 5;
+            const int tap0 = (k == 0) ? 0 : 36 + 9 * (k - 1);
+            float sr = 0.0f, srr = 0.0f, ws = 0.0f;
+            uint64_t mask = 0;
+            for (int i = 0; i < n1; ++i)
+                for (int j = 0; j < n1; ++j) {
+                    const int rx = ax - 5 + inc * i, ry = ay - 5 + inc * j;
+                    const int tk = i * n1 + j;
+                    if (use_sa && sa_at_dev(a, rx, ry) != cid) {
+                        L.rref[(tap0 + tk) * VM_P + p1] = 0.0f;
+                        continue;
+                    }
+                    const float r = tex_ref(a, rx, ry);
+                    L.rref[(tap0 + tk) * VM_P + p1] = r;
+                    mask |= 1ull << tk;
+                    sr += r;
+                    srr = fmaf(r, r, srr);
+                    ws += 1.0f;
+                }
+            L.wsr[k * VM_P + p1] = sr;
+            L.wsrr[k * VM_P + p1] = srr;
+            L.wsum[k * VM_P + p1] = ws;
+            if (k == 0) L.tmask0[p1] = mask;
+            else L.tmask[(k - 1) * VM_P + p1] = (uint32_t)mask;
+        }
+    }
+    __syncthreads();
+
+    // ---- P1: (hypothesis, view) tasks
+    for (int t = wave; t < 9 * N; t += VM_WAVES) {
+        const int h = t / N, v = t - h * N;
+        float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
+        const bool want = pv1 && (h == 8 || ((L.hflag[p1] >> h) & 1u));
+        const float4 pl = L.hyp[h * VM_P + p1];
+        const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want);
+        if (want) {
+            val = nv;
+            if (h == 8 && geom) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
+        }
+        costL[t * VM_P + p1] = val;
+    }
+    __syncthreads();
+
+    // ---- P2: lane = (pixel, view) groups
+    const int Gp = WAVE / N;
+    const int ppr = VM_WAVES * Gp;
+    for (int r0 = 0; r0 < np; r0 += ppr) {
+        int g = lane / N;
+        const bool lane_ok = g < Gp;
+        int v = lane - g * N;
+        if (!lane_ok) { g = 0; v = (lane - Gp * N) % N; }
+        Group G;
+        G.v = v; G.base = g * N; G.slot = g; G.li = 0;
+        G.gmask = (N >= 64) ? ~0ull : ((1ull << N) - 1ull);
+        const int pr = r0 + wave * Gp + g;
+        G.valid = lane_ok && pr < np;
+        const int p = min(pr, np - 1);
+        const int c = list[first + p];
+        const int py = c / W, px = c - py * W;
+        const uint32_t hflag = L.hflag[p];
+        float prior = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int q = L.npos[i * VM_P + p];
+            if (q >= 0) prior += ((a.sel[q] >> v) & 1u) ? 0.9f : 0.1f;
+        }
+        float ca[8];
+#pragma unroll
+        for (int h = 0; h < 8; ++h) ca[h] = costL[(h * N + v) * VM_P + p];
+        const float cv_now = costL[(8 * N + v) * VM_P + p];
+        Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c, ord_weak(iter));
+        const int w = view_selection(ca, prior, iter, rg, G, N);
+        const uint32_t tsel = group_bits(w > 0, G);
+        float gval[8];
+#pragma unroll 1
+        for (int j = 0; j < 8; ++j) {
+            float cj = ca[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) if (j == k) cj = ca[k];
+            float vv = cj;
+            if (geom && w > 0)
+                vv = ((hflag >> j) & 1u) ? fmaf(gf, geom_cost(a, px, py, v + 1, L.hyp[j * VM_P + p]), cj) : fmaf(gf, 3.0f, cj);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) if (j == k) gval[k] = vv;
+        }
+        float fc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        float wn = 0.0f, cost_now = 0.0f;
+        for (int k = 0; k < N; ++k) {
+            const int wk = __shfl(w, G.base + k);
+            const float fwk = (float)wk;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float vk = __shfl(gval[j], G.base + k);
+                if (wk > 0) fc[j] = fmaf(fwk, vk, fc[j]);
+            }
+            if (wk > 0) wn += fwk;
+            cost_now = fmaf(fwk, __shfl(cv_now, G.base + k), cost_now);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fc[j] /= wn;
+        cost_now /= wn;
+        const float cost_init = cost_now;
+        int mi = 0;
+        {
+            float m = fc[0];
+#pragma unroll
+            for (int j = 1; j < 8; ++j) if (fc[j] <= m) { m = fc[j]; mi = j; }
+        }
+        const float4 cur = L.hyp[8 * VM_P + p];
+        float depth_now = depth_from_plane(cam0, cur, px, py);
+        float4 pnow = cur;
+        {
+            float fcm = fc[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) if (mi == k) fcm = fc[k];
+            if ((hflag >> mi) & 1u) {
+                const float4 cand = L.hyp[mi * VM_P + p];
+                const float db = depth_from_plane(cam0, cand, px, py);
+                if (db >= a.dmin && db <= a.dmax && fcm < cost_now) {
+                    depth_now = db; pnow = cand; cost_now = fcm;
+                    if (G.valid && G.v == 0) a.sel[c] = tsel;
+                }
+            }
+        }
+        if (G.valid) {
+            wts[v * VM_P + p] = w;
+            if (G.v == 0) {
+                const float4 fit = L.fit[p];
+                L.pnow[p] = pnow;
+                L.st[0 * VM_P + p] = depth_now;
+                L.st[1 * VM_P + p] = cost_now;
+                L.st[2 * VM_P + p] = cost_init;
+                L.st[3 * VM_P + p] = wn;
+                L.st[4 * VM_P + p] = (fit.x == 0 && fit.y == 0 && fit.z == 0) ? 0.0f : 1.0f;
+                L.rng_n[p] = rg.n;
+            }
+        }
+    }
+    __syncthreads();
+    const bool refine = pv1 && L.st[4 * VM_P + p1] != 0.0f;
+
+    // ---- P3: fit-plane tasks (views with weight > 0)
+    for (int v = wave; v < N; v += VM_WAVES) {
+        float cv = 0.0f;
+        const bool want = refine && wts[v * VM_P + p1] > 0;
+        const float4 fit = L.fit[p1];
+        const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, fit, want);
+        if (want) {
+            cv = nv;
+            if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, fit), cv);
+        }
+        costL[v * VM_P + p1] = cv;
+    }
+    __syncthreads();
+
+    // ---- P4: fit acceptance, refinement candidates (PlaneHypothesisRefinementWeak, APD.cu:1008-1067)
+    if (wave == 0 && refine) {
+        const float wn = L.st[3 * VM_P + p1];
+        float depth_now = L.st[0 * VM_P + p1], cost_now = L.st[1 * VM_P + p1];
+        float4 pnow = L.pnow[p1];
+        const float4 fit = L.fit[p1];
+        float tc = 0.0f;
+        for (int kk = 0; kk < N; ++kk) {
+            const int wk = wts[kk * VM_P + p1];
+            if (wk > 0) tc = fmaf((float)wk, costL[kk * VM_P + p1], tc);
+        }
+        tc /= wn;
+        const float db = depth_from_plane(cam0, fit, px1, py1);
+        if (db >= a.dmin && db <= a.dmax && tc < cost_now) { depth_now = db; pnow = fit; cost_now = tc; }
+        Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c1, ord_weak(iter));
+        rg.n = L.rng_n[p1];
+        if (rg.n & 3u) rg.refill();
+        const Cands C = refine_candidates(a, px1, py1, rg, pnow, depth_now);
+        for (int k = 0; k < 5; ++k) {
+            float dk;
+            float4 t = candidate(C, k, pnow, depth_now, dk);
+            t.w = dist2origin(cam0, px1, py1, dk, t);
+            L.cand[k * VM_P + p1] = t;
+        }
+        L.pnow[p1] = pnow;
+        L.st[0 * VM_P + p1] = depth_now;
+        L.st[1 * VM_P + p1] = cost_now;
+    }
+    __syncthreads();
+
+    // ---- P5: candidate tasks (views with weight > 0)
+    for (int t = wave; t < 5 * N; t += VM_WAVES) {
+        const int k = t / N, v = t - k * N;
+        float cv = 0.0f;
+        const bool want = refine && wts[v * VM_P + p1] > 0;
+        const float4 tp = L.cand[k * VM_P + p1];
+        const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, tp, want);
+        if (want) {
+            cv = nv;
+            if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
+        }
+        costL[t * VM_P + p1] = cv;
+    }
+    __syncthreads();
+
+    // ---- P6: acceptance, writes
+    if (pv1) {
+        for (int v = wave; v < N; v += VM_WAVES) a.vw[(size_t)v * a.HW + c1] = (uint8_t)wts[v * VM_P + p1];
+        if (wave == 0) {
+            float cost_now = L.st[1 * VM_P + p1];
+            const float cost_init = L.st[2 * VM_P + p1], wn = L.st[3 * VM_P + p1];
+            float4 pnow = L.pnow[p1];
+            if (refine) {
+                for (int k = 0; k < 5; ++k) {
+                    const float4 t = L.cand[k * VM_P + p1];
+                    float tc = 0.0f;
+                    for (int kk = 0; kk < N; ++kk) {
+                        const int wk = wts[kk * VM_P + p1];
+                        if (wk > 0) tc = fmaf((float)wk, costL[(k * N + kk) * VM_P + p1], tc);
+                    }
+                    tc /= wn;
+                    const float db = depth_from_plane(cam0, t, px1, py1);
+                    if (db >= a.dmin && db <= a.dmax && tc < cost_now) { pnow = t; cost_now = tc; }
+                }
+            }
+            if (a.state == APD_REFINE_INIT) {
+                if ((double)cost_now < (double)cost_init - 0.1) { a.cost[c1] = cost_now; a.plane[c1] = pnow; }
+                else a.cost[c1] = cost_init;
+            } else {
+                a.cost[c1] = cost_now;
+                a.plane[c1] = pnow;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // CheckerboardPropagationWeak + PlaneHypothesisRefinementWeak (APD.cu:1442-1615, 1008-1096)
 // ---------------------------------------------------------------------------------------------
 template <bool F16>
@@ -2185,6 +2663,10 @@ apd_ctx *apd_create(int32_t device) {
                               160 * 1024);
     (void)hipFuncSetAttribute((const void *)k_random_init_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_sweep_weak_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_sweep_weak_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     return ctx;
 }
 
@@ -2508,8 +2990,12 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
         for (int colour = 0; colour < 2; ++colour) {
             const int n = ctx->cnt[2 + colour];
             if (n <= 0) continue;
-            LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
-                               (const int *)list_ptr(ctx, 2 + colour), n, iter);
+            if (ctx->sweep_vm)
+                LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), wv_lds_bytes(a.N), s,
+                           a, (const int *)list_ptr(ctx, 2 + colour), n, iter);
+            else
+                LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
+                           (const int *)list_ptr(ctx, 2 + colour), n, iter);
         }
         if ((st = check_launch(ctx, "weak sweep"))) return st;
     }
