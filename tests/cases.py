@@ -89,6 +89,8 @@ CASES = {
     "refine_iter_geom": (128, 96, 4, "geom"),
     "refine_init_apd": (128, 96, 4, "apd"),
     "refine_iter_apd_geom_sa": (128, 96, 4, "apd_geom_sa"),
+    "first_n12": (96, 72, 12, "first"),           # view-major P2 in several rounds, 3 tasks per wave
+    "refine_iter_n16_apd_geom": (80, 60, 16, "apd_geom"),
 }
 
 
@@ -104,6 +106,8 @@ def make_case(name, oracle_run):
         return refine_problem(sc, priors, 0, n, state=A.REFINE_INIT, geom=False, apd=True)
     if kind == "apd_geom_sa":
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, sa=True)
+    if kind == "apd_geom":
+        return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True)
     raise KeyError(kind)
 
 
