@@ -942,8 +942,11 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     // tasks whose window needs the out-of-line path are collected in `defer` (bit k = k-th task of
     // this wave) and evaluated after the loop, so the hot loop holds no call.
     uint64_t defer[2] = {0, 0};  // up to 128 tasks per wave (9 * 31 / VM_WAVES)
-    for (int t = wave, k = 0; t < 9 * N; t += VM_WAVES, ++k) {
-        const int h = t / N, v = t - h * N;
+    // tasks in view-major order, one contiguous chunk per wave: consecutive NCCs of a wave read the
+    // same source image around the same pixels (L1 reuse); (h, v) -> table index t = h * N + v
+    const int c1n = (9 * N + VM_WAVES - 1) / VM_WAVES, u0 = wave * c1n, u1 = min(u0 + c1n, 9 * N);
+    for (int u = u0, k = 0; u < u1; ++u, ++k) {
+        const int v = u / 9, h = u - 9 * v, t = h * N + v;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;  // float cost_array[8][32] = {2.0f} (APD.cu:1120)
         const bool fh = h == 8 || L.npos[h * VM_P + p1] >= 0;
         if (pv1 && fh) {
@@ -959,7 +962,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     while (defer[w2]) {
         const int k = __builtin_ctzll(defer[w2]) + 64 * w2;
         defer[w2] &= defer[w2] - 1;
-        const int t = wave + k * VM_WAVES, h = t / N, v = t - h * N;
+        const int u = u0 + k, v = u / 9, h = u - 9 * v, t = h * N + v;
         const float4 pl = L.hyp[h * VM_P + p1];
         float val = ncc_old_slow<F16>(a.self, px1, py1, v + 1, pl, rw.r, VM_P, rw.mean, rw.var);
         if (h == 8 && geom_imp) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
@@ -1061,8 +1064,9 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 
     // ---- P3: lane = pixel, wave = (candidate, view) tasks
     defer[0] = defer[1] = 0;
-    for (int t = wave, kt = 0; t < 5 * N; t += VM_WAVES, ++kt) {
-        const int k = t / N, v = t - k * N;
+    const int c3n = (5 * N + VM_WAVES - 1) / VM_WAVES, w0 = wave * c3n, w1 = min(w0 + c3n, 5 * N);
+    for (int u = w0, kt = 0; u < w1; ++u, ++kt) {
+        const int v = u / 5, k = u - 5 * v, t = k * N + v;
         float cv = 0.0f;
         // a view with sampled weight 0 contributes fmaf(0, cv, tc) == tc for every finite cv (costs are
         // clamped to [0, 2]), so its refinement NCCs are skipped without changing any result
@@ -1079,7 +1083,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     while (defer[w2]) {
         const int kt = __builtin_ctzll(defer[w2]) + 64 * w2;
         defer[w2] &= defer[w2] - 1;
-        const int t = wave + kt * VM_WAVES, k = t / N, v = t - k * N;
+        const int u = w0 + kt, v = u / 5, k = u - 5 * v, t = k * N + v;
         const float4 tp = L.cand[k * VM_P + p1];
         float cv = ncc_old_slow<F16>(a.self, px1, py1, v + 1, tp, rw.r, VM_P, rw.mean, rw.var);
         if (geom_imp) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
