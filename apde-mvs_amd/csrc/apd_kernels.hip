@@ -1904,8 +1904,10 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
         const int dc = min(chunk, 61 - d0);
         // ---- P1: (depth, view) tasks, lane = pixel
         uint64_t defer = 0;
-        for (int t = wave, k = 0; t < dc * N; t += VM_WAVES, ++k) {
-            const int dd = t / N, v = t - dd * N;
+        // view-major contiguous chunk per wave (consecutive tasks on the same source image)
+        const int cn = (dc * N + VM_WAVES - 1) / VM_WAVES, u0 = wave * cn, u1 = min(u0 + cn, dc * N);
+        for (int u = u0, k = 0; u < u1; ++u, ++k) {
+            const int v = u / dc, dd = u - dc * v, t = dd * N + v;
             const int d = d0 + dd;
             const float pdepth = cam0.K[0] * base / (disp + (float)(d - 30));
             const bool in_range = !(pdepth < a.dmin || pdepth > a.dmax);
@@ -1923,7 +1925,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
         while (defer) {
             const int k = __builtin_ctzll(defer);
             defer &= defer - 1;
-            const int t = wave + k * VM_WAVES, dd = t / N, v = t - dd * N;
+            const int u = u0 + k, v = u / dc, dd = u - dc * v, t = dd * N + v;
             const float pdepth = cam0.K[0] * base / (disp + (float)(d0 + dd - 30));
             float4 tp = pl;
             tp.w = dist2origin(cam0, px, py, pdepth, tp);
@@ -2206,8 +2208,9 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, i
     for (int d0 = 0; d0 < 11; d0 += chunk) {
         const int dc = min(chunk, 11 - d0);
         uint64_t defer = 0;
-        for (int t = wave, k = 0; t < dc * N; t += VM_WAVES, ++k) {
-            const int dd = t / N, v = t - dd * N;
+        const int cn = (dc * N + VM_WAVES - 1) / VM_WAVES, u0 = wave * cn, u1 = min(u0 + cn, dc * N);
+        for (int u = u0, k = 0; u < u1; ++u, ++k) {
+            const int v = u / dc, dd = u - dc * v, t = dd * N + v;
             const int d = d0 + dd - 5;
             const float pdepth = cam0.K[0] * base / (disp + (float)d);
             const bool in_range = !(pdepth < a.dmin || pdepth > a.dmax);
@@ -2226,7 +2229,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, i
         while (defer) {
             const int k = __builtin_ctzll(defer);
             defer &= defer - 1;
-            const int t = wave + k * VM_WAVES, dd = t / N, v = t - dd * N;
+            const int u = u0 + k, v = u / dc, dd = u - dc * v, t = dd * N + v;
             const float pdepth = cam0.K[0] * base / (disp + (float)(d0 + dd - 5));
             float4 tp = pl;
             tp.w = dist2origin(cam0, px, py, pdepth, tp);
