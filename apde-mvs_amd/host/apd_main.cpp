@@ -12,7 +12,8 @@
 //                        previous pass's maps; required for > 1 GPU, results independent of the
 //                        device count and of the processing order)
 //   --seed N             base of the deterministic per-problem RNG seed
-// Fusion (RunFusion*, APD.cpp:962-1608) is outside this engine's scope.
+// Fusion (RunFusion / RunFusion_TAT_I / RunFusion_TAT_A + WeakVisFilter, APD.cpp:962-1608) runs in
+// fusion.cpp: per-(pixel, source) tests on the GPU, the ordered commit on the host.
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -27,6 +28,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include "fusion.h"
 
 #include "../../include/apd_hip.h"
 #include "image.h"
@@ -490,9 +493,28 @@ int main(int argc, char **argv) {
         return EXIT_FAILURE;
     }
     std::cout << "There are " << problems.size() << " problems needed to be processed!" << std::endl;
+    auto fuse = [&]() -> bool {
+        FusionOptions fo;
+        fo.dense_folder = dense;
+        fo.dataset = dataset;
+        fo.weak_filter = weak_filter;
+        fo.export_color = export_color;
+        fo.device = gpus[0];
+        FusionReport rep;
+        std::string ferr;
+        if (!run_fusion(problems, fo, store, rep, ferr)) {
+            std::cout << "Error: " << ferr << std::endl;
+            return false;
+        }
+        printf("Fusion: %lld points, load %.0f ms, upload %.0f ms, weak filter %.0f ms, fuse %.0f ms (device %.0f ms), "
+               "write %.0f ms\n",
+               (long long)rep.points, rep.load_ms, rep.upload_ms, rep.filter_ms, rep.fuse_ms, rep.gpu_ms, rep.write_ms);
+        return true;
+    };
     if (only_fuse) {
-        std::cout << "Fusion is outside this engine (DESIGN.md section 8): nothing to do for --only_fuse" << std::endl;
-        return EXIT_FAILURE;
+        if (!fuse()) return EXIT_FAILURE;
+        printf("Fusion done!\n");
+        return EXIT_SUCCESS;
     }
     int max_size = std::max(W0, H0), round_num = 1;
     while (max_size > 800) {
@@ -626,8 +648,7 @@ int main(int argc, char **argv) {
         return EXIT_SUCCESS;
     }
     std::cout << "Run fusion\n";
-    std::cout << "Fusion is outside this engine (DESIGN.md section 8); depth maps are in " << dense << "/APD"
-              << std::endl;
+    if (!fuse()) return EXIT_FAILURE;
     std::cout << "All done\n";
     return EXIT_SUCCESS;
 }

@@ -27,3 +27,26 @@ void apdhost_resize_nearest(const void *src, int sw, int sh, void *dst, int dw, 
 }
 int apdhost_read_camera(const char *path, apd_camera *cam) { return read_camera(path, *cam) ? 0 : -1; }
 }
+
+#include "fusion.h"
+extern "C" {
+// cv::imread(IMREAD_COLOR): BGR bytes; same return convention as apdhost_read_gray8
+long apdhost_read_bgr8(const char *path, unsigned char *out, long out_cap, int *w, int *h) {
+    Bgr8 g;
+    std::string err;
+    if (!read_bgr8(path, g, err)) return -1;
+    *w = g.width;
+    *h = g.height;
+    const long n = (long)g.px.size();
+    if (out && out_cap >= n) memcpy(out, g.px.data(), n);
+    return n;
+}
+void apdhost_resize_linear_u8c3(const unsigned char *src, int sw, int sh, unsigned char *dst, int dw, int dh) {
+    resize_linear_u8c3(src, sw, sh, dst, dw, dh);
+}
+int apdhost_write_png_gray8(const char *path, const unsigned char *px, int w, int h) {
+    return write_png_gray8(path, px, w, h) ? 0 : -1;
+}
+float apdhost_angle_cut_lt(float t) { return angle_cut_lt(t); }
+float apdhost_view_cut_deg(float d) { return view_cut_deg(d); }
+}

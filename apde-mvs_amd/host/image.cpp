@@ -43,7 +43,14 @@ static uint8_t rgb_to_gray(int r, int g, int b) {
 // ----------------------------------------------------------------------------------------------
 static uint32_t be32(const uint8_t *p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
 
-bool decode_png_gray(const std::vector<uint8_t> &file, Gray8 &out, std::string &err) {
+namespace {
+struct PngRaw {
+    int w = 0, h = 0, ctype = 0, ch = 0;
+    std::vector<uint8_t> img, plte;  // unfiltered 8-bit samples, w*ch per row
+};
+}  // namespace
+
+static bool png_raw(const std::vector<uint8_t> &file, PngRaw &png, std::string &err) {
     static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
     if (file.size() < 8 || memcmp(file.data(), sig, 8) != 0) { err = "not a PNG file"; return false; }
     size_t pos = 8;
@@ -116,6 +123,20 @@ bool decode_png_gray(const std::vector<uint8_t> &file, Gray8 &out, std::string &
             cur[i] = (uint8_t)v;
         }
     }
+    png.w = w;
+    png.h = h;
+    png.ctype = ctype;
+    png.ch = ch;
+    png.img.swap(img);
+    png.plte.swap(plte);
+    return true;
+}
+
+bool decode_png_gray(const std::vector<uint8_t> &file, Gray8 &out, std::string &err) {
+    PngRaw png;
+    if (!png_raw(file, png, err)) return false;
+    const int w = png.w, h = png.h, ctype = png.ctype, ch = png.ch;
+    const std::vector<uint8_t> &img = png.img, &plte = png.plte;
     out.width = w;
     out.height = h;
     out.px.resize((size_t)w * h);
@@ -186,7 +207,7 @@ struct Huff {
 struct Comp {
     int id, h, v, tq, td = 0, ta = 0, pred = 0;
     int bw, bh;                  // blocks per line / column in the component (padded to MCUs)
-    std::vector<int16_t> coef;   // bw*bh*64, natural order (only kept for component 0)
+    std::vector<int16_t> coef;   // bw*bh*64, natural order (component 0, or all when decoding colour)
 };
 
 struct BitReader {
@@ -324,7 +345,19 @@ void idct_islow(const int16_t *coef, const uint16_t *q, uint8_t *out, int ostrid
 }
 }  // namespace
 
-bool decode_jpeg_gray(const std::vector<uint8_t> &f, Gray8 &out, std::string &err) {
+// Entropy decode + islow IDCT of every needed component into padded sample planes.
+struct JpegPlanes {
+    int W = 0, H = 0, hmax = 1, vmax = 1;
+    bool jfif = false;
+    int adobe_transform = -1;  // APP14 "Adobe" transform flag, -1 if absent
+    struct Plane {
+        int id, h, v, pw, ph;  // sampling factors, padded plane size (blocks * 8)
+        std::vector<uint8_t> px;
+    };
+    std::vector<Plane> planes;
+};
+
+static bool jpeg_decode(const std::vector<uint8_t> &f, bool all_comps, JpegPlanes &res, std::string &err) {
     if (f.size() < 4 || f[0] != 0xFF || f[1] != 0xD8) { err = "not a JPEG file"; return false; }
     uint16_t qt[4][64];
     bool qt_ok[4] = {false, false, false, false};
@@ -344,7 +377,11 @@ bool decode_jpeg_gray(const std::vector<uint8_t> &f, Gray8 &out, std::string &er
         if (pos + len > f.size()) { err = "truncated JPEG segment"; return false; }
         const uint8_t *d = &f[pos + 2];
         const size_t dl = len - 2;
-        if (m == 0xDB) {  // DQT
+        if (m == 0xE0 && dl >= 5 && memcmp(d, "JFIF", 5) == 0) {
+            res.jfif = true;
+        } else if (m == 0xEE && dl >= 12 && memcmp(d, "Adobe", 5) == 0) {
+            res.adobe_transform = d[11];
+        } else if (m == 0xDB) {  // DQT
             size_t i = 0;
             while (i < dl) {
                 const int pq = d[i] >> 4, tq = d[i] & 15;
@@ -406,7 +443,8 @@ bool decode_jpeg_gray(const std::vector<uint8_t> &f, Gray8 &out, std::string &er
                 c.bh = mcuy * c.v;
             }
             if (comps[0].h != hmax || comps[0].v != vmax) { err = "subsampled luma is not supported"; return false; }
-            comps[0].coef.assign((size_t)comps[0].bw * comps[0].bh * 64, 0);
+            for (size_t c = 0; c < comps.size(); ++c)
+                if (c == 0 || all_comps) comps[c].coef.assign((size_t)comps[c].bw * comps[c].bh * 64, 0);
             sof = true;
         } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
             err = "progressive / arithmetic / lossless JPEG is not supported";
@@ -450,7 +488,7 @@ bool decode_jpeg_gray(const std::vector<uint8_t> &f, Gray8 &out, std::string &er
                     blk[kZigzag[k]] = (int16_t)extend(br.get(s), s);
                     ++k;
                 }
-                if (&c == &comps[0] && bx < c.bw && by < c.bh)
+                if (!c.coef.empty() && bx < c.bw && by < c.bh)
                     memcpy(&c.coef[((size_t)by * c.bw + bx) * 64], blk, sizeof(blk));
                 return true;
             };
@@ -495,17 +533,33 @@ bool decode_jpeg_gray(const std::vector<uint8_t> &f, Gray8 &out, std::string &er
         pos += len;
     }
     if (!sof) { err = "JPEG without SOF"; return false; }
-    Comp &y = comps[0];
-    if (!qt_ok[y.tq]) { err = "missing quantisation table"; return false; }
-    std::vector<uint8_t> plane((size_t)y.bw * 8 * y.bh * 8);
-    const int pw = y.bw * 8;
-    for (int by = 0; by < y.bh; ++by)
-        for (int bx = 0; bx < y.bw; ++bx)
-            idct_islow(&y.coef[((size_t)by * y.bw + bx) * 64], qt[y.tq], &plane[(size_t)by * 8 * pw + bx * 8], pw);
-    out.width = W;
-    out.height = H;
-    out.px.resize((size_t)W * H);
-    for (int r = 0; r < H; ++r) memcpy(&out.px[(size_t)r * W], &plane[(size_t)r * pw], W);
+    res.W = W;
+    res.H = H;
+    res.hmax = hmax;
+    res.vmax = vmax;
+    for (size_t c = 0; c < comps.size(); ++c) {
+        Comp &y = comps[c];
+        if (y.coef.empty()) continue;
+        if (!qt_ok[y.tq]) { err = "missing quantisation table"; return false; }
+        JpegPlanes::Plane pl{y.id, y.h, y.v, y.bw * 8, y.bh * 8, {}};
+        pl.px.resize((size_t)pl.pw * pl.ph);
+        for (int by = 0; by < y.bh; ++by)
+            for (int bx = 0; bx < y.bw; ++bx)
+                idct_islow(&y.coef[((size_t)by * y.bw + bx) * 64], qt[y.tq], &pl.px[(size_t)by * 8 * pl.pw + bx * 8],
+                           pl.pw);
+        res.planes.push_back(std::move(pl));
+    }
+    return true;
+}
+
+bool decode_jpeg_gray(const std::vector<uint8_t> &f, Gray8 &out, std::string &err) {
+    JpegPlanes jp;
+    if (!jpeg_decode(f, false, jp, err)) return false;
+    const JpegPlanes::Plane &y = jp.planes[0];
+    out.width = jp.W;
+    out.height = jp.H;
+    out.px.resize((size_t)jp.W * jp.H);
+    for (int r = 0; r < jp.H; ++r) memcpy(&out.px[(size_t)r * jp.W], &y.px[(size_t)r * y.pw], jp.W);
     return true;
 }
 
@@ -520,6 +574,220 @@ bool read_gray8(const std::string &path, Gray8 &out, std::string &err) {
 }
 
 // ----------------------------------------------------------------------------------------------
+// colour: cv::imread(IMREAD_COLOR) for fusion (RunFusion, APD.cpp:1077)
+// ----------------------------------------------------------------------------------------------
+bool decode_png_bgr(const std::vector<uint8_t> &file, Bgr8 &out, std::string &err) {
+    PngRaw png;
+    if (!png_raw(file, png, err)) return false;
+    out.width = png.w;
+    out.height = png.h;
+    out.px.resize((size_t)png.w * png.h * 3);
+    for (size_t i = 0; i < (size_t)png.w * png.h; ++i) {
+        const uint8_t *p = &png.img[i * png.ch];
+        uint8_t *o = &out.px[3 * i];
+        switch (png.ctype) {
+            case 0: case 4: o[0] = o[1] = o[2] = p[0]; break;  // png_set_gray_to_rgb, alpha stripped
+            case 2: case 6: o[0] = p[2]; o[1] = p[1]; o[2] = p[0]; break;
+            case 3: {
+                const size_t k = (size_t)p[0] * 3;
+                if (k + 2 >= png.plte.size()) { err = "PNG palette index out of range"; return false; }
+                o[0] = png.plte[k + 2]; o[1] = png.plte[k + 1]; o[2] = png.plte[k];
+                break;
+            }
+        }
+    }
+    return true;
+}
+
+bool decode_pnm_bgr(const std::vector<uint8_t> &file, Bgr8 &out, std::string &err) {
+    Gray8 g;
+    if (file.size() >= 2 && file[1] == '5') {
+        if (!decode_pnm_gray(file, g, err)) return false;
+        out.width = g.width;
+        out.height = g.height;
+        out.px.resize(g.px.size() * 3);
+        for (size_t i = 0; i < g.px.size(); ++i) out.px[3 * i] = out.px[3 * i + 1] = out.px[3 * i + 2] = g.px[i];
+        return true;
+    }
+    // P6: parse the header with the gray decoder's rules, then copy RGB -> BGR
+    if (!decode_pnm_gray(file, g, err)) return false;
+    const size_t n = (size_t)g.width * g.height;
+    const size_t start = file.size() - n * 3;  // the decoder checked the payload fits; P6 data ends the file
+    out.width = g.width;
+    out.height = g.height;
+    out.px.resize(n * 3);
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t *p = &file[start + 3 * i];
+        out.px[3 * i] = p[2];
+        out.px[3 * i + 1] = p[1];
+        out.px[3 * i + 2] = p[0];
+    }
+    return true;
+}
+
+namespace {
+// libjpeg-turbo jdsample.c with do_fancy_upsampling (the default): upsample one component plane to
+// (hmax/h) x (vmax/v) of its downsampled size (dw x dh real samples; edges replicate, as the
+// context rows of jdmainct.c and the first/last-column special cases do).
+std::vector<uint8_t> upsample_plane(const JpegPlanes::Plane &pl, int dw, int dh, int fx, int fy, int &ow, int &oh) {
+    ow = dw * fx;
+    oh = dh * fy;
+    std::vector<uint8_t> o((size_t)ow * oh);
+    auto at = [&](int r, int c) -> int {
+        r = r < 0 ? 0 : (r >= dh ? dh - 1 : r);
+        c = c < 0 ? 0 : (c >= dw ? dw - 1 : c);
+        return pl.px[(size_t)r * pl.pw + c];
+    };
+    const bool fancy_h = dw > 2;
+    if (fx == 2 && fy == 1) {
+        for (int r = 0; r < dh; ++r)
+            for (int c = 0; c < dw; ++c) {
+                const int v = at(r, c);
+                uint8_t *d = &o[(size_t)r * ow + 2 * c];
+                if (fancy_h) {  // h2v1_fancy_upsample
+                    d[0] = (uint8_t)(c == 0 ? v : (v * 3 + at(r, c - 1) + 1) >> 2);
+                    d[1] = (uint8_t)(c == dw - 1 ? v : (v * 3 + at(r, c + 1) + 2) >> 2);
+                } else {
+                    d[0] = d[1] = (uint8_t)v;
+                }
+            }
+    } else if (fx == 1 && fy == 2) {  // h1v2_fancy_upsample
+        for (int r = 0; r < dh; ++r)
+            for (int c = 0; c < dw; ++c) {
+                const int v3 = at(r, c) * 3;
+                o[(size_t)(2 * r) * ow + c] = (uint8_t)((v3 + at(r - 1, c) + 1) >> 2);
+                o[(size_t)(2 * r + 1) * ow + c] = (uint8_t)((v3 + at(r + 1, c) + 2) >> 2);
+            }
+    } else if (fx == 2 && fy == 2 && fancy_h) {  // h2v2_fancy_upsample
+        for (int r = 0; r < dh; ++r)
+            for (int v = 0; v < 2; ++v) {
+                const int rn = v == 0 ? r - 1 : r + 1;
+                auto colsum = [&](int c) { return at(r, c) * 3 + at(rn, c); };
+                uint8_t *d = &o[(size_t)(2 * r + v) * ow];
+                for (int c = 0; c < dw; ++c) {
+                    const int t = colsum(c);
+                    d[2 * c] = (uint8_t)(c == 0 ? (t * 4 + 8) >> 4 : (t * 3 + colsum(c - 1) + 8) >> 4);
+                    d[2 * c + 1] = (uint8_t)(c == dw - 1 ? (t * 4 + 7) >> 4 : (t * 3 + colsum(c + 1) + 7) >> 4);
+                }
+            }
+    } else {  // h2v1/h2v2 with narrow planes and every other integral ratio: replication (int_upsample)
+        for (int r = 0; r < oh; ++r)
+            for (int c = 0; c < ow; ++c) o[(size_t)r * ow + c] = (uint8_t)at(r / fy, c / fx);
+    }
+    return o;
+}
+}  // namespace
+
+bool decode_jpeg_bgr(const std::vector<uint8_t> &f, Bgr8 &out, std::string &err) {
+    JpegPlanes jp;
+    if (!jpeg_decode(f, true, jp, err)) return false;
+    const int W = jp.W, H = jp.H;
+    out.width = W;
+    out.height = H;
+    out.px.resize((size_t)W * H * 3);
+    if (jp.planes.size() == 1) {  // gray_rgb_convert
+        const JpegPlanes::Plane &y = jp.planes[0];
+        for (int r = 0; r < H; ++r)
+            for (int c = 0; c < W; ++c) {
+                uint8_t *o = &out.px[3 * ((size_t)r * W + c)];
+                o[0] = o[1] = o[2] = y.px[(size_t)r * y.pw + c];
+            }
+        return true;
+    }
+    if (jp.planes.size() != 3) { err = "only 1- and 3-component JPEG is supported"; return false; }
+    std::vector<std::vector<uint8_t>> full(3);
+    std::vector<int> fw(3);
+    for (int k = 0; k < 3; ++k) {
+        const JpegPlanes::Plane &pl = jp.planes[k];
+        if (jp.hmax % pl.h || jp.vmax % pl.v) { err = "non-integral JPEG sampling ratio"; return false; }
+        const int dw = (W * pl.h + jp.hmax - 1) / jp.hmax, dh = (H * pl.v + jp.vmax - 1) / jp.vmax;  // jdinput.c
+        int ow, oh;
+        full[k] = upsample_plane(pl, dw, dh, jp.hmax / pl.h, jp.vmax / pl.v, ow, oh);
+        fw[k] = ow;
+    }
+    // jdapimin.c default_decompress_parms: JFIF -> YCbCr; Adobe transform 0 -> RGB; else by ids
+    bool rgb = false;
+    if (!jp.jfif) {
+        if (jp.adobe_transform >= 0) rgb = jp.adobe_transform == 0;
+        else rgb = jp.planes[0].id == 82 && jp.planes[1].id == 71 && jp.planes[2].id == 66;
+    }
+    // jdcolor.c build_ycc_rgb_table / ycc_rgb_convert (SCALEBITS 16)
+    static int cr_r[256], cb_b[256], cr_g[256], cb_g[256];
+    static bool init = false;
+    if (!init) {
+        auto FIX = [](double x) { return (int)(x * 65536.0 + 0.5); };
+        for (int i = 0; i < 256; ++i) {
+            const int x = i - 128;
+            cr_r[i] = (FIX(1.40200) * x + (1 << 15)) >> 16;
+            cb_b[i] = (FIX(1.77200) * x + (1 << 15)) >> 16;
+            cr_g[i] = -FIX(0.71414) * x;
+            cb_g[i] = -FIX(0.34414) * x + (1 << 15);
+        }
+        init = true;
+    }
+    auto clamp8 = [](int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); };
+    for (int r = 0; r < H; ++r)
+        for (int c = 0; c < W; ++c) {
+            const int y = full[0][(size_t)r * fw[0] + c], cb = full[1][(size_t)r * fw[1] + c],
+                      cr = full[2][(size_t)r * fw[2] + c];
+            uint8_t *o = &out.px[3 * ((size_t)r * W + c)];
+            if (rgb) {
+                o[0] = (uint8_t)cr; o[1] = (uint8_t)cb; o[2] = (uint8_t)y;
+            } else {
+                o[2] = clamp8(y + cr_r[cr]);
+                o[1] = clamp8(y + ((cb_g[cb] + cr_g[cr]) >> 16));
+                o[0] = clamp8(y + cb_b[cb]);
+            }
+        }
+    return true;
+}
+
+bool read_bgr8(const std::string &path, Bgr8 &out, std::string &err) {
+    std::vector<uint8_t> data;
+    if (!read_file(path, data)) { err = "cannot open " + path; return false; }
+    if (data.size() >= 8 && data[0] == 137 && data[1] == 'P') return decode_png_bgr(data, out, err);
+    if (data.size() >= 2 && data[0] == 0xFF && data[1] == 0xD8) return decode_jpeg_bgr(data, out, err);
+    if (data.size() >= 2 && data[0] == 'P') return decode_pnm_bgr(data, out, err);
+    err = "unsupported image format: " + path;
+    return false;
+}
+
+bool write_png_gray8(const std::string &path, const uint8_t *px, int w, int h) {
+    std::vector<uint8_t> raw(((size_t)w + 1) * h);
+    for (int r = 0; r < h; ++r) {
+        raw[((size_t)w + 1) * r] = 0;  // filter: none
+        memcpy(&raw[((size_t)w + 1) * r + 1], px + (size_t)r * w, w);
+    }
+    uLongf zlen = compressBound((uLong)raw.size());
+    std::vector<uint8_t> z(zlen);
+    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), 1) != Z_OK) return false;
+    z.resize(zlen);
+    std::ofstream o(path, std::ios::binary);
+    if (!o) return false;
+    auto put32 = [&](std::vector<uint8_t> &v, uint32_t x) {
+        v.push_back(x >> 24); v.push_back(x >> 16); v.push_back(x >> 8); v.push_back(x);
+    };
+    auto chunk = [&](const char *type, const std::vector<uint8_t> &data) {
+        std::vector<uint8_t> c;
+        put32(c, (uint32_t)data.size());
+        c.insert(c.end(), type, type + 4);
+        c.insert(c.end(), data.begin(), data.end());
+        put32(c, (uint32_t)crc32(0, c.data() + 4, (uInt)(c.size() - 4)));
+        o.write(reinterpret_cast<const char *>(c.data()), (std::streamsize)c.size());
+    };
+    static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+    o.write(reinterpret_cast<const char *>(sig), 8);
+    std::vector<uint8_t> ihdr;
+    put32(ihdr, (uint32_t)w);
+    put32(ihdr, (uint32_t)h);
+    ihdr.insert(ihdr.end(), {8, 0, 0, 0, 0});  // 8-bit gray, deflate, adaptive filter, no interlace
+    chunk("IHDR", ihdr);
+    chunk("IDAT", z);
+    chunk("IEND", {});
+    return (bool)o;
+}
+
+// ----------------------------------------------------------------------------------------------
 // resize
 // ----------------------------------------------------------------------------------------------
 namespace {
@@ -528,10 +796,12 @@ struct LinTab {
     std::vector<float> a0, a1;
     int lim = 0;  // first index that has only one tap (right border)
 };
-// OpenCV resize() coefficient loop for INTER_LINEAR (ksize 2), per axis
-LinTab linear_table(int ssz, int dsz) {
+// OpenCV resize() coefficient loop for INTER_LINEAR (ksize 2), per axis. Along x the tap and its
+// weight are clamped at the borders; along y (clamp = false) only the ROWS are clamped later
+// (resizeGeneric_Invoker clips sy to [0, H-1]) and the weights keep fy.
+LinTab linear_table(int ssz, int dsz, bool clamp = true) {
     LinTab t;
-    const double scale = (double)ssz / dsz;
+    const double scale = 1.0 / ((double)dsz / ssz);  // hal::resize: scale_x = 1./inv_scale_x
     t.ofs.resize(dsz);
     t.a0.resize(dsz);
     t.a1.resize(dsz);
@@ -540,10 +810,12 @@ LinTab linear_table(int ssz, int dsz) {
         float fx = (float)((d + 0.5) * scale - 0.5);
         int sx = (int)std::floor(fx);
         fx -= (float)sx;
-        if (sx < 0) { fx = 0.0f; sx = 0; }
-        if (sx + 1 >= ssz) {
-            t.lim = std::min(t.lim, d);
-            if (sx >= ssz - 1) { fx = 0.0f; sx = ssz - 1; }
+        if (clamp) {
+            if (sx < 0) { fx = 0.0f; sx = 0; }
+            if (sx + 1 >= ssz) {
+                t.lim = std::min(t.lim, d);
+                if (sx >= ssz - 1) { fx = 0.0f; sx = ssz - 1; }
+            }
         }
         t.ofs[d] = sx;
         t.a0[d] = 1.0f - fx;
@@ -551,6 +823,7 @@ LinTab linear_table(int ssz, int dsz) {
     }
     return t;
 }
+inline int clip_row(int y, int h) { return y < 0 ? 0 : (y >= h ? h - 1 : y); }
 }  // namespace
 
 void resize_linear_f32(const float *src, int sw, int sh, float *dst, int dw, int dh) {
@@ -558,7 +831,7 @@ void resize_linear_f32(const float *src, int sw, int sh, float *dst, int dw, int
         memcpy(dst, src, sizeof(float) * sw * sh);
         return;
     }
-    const double sx = (double)sw / dw, sy = (double)sh / dh;
+    const double sx = 1.0 / ((double)dw / sw), sy = 1.0 / ((double)dh / sh);
     const int isx = (int)std::lround(sx), isy = (int)std::lround(sy);
     if (std::fabs(sx - isx) < 2.220446049250313e-16 && std::fabs(sy - isy) < 2.220446049250313e-16 && isx == 2 &&
         isy == 2) {
@@ -571,7 +844,7 @@ void resize_linear_f32(const float *src, int sw, int sh, float *dst, int dw, int
             }
         return;
     }
-    const LinTab tx = linear_table(sw, dw), ty = linear_table(sh, dh);
+    const LinTab tx = linear_table(sw, dw), ty = linear_table(sh, dh, false);
     std::vector<float> r0(dw), r1(dw);
     auto hpass = [&](int row, std::vector<float> &o) {
         const float *s = src + (size_t)row * sw;
@@ -588,13 +861,75 @@ void resize_linear_f32(const float *src, int sw, int sh, float *dst, int dw, int
     };
     for (int y = 0; y < dh; ++y) {
         const int k = ty.ofs[y];
-        hpass(k, r0);
-        hpass(std::min(k + 1, sh - 1), r1);
+        hpass(clip_row(k, sh), r0);
+        hpass(clip_row(k + 1, sh), r1);
         const float b0 = ty.a0[y], b1 = ty.a1[y];
         for (int x = 0; x < dw; ++x) {
             const float p = r0[x] * b0;
             const float q = r1[x] * b1;
             dst[(size_t)y * dw + x] = p + q;
+        }
+    }
+}
+
+// cv::resize INTER_LINEAR on CV_8UC3, OpenCV 4.x fixed-point path (INTER_RESIZE_COEF_BITS 11):
+// HResizeLinear<uchar,int,short> is exact integer arithmetic; VResizeLinear is taken as the x86
+// SIMD kernel (VResizeLinearVec_32s8u: ((S0>>4)*b0 >> 16) + ((S1>>4)*b1 >> 16), then (+2) >> 2,
+// 16- then 8-byte blocks at 128-bit width) with the scalar FixedPtCast tail ((S0*b0 + S1*b1 + 2^21) >> 22). Exact 2x
+// downscales take INTER_AREA's resizeAreaFast ((a+b+c+d+2) >> 2).
+void resize_linear_u8c3(const uint8_t *src, int sw, int sh, uint8_t *dst, int dw, int dh) {
+    const int cn = 3;
+    if (sw == dw && sh == dh) {
+        memcpy(dst, src, (size_t)sw * sh * cn);
+        return;
+    }
+    const double sx = 1.0 / ((double)dw / sw), sy = 1.0 / ((double)dh / sh);
+    const int isx = (int)std::lround(sx), isy = (int)std::lround(sy);
+    if (std::fabs(sx - isx) < 2.220446049250313e-16 && std::fabs(sy - isy) < 2.220446049250313e-16 && isx == 2 &&
+        isy == 2) {
+        for (int y = 0; y < dh; ++y)
+            for (int x = 0; x < dw; ++x)
+                for (int k = 0; k < cn; ++k) {
+                    const uint8_t *s0 = src + ((size_t)(2 * y) * sw + 2 * x) * cn + k, *s1 = s0 + (size_t)sw * cn;
+                    dst[((size_t)y * dw + x) * cn + k] = (uint8_t)((s0[0] + s0[cn] + s1[0] + s1[cn] + 2) >> 2);
+                }
+        return;
+    }
+    auto to_short = [](float v) { return (int)std::nearbyint(v); };  // saturate_cast<short>(float)
+    const LinTab tx = linear_table(sw, dw), ty = linear_table(sh, dh, false);
+    std::vector<int> ax0(dw), ax1(dw);
+    for (int x = 0; x < dw; ++x) {
+        ax0[x] = to_short(tx.a0[x] * 2048.0f);
+        ax1[x] = to_short(tx.a1[x] * 2048.0f);
+    }
+    const int width = dw * cn;
+    std::vector<int> r0(width), r1(width);
+    auto hpass = [&](int row, std::vector<int> &o) {
+        const uint8_t *s = src + (size_t)row * sw * cn;
+        for (int x = 0; x < dw; ++x)
+            for (int k = 0; k < cn; ++k) {
+                const int j = tx.ofs[x] * cn + k;
+                o[x * cn + k] = x < tx.lim ? s[j] * ax0[x] + s[j + cn] * ax1[x] : s[j] * 2048;
+            }
+    };
+    for (int y = 0; y < dh; ++y) {
+        hpass(clip_row(ty.ofs[y], sh), r0);
+        hpass(clip_row(ty.ofs[y] + 1, sh), r1);
+        const int b0 = to_short(ty.a0[y] * 2048.0f), b1 = to_short(ty.a1[y] * 2048.0f);
+        uint8_t *d = dst + (size_t)y * width;
+        auto simd = [&](int x) {
+            const int v = (((r0[x] >> 4) * b0) >> 16) + (((r1[x] >> 4) * b1) >> 16);
+            const int o = (v + 2) >> 2;
+            d[x] = (uint8_t)(o < 0 ? 0 : (o > 255 ? 255 : o));
+        };
+        int x = 0;
+        for (; x <= width - 16; x += 16)  // v_uint8 blocks
+            for (int k = 0; k < 16; ++k) simd(x + k);
+        for (; x < width - 8; x += 8)  // v_int16 blocks (strict <, as in the source)
+            for (int k = 0; k < 8; ++k) simd(x + k);
+        for (; x < width; ++x) {
+            const int o = (r0[x] * b0 + r1[x] * b1 + (1 << 21)) >> 22;
+            d[x] = (uint8_t)(o < 0 ? 0 : (o > 255 ? 255 : o));
         }
     }
 }

@@ -23,6 +23,22 @@ bool decode_png_gray(const std::vector<uint8_t> &file, Gray8 &out, std::string &
 bool decode_jpeg_gray(const std::vector<uint8_t> &file, Gray8 &out, std::string &err);
 bool decode_pnm_gray(const std::vector<uint8_t> &file, Gray8 &out, std::string &err);
 
+// Colour image, BGR interleaved (cv::imread(IMREAD_COLOR), used by fusion: APD.cpp:1077).
+struct Bgr8 {
+    int width = 0, height = 0;
+    std::vector<uint8_t> px;  // row-major B,G,R
+};
+// PNG (gray/RGB/palette, alpha stripped), baseline JPEG (libjpeg-turbo default decode: islow IDCT,
+// fancy chroma upsampling, jdcolor.c YCbCr->RGB tables), binary PGM/PPM.
+bool read_bgr8(const std::string &path, Bgr8 &out, std::string &err);
+bool decode_png_bgr(const std::vector<uint8_t> &file, Bgr8 &out, std::string &err);
+bool decode_jpeg_bgr(const std::vector<uint8_t> &file, Bgr8 &out, std::string &err);
+bool decode_pnm_bgr(const std::vector<uint8_t> &file, Bgr8 &out, std::string &err);
+// cv::imwrite of an 8-bit gray image as PNG (skip.png, APD.cpp:1036-1037).
+bool write_png_gray8(const std::string &path, const uint8_t *px, int w, int h);
+// cv::resize INTER_LINEAR on CV_8UC3 (RescaleImageAndCamera, APD.cpp:857); fixed-point path.
+void resize_linear_u8c3(const uint8_t *src, int sw, int sh, uint8_t *dst, int dw, int dh);
+
 // cv::resize(src, dst, Size(dw, dh), 0, 0, INTER_LINEAR) on a CV_32FC1 image (OpenCV 4.x rules:
 // half-pixel centres, clamped borders, exact 2x downscale handled as INTER_AREA).
 void resize_linear_f32(const float *src, int sw, int sh, float *dst, int dw, int dh);

@@ -81,27 +81,27 @@ def resize_linear(img, w, h):
         a = img[0::2, 0::2]; b = img[0::2, 1::2]; c = img[1::2, 0::2]; d = img[1::2, 1::2]
         return (((a + b) + (c + d)) * F32(0.25)).astype(F32)
 
-    def tab(ssz, dsz):
-        scale = ssz / dsz
+    def tab(ssz, dsz, clamp=True):
+        scale = 1.0 / (dsz / ssz)
         ofs, a0, a1, lim = [], [], [], dsz
         for dd in range(dsz):
             fx = F32((dd + 0.5) * scale - 0.5)
             sx = int(math.floor(fx))
             fx = F32(fx - F32(sx))
-            if sx < 0:
+            if clamp and sx < 0:
                 fx, sx = F32(0), 0
-            if sx + 1 >= ssz:
+            if clamp and sx + 1 >= ssz:
                 lim = min(lim, dd)
                 if sx >= ssz - 1:
                     fx, sx = F32(0), ssz - 1
             ofs.append(sx); a0.append(F32(1) - fx); a1.append(fx)
         return np.array(ofs), np.array(a0, F32), np.array(a1, F32), lim
     xo, xa0, xa1, xl = tab(sw, w)
-    yo, ya0, ya1, _ = tab(sh, h)
+    yo, ya0, ya1, _ = tab(sh, h, clamp=False)  # rows clipped below, weights keep fy
     xo1 = np.minimum(xo + 1, sw - 1)
     rows = img[:, xo] * xa0 + np.where(np.arange(w) < xl, img[:, xo1] * xa1, F32(0))
-    r0 = rows[yo]
-    r1 = rows[np.minimum(yo + 1, sh - 1)]
+    r0 = rows[np.clip(yo, 0, sh - 1)]
+    r1 = rows[np.clip(yo + 1, 0, sh - 1)]
     return (r0 * ya0[:, None] + r1 * ya1[:, None]).astype(F32)
 
 
