@@ -178,7 +178,14 @@ class Outputs:
 EXPORTS = ["apd_abi_version", "apd_device_count", "apd_create", "apd_destroy", "apd_last_error",
            "apd_set_problem", "apd_run_patchmatch", "apd_stage_prepare", "apd_stage_iteration",
            "apd_stage_finish", "apd_synchronize", "apd_get_results", "apd_get_timing", "apd_profile_reset",
-           "apd_profile_query", "apd_epilogue"]
+           "apd_profile_query", "apd_epilogue", "apd_fusion_create", "apd_fusion_destroy",
+           "apd_fusion_last_error", "apd_fusion_set_views", "apd_fusion_weak_filter", "apd_fusion_consistency",
+           "apd_fusion_tat_levels"]
+
+
+class ApdFusionView(C.Structure):  # include/apd_fusion.h
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("camera", ApdCamera),
+                ("depth", C.c_void_p), ("normal", C.c_void_p), ("weak", C.c_void_p), ("confidence", C.c_void_p)]
 
 
 def load_library(path: str = LIB_PATH) -> C.CDLL:
@@ -208,10 +215,86 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.apd_profile_query.restype = C.c_int32
     lib.apd_profile_query.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                       C.POINTER(C.c_int64)]
+    lib.apd_fusion_create.restype = C.c_void_p
+    lib.apd_fusion_create.argtypes = [C.c_int32]
+    lib.apd_fusion_destroy.argtypes = [C.c_void_p]
+    lib.apd_fusion_last_error.restype = C.c_char_p
+    lib.apd_fusion_last_error.argtypes = [C.c_void_p]
+    lib.apd_fusion_set_views.restype = C.c_int32
+    lib.apd_fusion_set_views.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ApdFusionView)]
+    lib.apd_fusion_weak_filter.restype = C.c_int32
+    lib.apd_fusion_weak_filter.argtypes = [C.c_void_p, C.c_int32, C.c_float, C.c_void_p]
+    lib.apd_fusion_consistency.restype = C.c_int32
+    lib.apd_fusion_consistency.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_float, C.c_void_p,
+                                           C.c_void_p, C.c_void_p]
+    lib.apd_fusion_tat_levels.restype = C.c_int32
+    lib.apd_fusion_tat_levels.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_float, C.c_float,
+                                          C.c_void_p, C.c_void_p, C.c_void_p]
     lib.apd_epilogue.restype = C.c_int32
     lib.apd_epilogue.argtypes = [C.c_int32, C.c_int32, C.POINTER(C.c_float), C.c_float, C.c_float,
                                  C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_uint8)]
     return lib
+
+
+class FusionEngine:
+    """One apd_fusion_ctx (include/apd_fusion.h) with its views resident on the device."""
+
+    def __init__(self, device: int = 0, lib: Optional[C.CDLL] = None):
+        self.lib = lib or load_library()
+        self.ctx = self.lib.apd_fusion_create(device)
+        if not self.ctx:
+            raise ApdError("apd_fusion_create failed: " + (self.lib.apd_fusion_last_error(None) or b"?").decode())
+
+    def _check(self, st: int, what: str):
+        if st != 0:
+            msg = (self.lib.apd_fusion_last_error(self.ctx) or b"").decode()
+            raise ApdError(f"{what} -> {STATUS.get(st, st)}: {msg}")
+
+    def set_views(self, views):
+        """views: dicts with depth (H,W) f32, normal (H,W,3) f32, weak/conf (H,W) u8, cam ApdCamera."""
+        self._views = views
+        arr = (ApdFusionView * len(views))()
+        for i, v in enumerate(views):
+            arr[i] = ApdFusionView(v["depth"].shape[1], v["depth"].shape[0], v["cam"], v["depth"].ctypes.data,
+                                   v["normal"].ctypes.data, v["weak"].ctypes.data, v["conf"].ctypes.data)
+        self._check(self.lib.apd_fusion_set_views(self.ctx, len(views), arr), "apd_fusion_set_views")
+
+    def weak_filter(self, ref: int, q_view: float) -> np.ndarray:
+        out = np.zeros(self._views[ref]["depth"].shape, np.uint8)
+        self._check(self.lib.apd_fusion_weak_filter(self.ctx, ref, q_view, out.ctypes.data), "apd_fusion_weak_filter")
+        return out
+
+    def consistency(self, ref: int, src: Sequence[int], q_angle: float):
+        H, W = self._views[ref]["depth"].shape
+        s = np.asarray(src, np.int32)
+        pix = np.zeros((H, W, len(s)), np.int32)
+        er = np.zeros((H, W, len(s)), np.float32)
+        q = np.zeros((H, W, len(s)), np.float32)
+        self._check(self.lib.apd_fusion_consistency(self.ctx, ref, len(s), s.ctypes.data, q_angle, pix.ctypes.data,
+                                                    er.ctypes.data, q.ctypes.data), "apd_fusion_consistency")
+        return pix, er, q
+
+    def tat_levels(self, ref: int, src: Sequence[int], dist_base: float, depth_base: float, q_k=None):
+        H, W = self._views[ref]["depth"].shape
+        s = np.asarray(src, np.int32)
+        pix = np.zeros((H, W, len(s)), np.int32)
+        lv = np.zeros((H, W, len(s)), np.uint8)
+        qk = None if q_k is None else np.asarray(q_k, np.float32)
+        self._check(self.lib.apd_fusion_tat_levels(self.ctx, ref, len(s), s.ctypes.data, dist_base, depth_base,
+                                                   None if qk is None else qk.ctypes.data, pix.ctypes.data,
+                                                   lv.ctypes.data), "apd_fusion_tat_levels")
+        return pix, lv
+
+    def close(self):
+        if self.ctx:
+            self.lib.apd_fusion_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Engine:

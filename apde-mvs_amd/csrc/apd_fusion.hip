@@ -81,13 +81,13 @@ struct DevView {
     const uint8_t *conf;
 };
 
-// XCD-aware block order: consecutive blocks on one XCD walk neighbouring rows (shared L2 lines of
-// the source maps). 8 XCDs, round-robin dispatch.
+// XCD-aware block order: the dispatcher deals blocks round-robin to the 8 XCDs, so block b runs on
+// XCD b % 8; give each XCD a contiguous range of pixel blocks (neighbouring rows share L2 lines of the
+// source maps). Bijective for any block count.
 __device__ inline int xcd_block(int b, int nb) {
-    const int per = (nb + 7) / 8;
+    const int q = nb / 8, rem = nb % 8;
     const int x = b % 8, i = b / 8;
-    const int m = x * per + i;
-    return m < nb ? m : b;
+    return x * q + (x < rem ? x : rem) + i;
 }
 
 constexpr int kWeak = 0, kStrong = 1;  // PixelState, main.h:74-78

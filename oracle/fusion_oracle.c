@@ -162,6 +162,45 @@ void oracle_weak_vis_filter(int n, const oracle_fusion_view *v, int ref_index, u
     }
 }
 
+/* Per-(pixel, source) quantities of RunFusion / RunFusion_TAT_* (APD.cpp:1166-1187) for view `ref`
+   against source VIEW INDICES src[0..num_src), without masks: out index p*num_src + j.
+   sp = source pixel (-1: out of bounds or source depth <= 0); dist = reproj_error,
+   rel = relative_depth_diff, angle = GetAngle, q = its acosf argument. Unset for depth <= 0. */
+void oracle_fusion_candidates(const oracle_fusion_view *v, int ref, int num_src, const int32_t *src, int32_t *sp_out,
+                              float *dist_out, float *rel_out, float *angle_out, float *q_out) {
+    const oracle_fusion_view *rv = &v[ref];
+    for (int r = 0; r < rv->height; ++r)
+        for (int c = 0; c < rv->width; ++c) {
+            const size_t p = (size_t)r * rv->width + c;
+            float ref_depth = rv->depth[p];
+            for (int j = 0; j < num_src; ++j) sp_out[p * num_src + j] = -1;
+            if (ref_depth <= 0.0) continue;
+            const float *ref_normal = rv->normal + 3 * p;
+            f3 PointX = get_3d_point_on_world(c, r, ref_depth, &rv->camera);
+            for (int j = 0; j < num_src; ++j) {
+                const oracle_fusion_view *sv = &v[src[j]];
+                float px, py, proj_depth;
+                project_camera(PointX, &sv->camera, &px, &py, &proj_depth);
+                int src_r = int_x86(py + 0.5f), src_c = int_x86(px + 0.5f);
+                if (!(src_c >= 0 && src_c < sv->width && src_r >= 0 && src_r < sv->height)) continue;
+                const size_t spx = (size_t)src_r * sv->width + src_c;
+                float src_depth = sv->depth[spx];
+                if (src_depth <= 0.0) continue;
+                const float *src_normal = sv->normal + 3 * spx;
+                f3 tmp_X = get_3d_point_on_world(src_c, src_r, src_depth, &sv->camera);
+                float tx, ty;
+                project_camera(tmp_X, &rv->camera, &tx, &ty, &proj_depth);
+                const size_t o = p * num_src + j;
+                sp_out[o] = (int32_t)spx;
+                dist_out[o] = (float)sqrt(pow(c - tx, 2) + pow(r - ty, 2));
+                rel_out[o] = fabsf(proj_depth - ref_depth) / ref_depth;
+                angle_out[o] = get_angle(ref_normal, src_normal);
+                float dot = ref_normal[0] * src_normal[0] + ref_normal[1] * src_normal[1] + ref_normal[2] * src_normal[2];
+                q_out[o] = (float)(dot / (cv_norm3(ref_normal) * cv_norm3(src_normal)));
+            }
+        }
+}
+
 typedef struct {
     float *xyz, *bgr;
     int64_t count, cap;

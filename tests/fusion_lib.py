@@ -70,7 +70,7 @@ def resize_bgr(lib, img, w, h):
     return dst
 
 
-def make_fusion_scan(folder, width=96, height=72, n_src=4, seed=11, image_scale=1, noise=0.002):
+def make_fusion_scan(folder, width=96, height=72, n_src=4, seed=11, image_scale=1, noise=0.0003):
     """Writes a fusion-ready scan; returns the scene. image_scale > 1 stores colour images larger
     than the depth maps (RescaleImageAndCamera path)."""
     sc = synth.make_scene(width, height, n_src, seed=seed)
@@ -102,19 +102,26 @@ def make_fusion_scan(folder, width=96, height=72, n_src=4, seed=11, image_scale=
         fh.write(f"{nv}\n")
         for i, pl in enumerate(sc.pairs):
             fh.write(f"{i}\n{len(pl)} " + " ".join(f"{j} {s}" for j, s in pl) + "\n")
-    # per-quad world normals from the label map: estimate from the GT point cloud per label
     for i in range(nv):
         d = os.path.join(folder, "APD", f"{i:08d}")
         os.makedirs(d, exist_ok=True)
         gt = sc.gt_depth[i]
         depth = (gt * (1.0 + rng.normal(0.0, noise, gt.shape))).astype(np.float32)
+        depth[rng.random(gt.shape) < 0.08] *= 1.25  # outliers behind the surface: WeakVisFilter occlusions
         depth[rng.random(gt.shape) < 0.03] = 0.0
         depth[rng.random(gt.shape) < 0.01] = -1.0
-        # camera-frame normals from depth gradients of the GT (consistent across views up to R)
-        gy, gx = np.gradient(gt.astype(np.float64))
-        n = np.stack([-gx, -gy, np.full_like(gx, 0.02)], -1)
-        n /= np.linalg.norm(n, axis=-1, keepdims=True)
-        n += rng.normal(0.0, 0.02, n.shape)
+        # camera-frame surface normals of the GT geometry (cross product of the back-projected
+        # neighbours), so the same surface has nearly the same normal in every view
+        Kinv = np.linalg.inv(cam_k(sc.cameras[i]))
+        ys, xs = np.mgrid[0:height, 0:width].astype(np.float64)
+        rays = np.stack([xs, ys, np.ones_like(xs)], -1) @ Kinv.T
+        P = rays * gt[..., None].astype(np.float64)
+        du = np.gradient(P, axis=1)
+        dv = np.gradient(P, axis=0)
+        n = np.cross(du, dv)
+        n /= np.maximum(np.linalg.norm(n, axis=-1, keepdims=True), 1e-12)
+        n = np.where((n[..., 2:3] > 0), -n, n)  # face the camera
+        n += rng.normal(0.0, 0.01, n.shape)
         n = n.astype(np.float32)
         n[rng.random(gt.shape) < 0.005] = 0.0
         weak = rng.choice(np.array([0, 1, 2], np.uint8), size=gt.shape, p=[0.35, 0.6, 0.05])
@@ -125,6 +132,10 @@ def make_fusion_scan(folder, width=96, height=72, n_src=4, seed=11, image_scale=
         synth.write_bin_mat(os.path.join(d, "weak.bin"), weak)
         synth.write_bin_mat(os.path.join(d, "confidence.bin"), conf)
     return sc
+
+
+def cam_k(cam):
+    return cam.K
 
 
 def load_views(folder, hl):
@@ -161,6 +172,43 @@ def load_views(folder, hl):
 
 
 VARIANTS = {"ETH3D": 0, "TaT_i": 1, "TaT_a": 2}
+
+
+def _oracle_views(views):
+    n = len(views)
+    arr = (OracleFusionView * n)()
+    keep = []
+    for i, v in enumerate(views):
+        srcs = np.array(v["srcs"], np.int32)
+        keep.append(srcs)
+        arr[i] = OracleFusionView(v["depth"].shape[1], v["depth"].shape[0], v["cam"], v["depth"].ctypes.data,
+                                  v["normal"].ctypes.data, v["weak"].ctypes.data, v["conf"].ctypes.data,
+                                  v["bgr"].ctypes.data, v["ref"], len(srcs), srcs.ctypes.data)
+    return arr, keep
+
+
+def oracle_weak_filter(views, ref):
+    lib = oracle()
+    lib.oracle_weak_vis_filter.argtypes = [C.c_int, C.POINTER(OracleFusionView), C.c_int, C.c_void_p]
+    arr, _keep = _oracle_views(views)
+    out = np.zeros(views[ref]["depth"].shape, np.uint8)
+    lib.oracle_weak_vis_filter(len(views), arr, ref, out.ctypes.data)
+    return out
+
+
+def oracle_candidates(views, ref, src_idx):
+    """Per-(pixel, source) sp / dist / rel / angle / q of the reference's loops (no masks)."""
+    lib = oracle()
+    lib.oracle_fusion_candidates.argtypes = [C.POINTER(OracleFusionView), C.c_int, C.c_int, C.c_void_p] + \
+        [C.c_void_p] * 5
+    arr, _keep = _oracle_views(views)
+    H, W = views[ref]["depth"].shape
+    s = np.asarray(src_idx, np.int32)
+    shp = (H, W, len(s))
+    sp = np.zeros(shp, np.int32)
+    f = [np.zeros(shp, np.float32) for _ in range(4)]
+    lib.oracle_fusion_candidates(arr, ref, len(s), s.ctypes.data, sp.ctypes.data, *[x.ctypes.data for x in f])
+    return sp, f[0], f[1], f[2], f[3]
 
 
 def run_oracle(views, dataset, weak_filter):

@@ -203,6 +203,49 @@ def _run_cli(folder, dataset, weak_filter, export_color=True):
 
 
 @pytest.mark.gpu
+def test_fusion_kernels_match_oracle(fusion_scan, hl):
+    """Each device entry point of include/apd_fusion.h against the oracle's literal loops."""
+    views = FL.load_views(fusion_scan, hl)
+    eng = A.FusionEngine(0)
+    eng.set_views(views)
+    q_view = hl.apdhost_view_cut_deg(80.0)
+    q_angle = hl.apdhost_angle_cut_lt(f32(0.174533))
+    ab, ag = f32(0.06981317007977318), f32(0.05235987755982988)
+    q_k = [1.0, 1.0] + [hl.apdhost_angle_cut_lt(f32(np.float32(k) * np.float32(ag) + np.float32(ab)))
+                        for k in range(2, 33)]
+    for i in range(len(views)):
+        got = eng.weak_filter(i, q_view)
+        exp = FL.oracle_weak_filter(views, i)
+        assert np.array_equal(got, exp), f"weak filter view {i}: {int((got != exp).sum())} px differ"
+        src = list(range(len(views)))
+        src.remove(i)
+        sp, dist, rel, ang, q = FL.oracle_candidates(views, i, src)
+        live = (views[i]["depth"] > 0)[..., None] & np.ones(len(src), bool)
+        valid = sp >= 0
+        cons = valid & (dist < 2.0) & (rel < np.float32(0.01)) & (ang < np.float32(0.174533))
+        pix, er, qq = eng.consistency(i, src, q_angle)
+        exp_pix = np.where(cons, sp, -1)
+        bad = (pix != exp_pix) & live
+        assert not bad.any(), f"consistency view {i}: {int(bad.sum())} differ, first {np.argwhere(bad)[:3]}"
+        chk = valid & live
+        assert np.array_equal(er[chk].view(np.uint32), (dist + np.float32(200) * rel)[chk].view(np.uint32))
+        assert np.array_equal(qq[chk].view(np.uint32), q[chk].view(np.uint32))
+        for tat_i, depth_base in ((True, np.float32(1 / 3500)), (False, np.float32(1 / 3000))):
+            tp, lv = eng.tat_levels(i, src, 0.25, float(depth_base), q_k if tat_i else None)
+            exp_lv = np.full(sp.shape, 255, np.uint8)
+            for k in range(len(src), 1, -1):
+                kk = np.float32(k)
+                ok = valid & (dist < kk * np.float32(0.25)) & (rel < kk * depth_base)
+                if tat_i:
+                    ok &= ang < kk * ag + ab
+                exp_lv[ok] = k
+            assert not ((tp != sp) & live).any(), f"tat src pixels view {i}"
+            bad = (lv != exp_lv) & live
+            assert not bad.any(), f"tat levels view {i} tat_i={tat_i}: {int(bad.sum())} differ"
+    eng.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dataset", ["ETH3D", "TaT_i", "TaT_a"])
 @pytest.mark.parametrize("weak_filter", [True, False])
 def test_fusion_cli_matches_oracle(fusion_scan, hl, tmp_path, dataset, weak_filter):
@@ -212,7 +255,7 @@ def test_fusion_cli_matches_oracle(fusion_scan, hl, tmp_path, dataset, weak_filt
     assert "Fusion done!" in out
     views = FL.load_views(folder, hl)
     xyz, col, skips, counts = FL.run_oracle(views, dataset, weak_filter)
-    assert len(xyz) > 1000
+    assert len(xyz) > 500
     got = open(os.path.join(folder, "APD", "APD.ply"), "rb").read()
     exp = FL.ply_bytes(xyz, col)
     if got != exp:
