@@ -506,9 +506,10 @@ int main(int argc, char **argv) {
             std::cout << "Error: " << ferr << std::endl;
             return false;
         }
-        printf("Fusion: %lld points, load %.0f ms, upload %.0f ms, weak filter %.0f ms, fuse %.0f ms (device %.0f ms), "
-               "write %.0f ms\n",
-               (long long)rep.points, rep.load_ms, rep.upload_ms, rep.filter_ms, rep.fuse_ms, rep.gpu_ms, rep.write_ms);
+        printf("Fusion: %lld points, load %.0f ms, upload %.0f ms, weak filter %.0f ms, fuse %.0f ms (device %.0f ms, "
+               "terms %.0f ms, commit %.0f ms), write %.0f ms\n",
+               (long long)rep.points, rep.load_ms, rep.upload_ms, rep.filter_ms, rep.fuse_ms, rep.gpu_ms, rep.term_ms,
+               rep.commit_ms, rep.write_ms);
         return true;
     };
     if (only_fuse) {

@@ -123,7 +123,9 @@ struct View {
     apd_camera cam{};
     Mat depth, normal, weak, conf;
     Bgr8 color;  // at depth-map size
-    std::vector<uint8_t> mask, skip;
+    uint8_t *mask = nullptr;  // into the global mask array (all views, concatenated)
+    size_t off = 0;           // this view's first pixel in the global arrays
+    std::vector<uint8_t> skip;
 };
 
 // One view as RunFusion loads it (APD.cpp:1071-1133).
@@ -167,7 +169,6 @@ bool load_view(const std::string &dense, const Problem &pb, MatStore &store, Vie
         v.cam.width = W;
         v.cam.height = H;
     }
-    v.mask.assign((size_t)W * H, 0);
     v.skip.assign((size_t)W * H, 0);
     return true;
 }
@@ -210,59 +211,98 @@ struct Fuser {
 
     // Device half of one image of RunFusion: mask-independent candidate records.
     struct Cands {
-        std::vector<int32_t> pix;
-        std::vector<float> er, q;
+        // device records, compacted per pixel by consistency(): slot m < cnt[p] of pixel p holds the
+        // m-th consistent source (in j order): global target index tgt (view offset + source pixel),
+        // its exp term, and j
+        std::vector<int32_t> tgt;
+        std::vector<float> er, term;
+        std::vector<uint8_t> cnt, jj;
     };
+    double term_ms = 0, commit_ms = 0;
+    int threads = 1;
     bool consistency(int i, float q_angle, Cands &c) {
         const int ref = index_of(problems[i].ref_image_id);
         const std::vector<int32_t> src = src_list(i);
-        const size_t n = (size_t)views[ref].depth.rows * views[ref].depth.cols * src.size();
-        c.pix.resize(n);
+        const size_t npx = (size_t)views[ref].depth.rows * views[ref].depth.cols, N = src.size(), n = npx * N;
+        c.tgt.resize(n);
         c.er.resize(n);
-        c.q.resize(n);
-        const auto t0 = Clock::now();
-        const bool ok = dev(apd_fusion_consistency(ctx, ref, (int32_t)src.size(), src.data(), q_angle, c.pix.data(),
-                                                   c.er.data(), c.q.data()),
+        c.term.resize(n);
+        c.jj.resize(n);
+        c.cnt.resize(npx);
+        auto t0 = Clock::now();
+        const bool ok = dev(apd_fusion_consistency(ctx, ref, (int32_t)N, src.data(), q_angle, c.tgt.data(),
+                                                   c.er.data(), c.term.data()),
                             "apd_fusion_consistency");
         gpu_ms += ms_since(t0);
-        return ok;
+        if (!ok) return false;
+        // Mask-independent work in parallel: the exp(-tmp_index) term of every consistent candidate
+        // (APD.cpp:1192-1193, glibc acosf/expf like the reference) and the per-pixel compaction;
+        // skipped pixels (WeakVisFilter) get no candidates.
+        t0 = Clock::now();
+        const View &rv = views[ref];
+        std::vector<size_t> soff(N);
+        for (size_t j = 0; j < N; ++j) soff[j] = views[src[j]].off;
+        std::vector<std::thread> th;
+        const size_t chunk = (npx + threads - 1) / threads;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t]() {
+                const size_t e = std::min(npx, (t + 1) * chunk);
+                for (size_t p = t * chunk; p < e; ++p) {
+                    const size_t o = p * N;
+                    int m = 0;
+                    if (rv.skip[p] != 1)
+                        for (size_t j = 0; j < N; ++j) {
+                            const int32_t sp = c.tgt[o + j];
+                            if (sp < 0) continue;
+                            const float tmp_index = c.er[o + j] + angle_of_q(c.term[o + j]) * 10;
+                            c.tgt[o + m] = (int32_t)(soff[j] + (size_t)sp);
+                            c.term[o + m] = expf(-tmp_index);
+                            c.jj[o + m] = (uint8_t)j;
+                            ++m;
+                        }
+                    c.cnt[p] = (uint8_t)m;
+                }
+            });
+        for (auto &t : th) t.join();
+        term_ms += ms_since(t0);
+        return true;
     }
 
-    // RunFusion ordered commit (APD.cpp:1147-1219) over the kernel's records.
-    void commit_default(int i, const Cands &cd) {
+    // RunFusion ordered commit (APD.cpp:1147-1219) over the compacted candidates. A pixel without
+    // consistent candidates can never be accepted and has no side effect, so it is passed over.
+    void commit_default(int i, const Cands &cd, uint8_t *gmask) {
         const int ref = index_of(problems[i].ref_image_id);
         View &rv = views[ref];
         const std::vector<int32_t> src = src_list(i);
         const int N = (int)src.size(), W = rv.depth.cols, H = rv.depth.rows;
         const float *depth = rv.depth.ptr<float>();
         const uint8_t *weak = rv.weak.ptr<uint8_t>();
-        std::vector<int32_t> used(N > 0 ? N : 1);
+        int32_t used[APD_MAX_IMAGES];
         for (int r = 0; r < H; ++r)
             for (int c = 0; c < W; ++c) {
                 const size_t p = (size_t)r * W + c;
-                if (rv.mask[p] == 1 || rv.skip[p] == 1) continue;
-                const float ref_depth = depth[p];
-                if (ref_depth <= 0.0) continue;
+                const int m = cd.cnt[p];
+                if (m == 0 || rv.mask[p] == 1) continue;
+                const size_t o = p * N;
                 int num_consistent = 0;
                 float dynamic_consistency = 0.0f;
-                const size_t o = p * N;
-                for (int j = 0; j < N; ++j) {
-                    used[j] = -1;
-                    const int32_t sp = cd.pix[o + j];
-                    if (sp < 0 || views[src[j]].mask[sp] == 1) continue;
-                    used[j] = sp;
-                    const float tmp_index = cd.er[o + j] + angle_of_q(cd.q[o + j]) * 10;
-                    dynamic_consistency += expf(-tmp_index);
+                for (int k = 0; k < m; ++k) {
+                    const int32_t t = cd.tgt[o + k];
+                    used[k] = -1;
+                    if (gmask[t] == 1) continue;
+                    used[k] = t;
+                    dynamic_consistency += cd.term[o + k];
                     num_consistent++;
                 }
                 const float factor = (weak[p] == APD_WEAK ? 0.45f : 0.3f);
                 if (num_consistent >= 1 && (dynamic_consistency > factor * num_consistent)) {
                     const uint8_t *rc = color_at(ref, (int)p);
                     float col[3] = {(float)rc[0], (float)rc[1], (float)rc[2]};
-                    for (int j = 0; j < N; ++j) {
-                        if (used[j] == -1) continue;
-                        views[src[j]].mask[used[j]] = 1;
-                        const uint8_t *sc = color_at(src[j], used[j]);
+                    for (int k = 0; k < m; ++k) {
+                        if (used[k] == -1) continue;
+                        gmask[used[k]] = 1;
+                        const int sv = src[cd.jj[o + k]];
+                        const uint8_t *sc = color_at(sv, (int)(used[k] - (int64_t)views[sv].off));
                         col[0] += sc[0];
                         col[1] += sc[1];
                         col[2] += sc[2];
@@ -270,7 +310,7 @@ struct Fuser {
                     col[0] /= (num_consistent + 1);
                     col[1] /= (num_consistent + 1);
                     col[2] /= (num_consistent + 1);
-                    emit(point_on_world(c, r, ref_depth, rv.cam), col);
+                    emit(point_on_world(c, r, depth[p], rv.cam), col);
                 }
             }
     }
@@ -295,57 +335,136 @@ struct Fuser {
         return ok;
     }
 
-    // RunFusion_TAT_I / _A ordered commit (APD.cpp:1347-1427, 1541-1603): the per-image cost cache
-    // `diff` becomes (level, source pixel) per source, refreshed only by usable candidates.
+    // RunFusion_TAT_I / _A ordered commit (APD.cpp:1347-1427, 1541-1603). The per-image cost cache
+    // `diff` becomes (level, source pixel) per source, refreshed only by usable candidates; a pixel's
+    // outcome depends on the cache state and masks[src], and writes only masks[ref] at itself. So when
+    // no source is the reference view itself (masks[src] are then fixed during this image), the scan
+    // splits exactly into row chunks: (1) each chunk's last cache update per source, in parallel,
+    // (2) the incoming cache of every chunk by a prefix fold, (3) each chunk replayed in parallel.
+    struct TatChunk {
+        std::vector<uint8_t> last_lv;
+        std::vector<int32_t> last_pix;
+        std::vector<float> xyz, bgr;
+        int64_t skip_weak = 0;
+    };
     int64_t commit_tat(int i, bool tat_i, const Levels &l) {
         const int ref = index_of(problems[i].ref_image_id);
         View &rv = views[ref];
         const std::vector<int32_t> src = src_list(i);
         const int N = (int)src.size(), W = rv.depth.cols, H = rv.depth.rows;
         const float *depth = rv.depth.ptr<float>();
-        std::vector<uint8_t> cur_lv(N > 0 ? N : 1, 255);
-        std::vector<int32_t> cur_pix(N > 0 ? N : 1, 0);
-        int64_t skip_weak = 0;
-        for (int r = 0; r < H; ++r)
-            for (int c = 0; c < W; ++c) {
-                const size_t p = (size_t)r * W + c;
-                if (rv.skip[p] == 1) {
-                    skip_weak++;
-                    continue;
-                }
-                const float ref_depth = depth[p];
-                if (ref_depth <= 0.0) continue;
+        bool self_src = false;
+        for (int s : src) self_src |= s == ref;
+        const int nch = self_src ? 1 : std::max(1, std::min(threads * 4, H));
+        std::vector<TatChunk> ch(nch);
+        auto rows_of = [&](int k, int &r0, int &r1) {
+            r0 = (int)((int64_t)H * k / nch);
+            r1 = (int)((int64_t)H * (k + 1) / nch);
+        };
+        auto usable = [&](size_t p) { return rv.skip[p] != 1 && !(depth[p] <= 0.0f); };  // NaN depths are processed
+        auto par = [&](auto fn) {
+            if (nch == 1) { fn(0); return; }
+            std::vector<std::thread> th;
+            std::atomic<int> next{0};
+            for (int t = 0; t < std::min(threads, nch); ++t)
+                th.emplace_back([&]() {
+                    for (int k; (k = next++) < nch;) fn(k);
+                });
+            for (auto &t : th) t.join();
+        };
+        // (1) last usable update per source in each chunk (255 = none in this chunk)
+        par([&](int k) {
+            TatChunk &C = ch[k];
+            C.last_lv.assign(N, 255);
+            C.last_pix.assign(N, -1);
+            int r0, r1;
+            rows_of(k, r0, r1);
+            for (size_t p = (size_t)r0 * W; p < (size_t)r1 * W; ++p) {
+                if (!usable(p)) continue;
                 const size_t o = p * N;
                 for (int j = 0; j < N; ++j) {
                     const int32_t sp = l.pix[o + j];
                     if (sp < 0 || views[src[j]].mask[sp] == 1) continue;
-                    cur_lv[j] = l.lv[o + j];
-                    cur_pix[j] = sp;
-                }
-                for (int k = 2; k <= N; ++k) {
-                    int count = 0;
-                    for (int j = 0; j < N; ++j) count += cur_lv[j] <= k;
-                    if (count >= k) {
-                        const uint8_t *rc = color_at(ref, (int)p);
-                        float col[3] = {(float)rc[0], (float)rc[1], (float)rc[2]};
-                        if (tat_i) {
-                            for (int j = 0; j < N; ++j) {
-                                if (cur_lv[j] > k) continue;
-                                const uint8_t *sc = color_at(src[j], cur_pix[j]);
-                                col[0] += (float)sc[0];
-                                col[1] += (float)sc[1];
-                                col[2] += (float)sc[2];
-                            }
-                            col[0] /= (count + 1.0f);
-                            col[1] /= (count + 1.0f);
-                            col[2] /= (count + 1.0f);
-                        }
-                        emit(point_on_world(c, r, ref_depth, rv.cam), col);
-                        rv.mask[p] = 1;
-                        break;
-                    }
+                    C.last_lv[j] = l.lv[o + j];
+                    C.last_pix[j] = sp;
                 }
             }
+        });
+        // (2) incoming cache per chunk: the image starts with FLT_MAX costs (level 255)
+        std::vector<std::vector<uint8_t>> in_lv(nch, std::vector<uint8_t>(N, 255));
+        std::vector<std::vector<int32_t>> in_pix(nch, std::vector<int32_t>(N, 0));
+        for (int k = 1; k < nch; ++k)
+            for (int j = 0; j < N; ++j) {
+                const bool upd = ch[k - 1].last_pix[j] >= 0;
+                in_lv[k][j] = upd ? ch[k - 1].last_lv[j] : in_lv[k - 1][j];
+                in_pix[k][j] = upd ? ch[k - 1].last_pix[j] : in_pix[k - 1][j];
+            }
+        // (3) replay every chunk from its incoming cache
+        par([&](int k) {
+            TatChunk &C = ch[k];
+            std::vector<uint8_t> cur_lv = in_lv[k];
+            std::vector<int32_t> cur_pix = in_pix[k];
+            int r0, r1;
+            rows_of(k, r0, r1);
+            for (int r = r0; r < r1; ++r)
+                for (int c = 0; c < W; ++c) {
+                    const size_t p = (size_t)r * W + c;
+                    if (rv.skip[p] == 1) {
+                        C.skip_weak++;
+                        continue;
+                    }
+                    const float ref_depth = depth[p];
+                    if (ref_depth <= 0.0) continue;
+                    const size_t o = p * N;
+                    for (int j = 0; j < N; ++j) {
+                        const int32_t sp = l.pix[o + j];
+                        if (sp < 0 || views[src[j]].mask[sp] == 1) continue;
+                        cur_lv[j] = l.lv[o + j];
+                        cur_pix[j] = sp;
+                    }
+                    // count(k) = #{j : level_j <= k}: levels are monotone in k (thresholds grow with k)
+                    int hist[APD_MAX_IMAGES + 2] = {0};
+                    for (int j = 0; j < N; ++j) hist[cur_lv[j] <= N ? cur_lv[j] : N + 1]++;
+                    int count = 0;
+                    for (int kk = 2; kk <= N; ++kk) {
+                        count += hist[kk];
+                        if (count >= kk) {
+                            const uint8_t *rc = color_at(ref, (int)p);
+                            float col[3] = {(float)rc[0], (float)rc[1], (float)rc[2]};
+                            if (tat_i) {
+                                for (int j = 0; j < N; ++j) {
+                                    if (cur_lv[j] > kk) continue;
+                                    const uint8_t *sc = color_at(src[j], cur_pix[j]);
+                                    col[0] += (float)sc[0];
+                                    col[1] += (float)sc[1];
+                                    col[2] += (float)sc[2];
+                                }
+                                col[0] /= (count + 1.0f);
+                                col[1] /= (count + 1.0f);
+                                col[2] /= (count + 1.0f);
+                            }
+                            const F3 pt = point_on_world(c, r, ref_depth, rv.cam);
+                            C.xyz.insert(C.xyz.end(), {pt.x, pt.y, pt.z});
+                            C.bgr.insert(C.bgr.end(), {col[0], col[1], col[2]});
+                            rv.mask[p] = 1;
+                            break;
+                        }
+                    }
+                }
+        });
+        // points in the reference's order: chunk by chunk
+        int64_t skip_weak = 0;
+        std::vector<size_t> at(nch + 1, xyz.size());
+        for (int k = 0; k < nch; ++k) {
+            at[k + 1] = at[k] + ch[k].xyz.size();
+            skip_weak += ch[k].skip_weak;
+        }
+        xyz.resize(at[nch]);
+        bgr.resize(at[nch]);
+        par([&](int k) {
+            std::copy(ch[k].xyz.begin(), ch[k].xyz.end(), xyz.begin() + at[k]);
+            std::copy(ch[k].bgr.begin(), ch[k].bgr.end(), bgr.begin() + at[k]);
+        });
         return skip_weak;
     }
 };
@@ -379,7 +498,18 @@ bool run_fusion(const std::vector<Problem> &problems, const FusionOptions &opt, 
     }
     rep.load_ms = ms_since(t0);
 
+    size_t total_px = 0;
+    for (View &v : views) {
+        v.off = total_px;
+        total_px += (size_t)v.depth.cols * v.depth.rows;
+    }
+    if (total_px >= ((size_t)1 << 31)) { err = "fusion: more than 2^31 pixels in the scan"; return false; }
+    std::vector<uint8_t> gmask(total_px, 0);
+    for (View &v : views) v.mask = gmask.data() + v.off;
     Fuser fu(views, problems);
+    fu.xyz.reserve(3 * total_px);  // at most one point per pixel; untouched pages cost nothing
+    fu.bgr.reserve(3 * total_px);
+    fu.threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     fu.ctx = apd_fusion_create(opt.device);
     if (!fu.ctx) { err = std::string("fusion: ") + apd_fusion_last_error(nullptr); return false; }
     struct CtxGuard {
@@ -431,7 +561,9 @@ bool run_fusion(const std::vector<Problem> &problems, const FusionOptions &opt, 
             std::cout << "Fusing image " << std::setw(8) << std::setfill('0') << i << "..." << std::endl;
             std::future<bool> pre;
             if (i + 1 < n) pre = std::async(std::launch::async, [&, i]() { return fu.levels(i + 1, tat_i, qk, nxt); });
+            const auto tc = Clock::now();
             const int64_t sw = fu.commit_tat(i, tat_i, cur);
+            fu.commit_ms += ms_since(tc);
             if (!tat_i) printf("skip_weak: %lld\n", (long long)sw);
             if (pre.valid() && !pre.get()) { err = fu.err; return false; }
             std::swap(cur, nxt);
@@ -444,13 +576,17 @@ bool run_fusion(const std::vector<Problem> &problems, const FusionOptions &opt, 
             std::cout << "Fusing image " << std::setw(8) << std::setfill('0') << i << "..." << std::endl;
             std::future<bool> pre;
             if (i + 1 < n) pre = std::async(std::launch::async, [&, i]() { return fu.consistency(i + 1, q_angle, nxt); });
-            fu.commit_default(i, cur);
+            const auto tc = Clock::now();
+            fu.commit_default(i, cur, gmask.data());
+            fu.commit_ms += ms_since(tc);
             if (pre.valid() && !pre.get()) { err = fu.err; return false; }
             std::swap(cur, nxt);
         }
     }
     rep.fuse_ms = ms_since(t0);
     rep.gpu_ms = fu.gpu_ms;
+    rep.term_ms = fu.term_ms;
+    rep.commit_ms = fu.commit_ms;
 
     t0 = Clock::now();
     write_ply(opt.dense_folder + "/APD/" + opt.name, fu.xyz, fu.bgr, opt.export_color);

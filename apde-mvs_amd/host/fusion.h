@@ -26,7 +26,9 @@ struct FusionOptions {
 struct FusionReport {
     int64_t points = 0;
     double load_ms = 0, upload_ms = 0, filter_ms = 0, fuse_ms = 0, write_ms = 0;
-    double gpu_ms = 0;  // sum of the device calls (kernel + copy) inside filter/fuse
+    double gpu_ms = 0;     // sum of the device calls (kernel + copy) inside filter/fuse
+    double term_ms = 0;    // parallel host evaluation of the candidates' exp terms (RunFusion)
+    double commit_ms = 0;  // sequential ordered commit
 };
 
 // Runs the whole fusion and writes <dense>/APD/<name> (+ APD/<id>/skip.png with the weak filter).

@@ -30,11 +30,15 @@ def main():
     ap.add_argument("--weak_filter", type=int, default=1)
     ap.add_argument("--oracle", action="store_true")
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--scan_only", default="", help="only write the scan into this folder (for rocprofv3 runs)")
     a = ap.parse_args()
-    tmp = tempfile.mkdtemp(prefix="fscan_")
+    tmp = a.scan_only or tempfile.mkdtemp(prefix="fscan_")
     t0 = time.time()
     FL.make_fusion_scan(tmp, a.width, a.height, a.views - 1, seed=3)
     gen_s = time.time() - t0
+    if a.scan_only:
+        print(json.dumps({"scan": tmp, "scan_gen_s": round(gen_s, 2)}))
+        return
     res = dict(workload=f"fusion {a.dataset}, {a.views} views at {a.width}x{a.height}, weak_filter={a.weak_filter}",
                scan_gen_s=round(gen_s, 2))
     walls = []
@@ -48,8 +52,8 @@ def main():
             print(r.stdout[-2000:], r.stderr[-2000:], file=sys.stderr)
             sys.exit(1)
     m = re.search(r"Fusion: (\d+) points, load (\d+) ms, upload (\d+) ms, weak filter (\d+) ms, fuse (\d+) ms "
-                  r"\(device (\d+) ms\), write (\d+) ms", r.stdout)
-    keys = ["points", "load_ms", "upload_ms", "filter_ms", "fuse_ms", "device_ms", "write_ms"]
+                  r"\(device (\d+) ms, terms (\d+) ms, commit (\d+) ms\), write (\d+) ms", r.stdout)
+    keys = ["points", "load_ms", "upload_ms", "filter_ms", "fuse_ms", "device_ms", "terms_ms", "commit_ms", "write_ms"]
     res.update({k: int(v) for k, v in zip(keys, m.groups())})
     res["apd_wall_s"] = round(min(walls), 3)
     px = a.width * a.height * a.views
