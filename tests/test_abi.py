@@ -1,5 +1,6 @@
 """C-ABI boundary checks that need no GPU: libapd_hip.so loads, exports every entry point declared in
-include/apd_hip.h, and the ctypes mirror has the exact C layout (compiled probe with gcc)."""
+include/*.h (apd_hip.h, apd_fusion.h), and the ctypes mirror has the exact C layout (compiled probe
+with gcc)."""
 import ctypes as C
 import os
 import re
@@ -13,10 +14,11 @@ import apd_abi as A
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "apd_hip.h")
+HEADERS = [HEADER, os.path.join(REPO, "include", "apd_fusion.h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
+    src = "".join(open(h).read() for h in HEADERS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(apd_[a-z_]+)\s*\(", src)))
 
@@ -28,7 +30,7 @@ def lib():
 
 def test_every_declared_symbol_is_exported(lib):
     names = declared_functions()
-    assert len(names) >= 15
+    assert len(names) >= 22
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
     assert set(names) == set(A.EXPORTS)
@@ -45,6 +47,8 @@ def test_no_device_is_an_error_not_a_crash(lib):
         assert not lib.apd_create(0)
         assert b"device" in lib.apd_last_error(None)
     assert not lib.apd_create(10_000)
+    assert not lib.apd_fusion_create(10_000)
+    assert b"device" in lib.apd_fusion_last_error(None)
 
 
 def test_struct_layout_matches_header():
@@ -52,12 +56,15 @@ def test_struct_layout_matches_header():
 #include <stdio.h>
 #include <stddef.h>
 #include "apd_hip.h"
+#include "apd_fusion.h"
 #define P(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 int main(void) {
   printf("apd_camera %zu\napd_params %zu\napd_problem %zu\napd_outputs %zu\napd_timing %zu\n",
          sizeof(apd_camera), sizeof(apd_params), sizeof(apd_problem), sizeof(apd_outputs), sizeof(apd_timing));
   P(apd_camera, depth_num) P(apd_params, state) P(apd_params, geom_factor) P(apd_problem, params)
   P(apd_problem, seed) P(apd_problem, sa_mask) P(apd_outputs, reliable_curve) P(apd_timing, iterations)
+  printf("apd_fusion_view %zu\n", sizeof(apd_fusion_view));
+  P(apd_fusion_view, camera) P(apd_fusion_view, depth) P(apd_fusion_view, confidence)
   return 0;
 }
 '''
@@ -81,6 +88,10 @@ int main(void) {
     assert int(got["apd_problem.sa_mask"]) == A.ApdProblem.sa_mask.offset
     assert int(got["apd_outputs.reliable_curve"]) == A.ApdOutputs.reliable_curve.offset
     assert int(got["apd_timing.iterations"]) == A.ApdTiming.iterations.offset
+    assert int(got["apd_fusion_view"]) == C.sizeof(A.ApdFusionView)
+    assert int(got["apd_fusion_view.camera"]) == A.ApdFusionView.camera.offset
+    assert int(got["apd_fusion_view.depth"]) == A.ApdFusionView.depth.offset
+    assert int(got["apd_fusion_view.confidence"]) == A.ApdFusionView.confidence.offset
 
 
 def test_epilogue_matches_process_problem(lib):
