@@ -1173,7 +1173,7 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const WvLds &L, in
 #pragma unroll
             for (int k = 0; k < 9; ++k) Hp.h[k] = (k == 8) ? 1.0f : 0.0f;
         }
-        float vs[NW * NW];
+        const bool acc = live && fast;
 #pragma unroll
         for (int i = 0; i < NW; ++i) {
             const float x = (float)(ax - 5 + INC * i);
@@ -1190,18 +1190,17 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const WvLds &L, in
             }
 #pragma unroll
             for (int j = 0; j < NW; ++j) q[j] = T.load(t[j]);
+            // accumulate column by column, taps in (i, j) order as before
 #pragma unroll
-            for (int j = 0; j < NW; ++j) vs[i * NW + j] = T.finish(t[j], q[j]);
-        }
-        if (live && fast) {
-#pragma unroll
-            for (int tk = 0; tk < NW * NW; ++tk) {
-                if (!((mask >> tk) & 1ull)) continue;
-                const float v = vs[tk];
-                const float r = L.rref[(tap0 + tk) * VM_P + p];
-                ss += v;
-                sss = fmaf(v, v, sss);
-                srs = fmaf(r, v, srs);
+            for (int j = 0; j < NW; ++j) {
+                const int tk = i * NW + j;
+                const float v = T.finish(t[j], q[j]);
+                if (acc && ((mask >> tk) & 1ull)) {
+                    const float r = L.rref[(tap0 + tk) * VM_P + p];
+                    ss += v;
+                    sss = fmaf(v, v, sss);
+                    srs = fmaf(r, v, srs);
+                }
             }
         }
     }
@@ -1315,8 +1314,13 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvLds &L, int p
     return (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
 }
 
+// WvLds + the cost table take ~80 KiB per workgroup at N = 8, so at most 2 workgroups (2 waves per
+// SIMD) fit a CU: allow the 256 VGPRs that occupancy leaves instead of spilling under a 3-wave bound.
+#ifndef VM_WEAK_MINW
+#define VM_WEAK_MINW 2
+#endif
 template <bool F16>
-__global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
+__global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
                                                                 int iter) {
     const int N = a.N, W = a.W;
     WvLds &L = *reinterpret_cast<WvLds *>(apd_dyn_lds);
