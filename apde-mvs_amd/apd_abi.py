@@ -15,7 +15,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "lib", "libapd_hip.so")
+LIB_PATH = os.environ.get("APD_LIB") or os.path.join(HERE, "lib", "libapd_hip.so")  # APD_LIB: A/B tooling
 
 MAX_IMAGES = 32
 ANCHOR_NUM = 9
