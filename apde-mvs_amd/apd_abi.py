@@ -178,7 +178,7 @@ class Outputs:
 EXPORTS = ["apd_abi_version", "apd_device_count", "apd_create", "apd_destroy", "apd_last_error",
            "apd_set_problem", "apd_run_patchmatch", "apd_stage_prepare", "apd_stage_iteration",
            "apd_stage_finish", "apd_synchronize", "apd_get_results", "apd_get_timing", "apd_profile_reset",
-           "apd_profile_query", "apd_epilogue", "apd_fusion_create", "apd_fusion_destroy",
+           "apd_profile_query", "apd_profile_evaluations", "apd_epilogue", "apd_fusion_create", "apd_fusion_destroy",
            "apd_fusion_last_error", "apd_fusion_set_views", "apd_fusion_weak_filter", "apd_fusion_consistency",
            "apd_fusion_tat_levels"]
 
@@ -212,6 +212,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.apd_get_timing.argtypes = [C.c_void_p, C.POINTER(ApdTiming)]
     lib.apd_profile_reset.restype = C.c_int32
     lib.apd_profile_reset.argtypes = [C.c_void_p, C.c_int32]
+    lib.apd_profile_evaluations.restype = C.c_int32
+    lib.apd_profile_evaluations.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     lib.apd_profile_query.restype = C.c_int32
     lib.apd_profile_query.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                       C.POINTER(C.c_int64)]
@@ -348,6 +350,11 @@ class Engine:
         ms, n, px = C.c_double(), C.c_int64(), C.c_int64()
         self._check(self.lib.apd_profile_query(self.ctx, C.byref(ms), C.byref(n), C.byref(px)), "apd_profile_query")
         return ms.value, n.value, px.value
+
+    def profile_evaluations(self) -> int:
+        n = C.c_int64()
+        self._check(self.lib.apd_profile_evaluations(self.ctx, C.byref(n)), "apd_profile_evaluations")
+        return n.value
 
     def close(self):
         if self.ctx:

@@ -80,6 +80,7 @@ struct Args {
     APD_G float *curve;                    // optional H*W*61
     const APD_G short2 *near_offsets;      // 201*201 offsets sorted by (d^2, x, y)
     const APD_G struct Args *self;         // this struct in device memory, for out-of-line callees
+    APD_G unsigned long long *evals;       // profiling only (else null): NCC-Old evaluations issued
 };
 
 // ---------------------------------------------------------------------------------------------

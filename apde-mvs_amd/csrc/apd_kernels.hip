@@ -952,6 +952,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     // tasks whose window needs the out-of-line path are collected in `defer` (bit k = k-th task of
     // this wave) and evaluated after the loop, so the hot loop holds no call.
     uint64_t defer[2] = {0, 0};  // up to 128 tasks per wave (9 * 31 / VM_WAVES)
+    uint32_t issued = 0;         // NCC-Old evaluations of this lane (profiling count, a.evals)
     // tasks in view-major order, one contiguous chunk per wave: consecutive NCCs of a wave read the
     // same source image around the same pixels (L1 reuse); (h, v) -> table index t = h * N + v
     const int c1n = (9 * N + VM_WAVES - 1) / VM_WAVES, u0 = wave * c1n, u1 = min(u0 + c1n, 9 * N);
@@ -966,6 +967,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
         if (pv1 && fh) {
             const float4 pl = L.hyp[h * VM_P + p1];
             bool slow;
+            ++issued;
             val = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, pl, rw, slow);
             if (slow) defer[k >> 6] |= 1ull << (k & 63);
             if (h == 8 && geom_imp) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
@@ -1099,6 +1101,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 #endif
             const float4 tp = L.cand[k * VM_P + p1];
             bool slow;
+            ++issued;
             cv = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, tp, rw, slow);
             if (slow) defer[kt >> 6] |= 1ull << (kt & 63);
             if (geom_imp) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
@@ -1120,6 +1123,13 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
         costL[t * VM_P + p1] = cv;
     }
     __syncthreads();
+
+    if (a.evals) {  // profiling: one atomic per wave
+        uint32_t sum = issued;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+        if (lane == 0) atomicAdd(a.evals, (unsigned long long)sum);
+    }
 
     // ---- P4: weighted candidate costs in view order, acceptance, writes
     if (pv1) {
@@ -2550,7 +2560,7 @@ struct apd_ctx {
     std::string err;
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
-        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs;
+        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals;
     int n_near = 0;
     Args args{};
     bool loaded = false, prepared = false;
@@ -2744,7 +2754,7 @@ void apd_destroy(apd_ctx *ctx) {
     DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
-                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs};
+                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
@@ -3039,9 +3049,11 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             (void)hipEventCreate(&e1);
             (void)hipEventRecord(e0, s);
         }
+        Args ak = a;
+        if (ctx->prof && ctx->evals.p) ak.evals = (APD_G unsigned long long *)ctx->evals.p;
         if (ctx->sweep_vm)
             LAUNCH_TEX(k_sweep_strong_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), vm_lds_bytes(a.N), s,
-                       a, (const int *)list_ptr(ctx, colour), n, iter);
+                       ak, (const int *)list_ptr(ctx, colour), n, iter);
         else
             LAUNCH_TEX(k_sweep_strong, dim3(group_blocks(n, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a,
                        (const int *)list_ptr(ctx, colour), n, iter);
@@ -3180,6 +3192,21 @@ int32_t apd_profile_reset(apd_ctx *ctx, int32_t enable) {
     ctx->prof_ev.clear();
     ctx->prof_pixels = 0;
     ctx->prof = enable != 0;
+    if (ctx->prof) {
+        int st = ensure(ctx, ctx->evals, sizeof(unsigned long long));
+        if (st) return st;
+        HIP_OK(ctx, hipMemsetAsync(ctx->evals.p, 0, sizeof(unsigned long long), ctx->stream));
+    }
+    return APD_OK;
+}
+
+int32_t apd_profile_evaluations(apd_ctx *ctx, int64_t *ncc_evaluations) {
+    if (!ctx || !ncc_evaluations) return APD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+    unsigned long long n = 0;
+    if (ctx->evals.p) HIP_OK(ctx, hipMemcpy(&n, ctx->evals.p, sizeof(n), hipMemcpyDeviceToHost));
+    *ncc_evaluations = (int64_t)n;
     return APD_OK;
 }
 

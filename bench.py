@@ -39,8 +39,10 @@ PEAK_HBM_GBS = 8000.0
 
 
 def strong_evaluations(W: int, H: int, n_src: int, colour: int, row_limit: int) -> int:
-    """NCC-Old evaluations issued by one Strong sweep launch over all non-WEAK pixels of a colour:
-    per pixel (valid adaptive-checkerboard neighbours + current + 5 refinement candidates) x N views."""
+    """Upper bound on the NCC-Old evaluations of one Strong sweep launch over a colour: per pixel
+    (valid adaptive-checkerboard neighbours + current + 5 refinement candidates) x N views. The
+    refinement NCCs of views with sampled weight 0 are skipped by the kernel, so the device count
+    (apd_profile_evaluations) is lower; roofline.achieved uses the device count."""
     ys = np.arange(row_limit)[:, None]
     xs = np.arange(W)[None, :]
     mask = ((xs + ys) & 1) == colour
@@ -151,6 +153,7 @@ def main():
     barrier()
     elapsed = t_end - t_start
     sweep_ms, launches, sweep_px = eng.profile_query()
+    ncc_evals = eng.profile_evaluations()
     eng.profile_reset(False)
     if dist:
         torch, tdist, backend = dist
@@ -162,11 +165,12 @@ def main():
     n_gpus = world if dist else 1
     value = n_gpus * W * H * args.steps / elapsed / 1e6
 
-    # dominant kernel roofline (k_sweep_strong)
+    # dominant kernel roofline (k_sweep_strong): flops of the NCC-Old evaluations the launches actually
+    # issued (counted on the device), per launch; the static upper bound is kept beside it
     hh = H // 2
     row_limit = min(H, 32 * ((hh + 15) // 16))
-    evals_per_iter = strong_evaluations(W, H, N, 0, row_limit) + strong_evaluations(W, H, N, 1, row_limit)
-    flop_per_launch = evals_per_iter / 2 * FLOP_PER_NCC_OLD
+    evals_bound = strong_evaluations(W, H, N, 0, row_limit) + strong_evaluations(W, H, N, 1, row_limit)
+    flop_per_launch = ncc_evals / max(launches, 1) * FLOP_PER_NCC_OLD
     launch_ms = sweep_ms / max(launches, 1)
     achieved_tf = flop_per_launch / (launch_ms * 1e-3) / 1e12
     bytes_per_launch = (W * H / 2) * (4 * (N + 1) + 80)  # = 116 B/px at N=8
@@ -221,6 +225,8 @@ def main():
                                  "peak, which on gfx950 is the same 157.3 TF for VALU and f32 MFMA",
                          "launch_ms": round(launch_ms, 4), "launches": launches,
                          "flop_per_launch": flop_per_launch,
+                         "ncc_evals_per_launch": round(ncc_evals / max(launches, 1)),
+                         "ncc_evals_bound_per_launch": evals_bound // 2,
                          "hbm_algorithmic_gbs": round(bytes_per_launch / (launch_ms * 1e-3) / 1e9, 2),
                          "hbm_peak_gbs": PEAK_HBM_GBS},
             "cpu_baseline": cpu,

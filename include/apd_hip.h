@@ -195,6 +195,10 @@ int32_t apd_get_timing(apd_ctx *ctx, apd_timing *timing);
 int32_t apd_profile_reset(apd_ctx *ctx, int32_t enable);
 int32_t apd_profile_query(apd_ctx *ctx, double *sweep_ms_total, int64_t *sweep_launches,
                           int64_t *sweep_pixels);
+/* NCC-Old evaluations the profiled Strong sweep launches actually issued (counted on the device:
+   valid propagation candidates + current plane + refinement candidates of views with weight > 0),
+   so bench.py prices roofline.achieved on work done, not on an upper bound. */
+int32_t apd_profile_evaluations(apd_ctx *ctx, int64_t *ncc_evaluations);
 
 /* Host epilogue of ProcessProblem (main.cpp:168-178): depth = plane.w clipped to
    [depth_min, depth_max] (else 0 and PixelState UNKNOWN), normal = plane.xyz. Pure host code. */
