@@ -847,16 +847,21 @@ __global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a,
 #define APD_TASK_INTERLEAVE
 #endif
 #define VM_P 64
-struct VmLds {  // static part; the cost table [9][N][64] follows (dynamic)
+#ifndef APD_VM_LDS_PAD
+#define APD_VM_LDS_PAD 0  // experiments: extra LDS bytes per workgroup (fewer workgroups per CU)
+#endif
+// 39.9 KB at N = 8: four workgroups fit a CU's 160 KB of LDS.
+struct VmLds {  // static part; the cost table [9][N][64] and the weights [N][64] (uint8) follow
     float refw[36 * VM_P];       // [k][p]
-    float4 hyp[9 * VM_P];        // [h][p]: 8 propagated + current
-    int npos[8 * VM_P];          // [d][p]: neighbour index, -1 = invalid
-    float4 cand[5 * VM_P];       // [k][p]: refinement candidates (t.w = distance)
+    float4 hyp[9 * VM_P];        // [h][p]: 8 propagated + current; P2 overwrites [0..4] with the
+                                 // refinement candidates (VM_CAND) once the pixel's reads are done
+    uint8_t nval[8 * VM_P];      // [d][p]: neighbour d exists (adaptive-checkerboard scan hit)
     float4 pnow[VM_P];
     float st[4 * VM_P];          // depth_now, cost_now, cost_init, weight_norm
 };
+#define VM_CAND(L) ((L).hyp)     // [k][p], k < 5: refinement candidates (t.w = distance)
 static inline size_t vm_lds_bytes(int N) {
-    return sizeof(VmLds) + (size_t)9 * N * VM_P * sizeof(float) + (size_t)N * VM_P * sizeof(int);
+    return APD_VM_LDS_PAD + sizeof(VmLds) + (size_t)9 * N * VM_P * sizeof(float) + (size_t)N * VM_P;
 }
 
 // One direction of the adaptive checkerboard (APD.cu:1127-1316): d = 2*dir + far, dir in
@@ -913,7 +918,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     const int N = a.N, W = a.W, H = a.H;
     VmLds &L = *reinterpret_cast<VmLds *>(apd_dyn_lds);
     float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64], later [5][N][64]
-    int *wts = reinterpret_cast<int *>(costL + 9 * N * VM_P);            // [N][64]
+    uint8_t *wts = reinterpret_cast<uint8_t *>(costL + 9 * N * VM_P);    // [N][64] view weights
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int first = blk * VM_P;
     const int np = min(VM_P, count - first);
@@ -931,7 +936,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
             const int py = c / W, px = c - py * W;
             for (int d = wave; d < 8; d += VM_WAVES) {
                 const int q = scan_direction(a.cost, d, c, px, py, W, H);
-                L.npos[d * VM_P + p] = q;
+                L.nval[d * VM_P + p] = q >= 0;
                 if (q >= 0) L.hyp[d * VM_P + p] = a.plane[q];
             }
             if (wave == 0) L.hyp[8 * VM_P + p] = a.plane[c];
@@ -963,7 +968,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 #endif
         const int v = u / 9, h = u - 9 * v, t = h * N + v;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;  // float cost_array[8][32] = {2.0f} (APD.cu:1120)
-        const bool fh = h == 8 || L.npos[h * VM_P + p1] >= 0;
+        const bool fh = h == 8 || L.nval[h * VM_P + p1];
         if (pv1 && fh) {
             const float4 pl = L.hyp[h * VM_P + p1];
             bool slow;
@@ -1016,7 +1021,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
             const int nb[4] = {c - W, c + W, c - 1, c + 1};
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                if (L.npos[(2 * i) * VM_P + p] >= 0) prior += ((a.sel[nb[i]] >> v) & 1u) ? 0.9f : 0.1f;
+                if (L.nval[(2 * i) * VM_P + p]) prior += ((a.sel[nb[i]] >> v) & 1u) ? 0.9f : 0.1f;
         }
         Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c, ord_strong(iter));
         const int w = view_selection(ca, prior, iter, rg, G, N);
@@ -1051,7 +1056,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
             float fcm = fc[0];
 #pragma unroll
             for (int k = 1; k < 8; ++k) if (mi == k) fcm = fc[k];
-            if (L.npos[mi * VM_P + p] >= 0) {
+            if (L.nval[mi * VM_P + p]) {
                 const float4 cand = L.hyp[mi * VM_P + p];
                 const float db = depth_from_plane(cam0, cand, px, py);
                 if (db >= a.dmin && db <= a.dmax && fcm < cost_now) {
@@ -1063,14 +1068,14 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
         // PlaneHypothesisRefinementStrong candidates (APD.cu:950-980)
         const Cands C = refine_candidates(a, px, py, rg, pnow, depth_now);
         if (G.valid) {
-            wts[v * VM_P + p] = w;
+            wts[v * VM_P + p] = (uint8_t)w;
             if (G.v == 0) {
 #pragma unroll 1
                 for (int k = 0; k < 5; ++k) {
                     float dk;
                     float4 t = candidate(C, k, pnow, depth_now, dk);
                     t.w = dist2origin(cam0, px, py, dk, t);
-                    L.cand[k * VM_P + p] = t;
+                    VM_CAND(L)[k * VM_P + p] = t;
                 }
                 L.pnow[p] = pnow;
                 L.st[0 * VM_P + p] = depth_now;
@@ -1099,7 +1104,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 #else
         if (pv1 && wts[v * VM_P + p1] > 0) {
 #endif
-            const float4 tp = L.cand[k * VM_P + p1];
+            const float4 tp = VM_CAND(L)[k * VM_P + p1];
             bool slow;
             ++issued;
             cv = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, tp, rw, slow);
@@ -1117,7 +1122,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 #else
         const int u = w0 + kt, v = u / 5, k = u - 5 * v, t = k * N + v;
 #endif
-        const float4 tp = L.cand[k * VM_P + p1];
+        const float4 tp = VM_CAND(L)[k * VM_P + p1];
         float cv = ncc_old_slow<F16>(a.self, px1, py1, v + 1, tp, rw.r, VM_P, rw.mean, rw.var);
         if (geom_imp) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
         costL[t * VM_P + p1] = cv;
@@ -1141,7 +1146,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
             float4 pnow = L.pnow[p];
 #pragma unroll 1
             for (int k = 0; k < 5; ++k) {
-                const float4 t = L.cand[k * VM_P + p];
+                const float4 t = VM_CAND(L)[k * VM_P + p];
                 float tc = 0.0f;
                 for (int kk = 0; kk < N; ++kk) tc = fmaf((float)wts[kk * VM_P + p], costL[(k * N + kk) * VM_P + p], tc);
                 tc /= wn;
