@@ -1177,24 +1177,31 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 //   P5  (candidate, view) tasks for views with weight > 0
 //   P6  lane = pixel: acceptance, writes
 // ---------------------------------------------------------------------------------------------
-struct WvLds {
-    float rref[108 * VM_P];      // [tap][p]: window 0 taps 0..35 (6x6, step 2), anchor k taps 36+9(k-1).. (3x3, step 5)
-    float wsr[9 * VM_P], wsrr[9 * VM_P], wsum[9 * VM_P];  // per window moments over its valid taps
-    uint64_t tmask0[VM_P];       // SA tap masks (all ones without SA)
-    uint32_t tmask[8 * VM_P];
-    int anc[9 * VM_P];           // packed (x, y) of anchors 0..8, -1 = none
-    uint32_t awin[VM_P];         // bit k: window k is evaluated (anchor present and SA label matches)
-    float4 hyp[9 * VM_P];        // [h][p]: anchor planes 1..8 (if STRONG) + current
-    int npos[8 * VM_P];          // anchor pixel index (or -1)
-    uint32_t hflag[VM_P];        // bit h: hypothesis h present (anchor STRONG)
-    float4 fit[VM_P];
-    float4 cand[5 * VM_P];
+// 52.2 KiB with the cost table at N = 8 (fp16 reference taps): three workgroups per CU.
+template <bool F16>
+struct WvLdsT {
+    float4 hyp[9 * VM_P];        // [h][p]: anchor planes 1..8 (if STRONG) + current; P4 overwrites [0..4]
+                                 // with the refinement candidates (WV_CAND) after P2's last read
     float4 pnow[VM_P];
-    float st[5 * VM_P];          // depth_now, cost_now, cost_init, weight norm, refine (fit normal != 0)
-    uint32_t rng_n[VM_P];
+    uint64_t tmask0[VM_P];       // SA tap masks (all ones without SA)
+    float wsr[9 * VM_P], wsrr[9 * VM_P];  // per window moments over its valid taps
+    int anc[9 * VM_P];           // packed (x, y) of anchors 0..8, -1 = none
+    float st[4 * VM_P];          // depth_now, cost_now, cost_init, weight norm
+    uint32_t flags[VM_P];        // bits 0-8: hypothesis h present (anchor STRONG); 16-24: window k evaluated
+                                 // (anchor present and SA label matches); 31: refine (fit normal != 0)
+    // [tap][p]: window 0 taps 0..35 (6x6, step 2), anchor k taps 36+9(k-1).. (3x3, step 5); fp16 when
+    // the images are (exactly) fp16-representable, see apd_set_problem
+    typename std::conditional<F16, _Float16, float>::type rref[108 * VM_P];
+    uint16_t tmask[8 * VM_P];
+    uint16_t rng_n[VM_P];
+    uint8_t wsum[9 * VM_P];      // valid taps per window (<= 36)
 };
+#define WV_CAND(L) ((L).hyp)
+static_assert(sizeof(WvLdsT<true>) + 9 * 8 * VM_P * sizeof(float) + 8 * VM_P <= 53 * 1024,
+              "k_sweep_weak_vm at N = 8 must fit three workgroups per CU (160 KiB LDS)");
+template <bool F16>
 static inline size_t wv_lds_bytes(int N) {
-    return sizeof(WvLds) + (size_t)9 * N * VM_P * sizeof(float) + (size_t)N * VM_P * sizeof(int);
+    return sizeof(WvLdsT<F16>) + (size_t)9 * N * VM_P * sizeof(float) + (size_t)N * VM_P;
 }
 __device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
     const long idx = (long)y * a.W + x;
@@ -1207,7 +1214,7 @@ __device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
 // statement. Every lane of the wave executes the same instruction stream; lanes that do not need
 // this window (`live` false) run on a parked homography and discard the sums.
 template <bool F16, int NW, int INC>
-__device__ __forceinline__ void ncc_new_window(const Args &a, const WvLds &L, int p, int tap0, uint64_t mask,
+__device__ __forceinline__ void ncc_new_window(const Args &a, const WvLdsT<F16> &L, int p, int tap0, uint64_t mask,
                                                const Hom &Hm, int ax, int ay, bool live, bool fast,
                                                const FastTex<F16, true> &T, const SrcTex<F16> &Q, float &ss,
                                                float &sss, float &srs) {
@@ -1280,7 +1287,7 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const WvLds &L, in
 // view s, plane pl, with the reference side from WvLds. Called by every lane of the wave (converged);
 // `want` = the lane evaluates this task. Same operations, in the same order, as ncc_new.
 template <bool F16>
-__device__ __forceinline__ float ncc_new_vm(const Args &a, const WvLds &L, int p, int px, int py, int s, float4 pl,
+__device__ __forceinline__ float ncc_new_vm(const Args &a, const WvLdsT<F16> &L, int p, int px, int py, int s, float4 pl,
                                             bool want) {
     const int W = a.W, H = a.H;
     const Hom Hm = homography(a, s, pl);
@@ -1289,7 +1296,7 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvLds &L, int p
     bool alive = want && !(ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f);
     const FastTex<F16, true> T(a, s);
     const SrcTex<F16> Q(a, s);
-    const uint32_t awin = L.awin[p];
+    const uint32_t awin = (L.flags[p] >> 16) & 0x1FFu;
     float sc[9];
     int ns = 0;
     float center_cost = 0.0f, strong_weight = 0.0f;
@@ -1327,7 +1334,7 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvLds &L, int p
             ncc_new_window<F16, 3, 5>(a, L, p, 36 + 9 * (k - 1), (uint64_t)L.tmask[(k - 1) * VM_P + p], Hm, ax, ay,
                                       live, fast, T, Q, ss, sss, srs);
         if (!live) continue;
-        const float wsum = L.wsum[k * VM_P + p];
+        const float wsum = (float)L.wsum[k * VM_P + p];
         if (wsum == 0.0f) continue;
         const float c = ncc_finalize(L.wsr[k * VM_P + p], L.wsrr[k * VM_P + p], ss, sss, srs, wsum);
         if (k == 0) {
@@ -1359,18 +1366,18 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvLds &L, int p
     return (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
 }
 
-// WvLds + the cost table take ~80 KiB per workgroup at N = 8, so at most 2 workgroups (2 waves per
-// SIMD) fit a CU: allow the 256 VGPRs that occupancy leaves instead of spilling under a 3-wave bound.
+// WvLdsT + the cost table take 52 KiB per workgroup at N = 8 (fp16 reference taps): 3 workgroups per
+// CU; the kernel needs ~110 VGPRs, well inside the 3-wave budget.
 #ifndef VM_WEAK_MINW
-#define VM_WEAK_MINW 2
+#define VM_WEAK_MINW 3
 #endif
 template <bool F16>
 __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
                                                                 int iter) {
     const int N = a.N, W = a.W;
-    WvLds &L = *reinterpret_cast<WvLds *>(apd_dyn_lds);
+    WvLdsT<F16> &L = *reinterpret_cast<WvLdsT<F16> *>(apd_dyn_lds);
     float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64], later [5][N][64]
-    int *wts = reinterpret_cast<int *>(costL + 9 * N * VM_P);            // [N][64]
+    uint8_t *wts = reinterpret_cast<uint8_t *>(costL + 9 * N * VM_P);    // [N][64] view weights
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int first = blk * VM_P;
     const int np = min(VM_P, count - first);
@@ -1398,17 +1405,14 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
                 if (ok && !(use_sa && sa_at_dev(a, ap.x, ap.y) != cid)) awin |= 1u << k;
                 if (k >= 1) {
                     const int q = ok ? ap.x + ap.y * W : -1;
-                    L.npos[(k - 1) * VM_P + p1] = q;
                     if (ok && a.weak[q] == APD_STRONG) {
                         hflag |= 1u << (k - 1);
                         L.hyp[(k - 1) * VM_P + p1] = a.plane[q];
                     }
                 }
             }
-            L.hflag[p1] = hflag;
-            L.awin[p1] = awin;
+            L.flags[p1] = hflag | (awin << 16);
             L.hyp[8 * VM_P + p1] = a.plane[c1];
-            L.fit[p1] = a.fit[c1];
         }
         // reference windows: wave w builds windows w, w + VM_WAVES, ... (tap order = the reference's)
         for (int k = wave; k < 9; k += VM_WAVES) {
@@ -1436,9 +1440,9 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
                 }
             L.wsr[k * VM_P + p1] = sr;
             L.wsrr[k * VM_P + p1] = srr;
-            L.wsum[k * VM_P + p1] = ws;
+            L.wsum[k * VM_P + p1] = (uint8_t)ws;
             if (k == 0) L.tmask0[p1] = mask;
-            else L.tmask[(k - 1) * VM_P + p1] = (uint32_t)mask;
+            else L.tmask[(k - 1) * VM_P + p1] = (uint16_t)mask;
         }
     }
     __syncthreads();
@@ -1452,7 +1456,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         const int h = t / N, v = t - h * N;
 #endif
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
-        const bool want = pv1 && (h == 8 || ((L.hflag[p1] >> h) & 1u));
+        const bool want = pv1 && (h == 8 || ((L.flags[p1] >> h) & 1u));
         const float4 pl = L.hyp[h * VM_P + p1];
         const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want);
         if (want) {
@@ -1479,12 +1483,12 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         const int p = min(pr, np - 1);
         const int c = list[first + p];
         const int py = c / W, px = c - py * W;
-        const uint32_t hflag = L.hflag[p];
+        const uint32_t hflag = L.flags[p] & 0x1FFu;
         float prior = 0.0f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const int q = L.npos[i * VM_P + p];
-            if (q >= 0) prior += ((a.sel[q] >> v) & 1u) ? 0.9f : 0.1f;
+            const int pk = L.anc[(i + 1) * VM_P + p];  // anchor i+1's pixel, if any
+            if (pk >= 0) prior += ((a.sel[(pk & 0xFFFF) + (pk >> 16) * W] >> v) & 1u) ? 0.9f : 0.1f;
         }
         float ca[8];
 #pragma unroll
@@ -1545,27 +1549,28 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             }
         }
         if (G.valid) {
-            wts[v * VM_P + p] = w;
+            wts[v * VM_P + p] = (uint8_t)w;
             if (G.v == 0) {
-                const float4 fit = L.fit[p];
+                const float4 fit = a.fit[c];
                 L.pnow[p] = pnow;
                 L.st[0 * VM_P + p] = depth_now;
                 L.st[1 * VM_P + p] = cost_now;
                 L.st[2 * VM_P + p] = cost_init;
                 L.st[3 * VM_P + p] = wn;
-                L.st[4 * VM_P + p] = (fit.x == 0 && fit.y == 0 && fit.z == 0) ? 0.0f : 1.0f;
-                L.rng_n[p] = rg.n;
+                if (!(fit.x == 0 && fit.y == 0 && fit.z == 0)) L.flags[p] |= 1u << 31;
+                L.rng_n[p] = (uint16_t)rg.n;  // a few dozen draws
             }
         }
     }
     __syncthreads();
-    const bool refine = pv1 && L.st[4 * VM_P + p1] != 0.0f;
+    const bool refine = pv1 && (L.flags[p1] >> 31) != 0u;
+    const float4 fit1 = a.fit[c1];
 
     // ---- P3: fit-plane tasks (views with weight > 0)
     for (int v = wave; v < N; v += VM_WAVES) {
         float cv = 0.0f;
         const bool want = refine && wts[v * VM_P + p1] > 0;
-        const float4 fit = L.fit[p1];
+        const float4 fit = fit1;
         const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, fit, want);
         if (want) {
             cv = nv;
@@ -1580,7 +1585,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         const float wn = L.st[3 * VM_P + p1];
         float depth_now = L.st[0 * VM_P + p1], cost_now = L.st[1 * VM_P + p1];
         float4 pnow = L.pnow[p1];
-        const float4 fit = L.fit[p1];
+        const float4 fit = fit1;
         float tc = 0.0f;
         for (int kk = 0; kk < N; ++kk) {
             const int wk = wts[kk * VM_P + p1];
@@ -1597,7 +1602,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             float dk;
             float4 t = candidate(C, k, pnow, depth_now, dk);
             t.w = dist2origin(cam0, px1, py1, dk, t);
-            L.cand[k * VM_P + p1] = t;
+            WV_CAND(L)[k * VM_P + p1] = t;
         }
         L.pnow[p1] = pnow;
         L.st[0 * VM_P + p1] = depth_now;
@@ -1615,7 +1620,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
 #endif
         float cv = 0.0f;
         const bool want = refine && wts[v * VM_P + p1] > 0;
-        const float4 tp = L.cand[k * VM_P + p1];
+        const float4 tp = WV_CAND(L)[k * VM_P + p1];
         const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, tp, want);
         if (want) {
             cv = nv;
@@ -1634,7 +1639,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             float4 pnow = L.pnow[p1];
             if (refine) {
                 for (int k = 0; k < 5; ++k) {
-                    const float4 t = L.cand[k * VM_P + p1];
+                    const float4 t = WV_CAND(L)[k * VM_P + p1];
                     float tc = 0.0f;
                     for (int kk = 0; kk < N; ++kk) {
                         const int wk = wts[kk * VM_P + p1];
@@ -2793,7 +2798,7 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     // [0, 256) (8-bit images and their INTER_LINEAR 2^-k downscales are): such texels AND their
     // horizontal differences are exact in fp16 (FastTex::sample relies on both). Else fp32 quads.
     bool tex_f16 = getenv("APD_TEX_F32") == nullptr;
-    for (int i = 1; i < NI && tex_f16; ++i) {
+    for (int i = 0; i < NI && tex_f16; ++i) {  // the reference too: k_sweep_weak_vm keeps its taps in fp16
         const float *img = pb->images[i];
         if (!img) break;
         for (size_t k = 0; k < (size_t)W * H; ++k) {
@@ -3075,7 +3080,7 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             const int n = ctx->cnt[2 + colour];
             if (n <= 0) continue;
             if (ctx->sweep_vm)
-                LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), wv_lds_bytes(a.N), s,
+                LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N) : wv_lds_bytes<false>(a.N)), s,
                            a, (const int *)list_ptr(ctx, 2 + colour), n, iter);
             else
                 LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
