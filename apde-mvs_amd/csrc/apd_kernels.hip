@@ -96,6 +96,16 @@ __global__ __launch_bounds__(BLOCK) void k_build_quads(const float *__restrict__
     }
 }
 
+// *flag = 0 unless every value is a quarter-integer in [0, 256) (the fp16 texel condition)
+__global__ __launch_bounds__(BLOCK) void k_check_f16(const float *__restrict__ imgs, size_t n, int *flag) {
+    bool ok = true;
+    for (size_t i = blockIdx.x * (size_t)BLOCK + threadIdx.x; i < n; i += (size_t)gridDim.x * BLOCK) {
+        const float q = imgs[i] * 4.0f;
+        ok = ok && (q >= 0.0f && q < 1024.0f) && q == (float)(int)q;
+    }
+    if (!ok) *flag = 0;
+}
+
 // Source images -> fp16 vertical pairs P[(iy+1)*(W+2)+(ix+1)] = {half T(ix,iy), half T(ix,iy+1)},
 // ix in [-1, W], iy in [-1, H-1], clamp-to-edge (see SrcTex in apd_device.h).
 __global__ __launch_bounds__(BLOCK) void k_build_pairs(const float *__restrict__ imgs, uint32_t *__restrict__ pairs,
@@ -2794,21 +2804,34 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     if ((P.geom_consistency || P.use_APD) && !pb->depths) { ctx->err = "depth maps required (geom/APD)"; return APD_EINVAL; }
     const int N = NI - 1;
     const size_t HW = (size_t)W * H;
-    // source texel storage: fp16 vertical pairs when every source texel is a quarter-integer in
-    // [0, 256) (8-bit images and their INTER_LINEAR 2^-k downscales are): such texels AND their
-    // horizontal differences are exact in fp16 (FastTex::sample relies on both). Else fp32 quads.
+    int st;
+    hipStream_t s = ctx->stream;
+    if ((st = ensure(ctx, ctx->imgs, HW * NI * sizeof(float)))) return st;
+    if ((st = ensure(ctx, ctx->totals, 8 * sizeof(int)))) return st;
+    for (int i = 0; i < NI; ++i) {
+        if (!pb->images[i]) { ctx->err = "null image pointer"; return APD_EINVAL; }
+        HIP_OK(ctx, hipMemcpyAsync((float *)ctx->imgs.p + HW * i, pb->images[i], HW * sizeof(float),
+                                   hipMemcpyHostToDevice, s));
+    }
+    // source texel storage: fp16 vertical pairs when every texel -- the reference's too, whose taps
+    // k_sweep_weak_vm keeps in fp16 -- is a quarter-integer in [0, 256) (8-bit images and their
+    // INTER_LINEAR 2^-k downscales are): such texels AND their horizontal differences are exact in
+    // fp16 (FastTex::sample relies on both). Else fp32 quads. Checked on the device (one flag read).
     bool tex_f16 = getenv("APD_TEX_F32") == nullptr;
-    for (int i = 0; i < NI && tex_f16; ++i) {  // the reference too: k_sweep_weak_vm keeps its taps in fp16
-        const float *img = pb->images[i];
-        if (!img) break;
-        for (size_t k = 0; k < (size_t)W * H; ++k) {
-            const float q = img[k] * 4.0f;
-            if (!(q >= 0.0f && q < 1024.0f) || q != (float)(int)q) { tex_f16 = false; break; }
-        }
+    if (tex_f16) {
+        int *flag = (int *)ctx->totals.p + 7;
+        const int one = 1;
+        HIP_OK(ctx, hipMemcpyAsync(flag, &one, sizeof(int), hipMemcpyHostToDevice, s));
+        const size_t n = HW * NI;
+        hipLaunchKernelGGL(k_check_f16, dim3((unsigned)std::min<size_t>(blocks_for(n, BLOCK), 8192)), dim3(BLOCK), 0, s,
+                           (const float *)ctx->imgs.p, n, flag);
+        if ((st = check_launch(ctx, "k_check_f16"))) return st;
+        int ok = 0;
+        HIP_OK(ctx, hipMemcpyAsync(&ok, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIP_OK(ctx, hipStreamSynchronize(s));
+        tex_f16 = ok != 0;
     }
     const size_t qstride = tex_f16 ? (size_t)(W + 2) * (H + 1) : (size_t)(W + 1) * (H + 1);
-    int st;
-    if ((st = ensure(ctx, ctx->imgs, HW * NI * sizeof(float)))) return st;
     if ((st = ensure(ctx, ctx->quad, qstride * N * (tex_f16 ? sizeof(uint32_t) : sizeof(float4))))) return st;
     if ((st = ensure(ctx, ctx->views, NI * sizeof(SrcView)))) return st;
     if ((st = ensure(ctx, ctx->cams, NI * sizeof(Cam)))) return st;
@@ -2824,15 +2847,8 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     const size_t units = std::max<size_t>((size_t)H, (size_t)(W + 3) / 4 * ((H + 3) / 4));  // any tile shape
     if ((st = ensure(ctx, ctx->rowcnt, units * sizeof(int)))) return st;
     if ((st = ensure(ctx, ctx->rowoff, units * sizeof(int)))) return st;
-    if ((st = ensure(ctx, ctx->totals, 8 * sizeof(int)))) return st;
     const bool need_depth = P.geom_consistency || P.use_APD;
     if (need_depth && (st = ensure(ctx, ctx->depth, HW * NI * sizeof(float)))) return st;
-    hipStream_t s = ctx->stream;
-    for (int i = 0; i < NI; ++i) {
-        if (!pb->images[i]) { ctx->err = "null image pointer"; return APD_EINVAL; }
-        HIP_OK(ctx, hipMemcpyAsync((float *)ctx->imgs.p + HW * i, pb->images[i], HW * sizeof(float),
-                                   hipMemcpyHostToDevice, s));
-    }
     if (need_depth) {
         for (int i = 0; i < NI; ++i) {
             if (!pb->depths[i]) { ctx->err = "null depth pointer"; return APD_EINVAL; }

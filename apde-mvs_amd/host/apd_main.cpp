@@ -23,6 +23,7 @@
 #include <iomanip>
 #include <iostream>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <sstream>
 #include <string>
@@ -154,6 +155,74 @@ struct Job {
     long used_ms = 0;
 };
 
+// Decoded and rescaled images shared by every problem of the run. The reference decodes and
+// resizes all N+1 images again for each problem of each pass (APD.cpp:508-590): a 9-view 3024x2016
+// scan spent 41 of its 93 s there. Here each file is decoded once and each (file, scale, size)
+// resized once; the pixels are the ones the per-problem path produces (same decoder, same resize).
+struct ImageCache {
+    struct Decoded {
+        std::once_flag once;
+        bool ok = false;
+        Gray8 g;
+    };
+    struct Scaled {
+        std::once_flag once;
+        std::vector<float> img;
+        int w = 0, h = 0;
+    };
+    std::mutex mu;
+    std::map<std::string, std::shared_ptr<Decoded>> decoded;
+    std::map<std::string, std::shared_ptr<Scaled>> scaled;
+
+    std::shared_ptr<Decoded> decode(const std::string &path) {
+        std::shared_ptr<Decoded> e;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto &slot = decoded[path];
+            if (!slot) slot = std::make_shared<Decoded>();
+            e = slot;
+        }
+        std::call_once(e->once, [&] {
+            std::string err;
+            e->ok = read_gray8(path, e->g, err);
+            if (!e->ok) SAY("Error opening file: \"" << path << "\" (" << err << ")");
+        });
+        return e;
+    }
+    // convertTo(CV_32FC1) of the file, resized with INTER_LINEAR to round(src * 1/scale) when
+    // scale != 1, src_w x src_h being the size the reference resizes from (the ref image's, APD.cpp:567)
+    std::shared_ptr<Scaled> image(const std::string &path, int scale, int src_w, int src_h, const Gray8 &g) {
+        const std::string key = path + "|" + std::to_string(scale) + "|" + std::to_string(src_w) + "x" + std::to_string(src_h);
+        std::shared_ptr<Scaled> e;
+        {
+            std::lock_guard<std::mutex> l(mu);
+            auto &slot = scaled[key];
+            if (!slot) slot = std::make_shared<Scaled>();
+            e = slot;
+        }
+        std::call_once(e->once, [&] {
+            std::vector<float> f(g.px.size());
+            for (size_t i = 0; i < g.px.size(); ++i) f[i] = (float)g.px[i];
+            if (scale == 1) {
+                e->img.swap(f);
+                e->w = g.width;
+                e->h = g.height;
+                return;
+            }
+            const float factor = 1.0f / (float)scale;
+            e->w = (int)std::round(src_w * factor);
+            e->h = (int)std::round(src_h * factor);
+            e->img.resize((size_t)e->w * e->h);
+            resize_linear_f32(f.data(), src_w, src_h, e->img.data(), e->w, e->h);
+        });
+        return e;
+    }
+    void drop_scaled() {  // a new round: the previous scale is not used again
+        std::lock_guard<std::mutex> l(mu);
+        scaled.clear();
+    }
+};
+
 struct Pending {  // Jacobi ordering: outputs committed at the end of the pass
     std::string path;
     Mat mat;
@@ -165,6 +234,7 @@ struct Driver {
     uint64_t seed = 24301;
     bool jacobi = false;
     MatStore *store = nullptr;
+    ImageCache images;
     std::mutex pend_mu;
     std::vector<Pending> pending;
 
@@ -185,42 +255,31 @@ struct Driver {
     bool process(apd_ctx *ctx, Job &job);
 };
 
-bool load_image(const std::string &path, std::vector<float> &img, int &w, int &h) {
-    Gray8 g;
-    std::string err;
-    if (!read_gray8(path, g, err)) {
-        SAY("Error opening file: \"" << path << "\" (" << err << ")");
-        return false;
-    }
-    w = g.width;
-    h = g.height;
-    img.resize(g.px.size());
-    for (size_t i = 0; i < g.px.size(); ++i) img[i] = (float)g.px[i];  // convertTo(CV_32FC1)
-    return true;
-}
-
 bool Driver::process(apd_ctx *ctx, Job &job) {
     const Problem &pb = job.pb;
     const std::string result_folder = dense + "/APD/" + format_index(pb.ref_image_id);
     SAY("Processing image: " << format_index(pb.ref_image_id) << "...");
     const auto start = std::chrono::steady_clock::now();
-    // ---- images (APD.cpp:508-533)
-    std::vector<std::vector<float>> images;
+    // ---- images (APD.cpp:508-533), decoded once per run (ImageCache)
     std::vector<int> ids{pb.ref_image_id};
     ids.insert(ids.end(), pb.src_image_ids.begin(), pb.src_image_ids.end());
-    int width = 0, height = 0;
+    std::vector<std::shared_ptr<ImageCache::Decoded>> dec;
     for (size_t i = 0; i < ids.size(); ++i) {
-        std::vector<float> img;
-        int w, h;
-        if (!load_image(dense + "/images/" + format_index(ids[i]) + pb.img_ext, img, w, h)) return false;
-        if (i == 0) { width = w; height = h; }
-        images.push_back(std::move(img));
+        dec.push_back(images.decode(dense + "/images/" + format_index(ids[i]) + pb.img_ext));
+        if (!dec.back()->ok) return false;
     }
-    if (images.size() > APD_MAX_IMAGES) {
-        SAY("Can't process so much images: " << images.size());
+    int width = dec[0]->g.width, height = dec[0]->g.height;
+    for (size_t i = 1; i < dec.size(); ++i)
+        if (dec[i]->g.width != width || dec[i]->g.height != height) {
+            SAY("Image size mismatch: " << format_index(ids[i]) << " is " << dec[i]->g.width << "x" << dec[i]->g.height
+                                        << ", the reference image " << width << "x" << height);
+            return false;
+        }
+    if (dec.size() > APD_MAX_IMAGES) {
+        SAY("Can't process so much images: " << dec.size());
         exit(EXIT_FAILURE);
     }
-    const int NI = (int)images.size();
+    const int NI = (int)dec.size();
     // ---- cameras (APD.cpp:536-556)
     std::vector<apd_camera> cams(NI);
     for (int i = 0; i < NI; ++i) {
@@ -241,24 +300,22 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
         std::cout << "Depth range: " << P.depth_min << " " << P.depth_max << std::endl;
         std::cout << "Num images: " << P.num_images << std::endl;
     }
-    // ---- scale (APD.cpp:562-590)
-    if (job.scale_size != 1) {
-        for (int i = 0; i < NI; ++i) {
-            const float factor = 1.0f / (float)job.scale_size;
-            const int src_w = (i == 0) ? width : cams[i].width, src_h = (i == 0) ? height : cams[i].height;
-            const int new_cols = (int)std::round(src_w * factor);
-            const int new_rows = (int)std::round(src_h * factor);
-            const float scale_x = new_cols / (float)src_w, scale_y = new_rows / (float)src_h;
-            std::vector<float> dst((size_t)new_cols * new_rows);
-            resize_linear_f32(images[i].data(), src_w, src_h, dst.data(), new_cols, new_rows);
-            images[i].swap(dst);
+    // ---- scale (APD.cpp:562-590): every image is resized from the reference's size
+    std::vector<std::shared_ptr<ImageCache::Scaled>> scaled;
+    for (int i = 0; i < NI; ++i) {
+        scaled.push_back(images.image(dense + "/images/" + format_index(ids[i]) + pb.img_ext, job.scale_size, width,
+                                      height, dec[i]->g));
+        if (job.scale_size != 1) {
+            const float scale_x = scaled[i]->w / (float)width, scale_y = scaled[i]->h / (float)height;
             cams[i].K[0] *= scale_x;
             cams[i].K[2] *= scale_x;
             cams[i].K[4] *= scale_y;
             cams[i].K[5] *= scale_y;
-            cams[i].width = new_cols;
-            cams[i].height = new_rows;
+            cams[i].width = scaled[i]->w;
+            cams[i].height = scaled[i]->h;
         }
+    }
+    if (job.scale_size != 1) {
         width = cams[0].width;
         height = cams[0].height;
         SAY("Scale images and cameras done");
@@ -322,7 +379,7 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     }
     // ---- device (CudaSpaceInitialization + RunPatchMatch)
     std::vector<const float *> img_ptrs(NI), dep_ptrs(NI);
-    for (int i = 0; i < NI; ++i) img_ptrs[i] = images[i].data();
+    for (int i = 0; i < NI; ++i) img_ptrs[i] = scaled[i]->img.data();
     for (size_t i = 0; i < depths.size(); ++i) dep_ptrs[i] = depths[i].ptr<float>();
     apd_problem prob{};
     prob.width = width;
@@ -373,7 +430,7 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     }
     st = apd_get_results(ctx, &out);
     if (st != APD_OK) { SAY("apd_get_results failed: " << apd_last_error(ctx)); return false; }
-    if (!(P.geom_consistency || P.use_APD)) memset(confidence.data.data(), 1, confidence.data.size());
+    if (!(P.geom_consistency || P.use_APD)) memset(confidence.bytes(), 1, confidence.size_bytes());
     apd_epilogue(width, height, planes.data(), P.depth_min, P.depth_max, depth.ptr<float>(), normal.ptr<float>(),
                  states.ptr<uint8_t>());
     // ---- exports (APD.cu:2614-2626, 2649-2660); written immediately, they are not priors
@@ -583,6 +640,7 @@ int main(int argc, char **argv) {
     const int geom_iteration = 3;
     const auto start = std::chrono::steady_clock::now();
     for (int i = 0; i < round_num && ok; ++i) {
+        drv.images.drop_scaled();  // each round uses one scale
         std::cout << "========================== Round " << i << " ==========================" << std::endl;
         std::cout << "======== iteration " << iteration_index << "========" << std::endl;
         for (auto &job : jobs) {

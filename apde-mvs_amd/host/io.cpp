@@ -26,7 +26,7 @@ int cv_elem_size(int type) {
 
 Mat resize_nearest(const Mat &m, int w, int h) {
     Mat o(h, w, m.type);
-    resize_nearest(m.data.data(), m.cols, m.rows, o.data.data(), w, h, cv_elem_size(m.type));
+    resize_nearest(m.bytes(), m.cols, m.rows, o.bytes(), w, h, cv_elem_size(m.type));
     return o;
 }
 
@@ -39,7 +39,7 @@ bool read_binmat_file(const std::string &path, Mat &m) {
     const int es = cv_elem_size(hdr[3]);
     if (es == 0 || hdr[1] < 0 || hdr[2] < 0) return false;
     m = Mat(hdr[1], hdr[2], hdr[3]);
-    in.read(reinterpret_cast<char *>(m.data.data()), (std::streamsize)m.data.size());
+    in.read(reinterpret_cast<char *>(m.bytes()), (std::streamsize)m.size_bytes());
     return (bool)in;
 }
 
@@ -48,7 +48,7 @@ bool write_binmat_file(const std::string &path, const Mat &m) {
     if (!out) return false;
     const int32_t hdr[4] = {1, m.rows, m.cols, m.type};
     out.write(reinterpret_cast<const char *>(hdr), sizeof(hdr));
-    out.write(reinterpret_cast<const char *>(m.data.data()), (std::streamsize)m.data.size());
+    out.write(reinterpret_cast<const char *>(m.bytes()), (std::streamsize)m.size_bytes());
     return (bool)out;
 }
 

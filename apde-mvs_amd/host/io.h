@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -17,13 +18,20 @@ namespace apdhost {
 enum { CV_8UC1 = 0, CV_32SC1 = 4, CV_32FC1 = 5, CV_32FC3 = 21 };
 int cv_elem_size(int type);
 
+// Pixels are reference-counted like a cv::Mat's: copying a Mat (MemoryCache reads and writes,
+// priors) shares the buffer instead of copying hundreds of MB per problem. Every writer fills a
+// freshly constructed Mat, so sharing never exposes a partial write.
 struct Mat {
     int rows = 0, cols = 0, type = CV_8UC1;
-    std::vector<uint8_t> data;  // row-major, rows * cols * elem bytes
+    std::shared_ptr<std::vector<uint8_t>> buf;  // row-major, rows * cols * elem bytes
     Mat() = default;
-    Mat(int r, int c, int t) : rows(r), cols(c), type(t), data((size_t)r * c * cv_elem_size(t)) {}
-    template <class T> T *ptr() { return reinterpret_cast<T *>(data.data()); }
-    template <class T> const T *ptr() const { return reinterpret_cast<const T *>(data.data()); }
+    Mat(int r, int c, int t)
+        : rows(r), cols(c), type(t), buf(std::make_shared<std::vector<uint8_t>>((size_t)r * c * cv_elem_size(t))) {}
+    uint8_t *bytes() { return buf ? buf->data() : nullptr; }
+    const uint8_t *bytes() const { return buf ? buf->data() : nullptr; }
+    size_t size_bytes() const { return buf ? buf->size() : 0; }
+    template <class T> T *ptr() { return reinterpret_cast<T *>(bytes()); }
+    template <class T> const T *ptr() const { return reinterpret_cast<const T *>(bytes()); }
     bool empty() const { return rows == 0 || cols == 0; }
 };
 Mat resize_nearest(const Mat &m, int w, int h);

@@ -1,0 +1,32 @@
+"""Whole-scan timing of the `apd` binary (main.cpp's round schedule) on a synthetic scan written as
+JPEG images (ETH3D ships JPEG): wall time vs the summed "RunPatchMatch time" lines = host overhead
+(decode, resize, file I/O, uploads). Usage (GPU box):
+    python tools/time_scan.py [W H VIEWS] [extra apd flags...]"""
+import os, re, subprocess, sys, tempfile, time
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "apde-mvs_amd"), os.path.join(REPO, "tests")]
+import numpy as np
+import synth, host_schedule as HS
+
+W, H, V = (int(x) for x in sys.argv[1:4]) if len(sys.argv) >= 4 else (3024, 2016, 9)
+extra = sys.argv[4:]
+sc = synth.make_scene(W, H, V - 1)
+folder = tempfile.mkdtemp(prefix="apd_scan_")
+HS.write_dense_folder(sc, folder, ext=".png", masks=True)
+from PIL import Image
+for f in sorted(os.listdir(os.path.join(folder, "images"))):  # re-encode as baseline JPEG
+    p = os.path.join(folder, "images", f)
+    Image.open(p).save(p[:-4] + ".jpg", quality=95)
+    os.remove(p)
+apd = os.path.join(REPO, "apde-mvs_amd", "host", "build", "apd")
+cmd = [apd, "-d", folder, "--dataset", "ETH3D", "--no_fuse", "true"] + extra
+t0 = time.time()
+out = subprocess.run(cmd, capture_output=True, text=True)
+wall = time.time() - t0
+if out.returncode != 0:
+    print(out.stdout[-3000:], out.stderr[-3000:])
+    sys.exit(out.returncode)
+rpm = [int(x) for x in re.findall(r"RunPatchMatch time: (\d+) ms", out.stdout)]
+cost = [int(x) for x in re.findall(r"Cost time: (\d+) ms", out.stdout)][:-1]  # the last line is the total
+print(f"scan {W}x{H} x{V} views: wall {wall:.1f} s, problems {len(rpm)}, RunPatchMatch total {sum(rpm)/1e3:.1f} s, "
+      f"per-problem cost total {sum(cost)/1e3:.1f} s, host overhead {wall - sum(rpm)/1e3:.1f} s", flush=True)
