@@ -1903,25 +1903,32 @@ __global__ __launch_bounds__(BLOCK) void k_filter(Args a, const int *__restrict_
 // and the peak analysis. Waves skip every task none of their pixels selected (selected_views is
 // spatially coherent), which the lanes = views layout could not.
 // ---------------------------------------------------------------------------------------------
-#define DW_CHUNK_BYTES 32768
+#ifndef DW_CHUNK_BYTES
+#define DW_CHUNK_BYTES 16384  // 8 disparities per chunk at N = 8: 44 KiB per workgroup, 3 per CU (16: 2 per CU, 7 % slower)
+#endif
 struct DwLds {
     float refw[36 * VM_P];
     float pc[61 * VM_P];        // cost curve per pixel [d][p]
     float4 pl[VM_P];            // ref-frame plane
     float base[VM_P], disp[VM_P], wn[VM_P];
+    float rmean[VM_P], rvar[VM_P];  // reference-window moments (RefWin)
     uint32_t sel[VM_P];
     int active[VM_P];
+    int pxy[VM_P];              // px | py << 16
+    int vcnt[32];               // active pixels that selected view v
 };
 static inline int dw_chunk(int N) { return std::max(1, std::min(61, DW_CHUNK_BYTES / (N * VM_P * (int)sizeof(float)))); }
+// + cost table [chunk][N][64] fp32, view weights [N][64] u8, per-view pixel slots [N][64] u8
 static inline size_t dw_lds_bytes(int N) {
-    return sizeof(DwLds) + (size_t)dw_chunk(N) * N * VM_P * sizeof(float) + (size_t)N * VM_P * sizeof(int);
+    return sizeof(DwLds) + (size_t)dw_chunk(N) * N * VM_P * sizeof(float) + (size_t)2 * N * VM_P;
 }
 template <bool F16>
 __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, int chunk, int tw) {
     const int N = a.N, W = a.W, H = a.H;
     DwLds &L = *reinterpret_cast<DwLds *>(apd_dyn_lds);
-    float *tcL = reinterpret_cast<float *>(&L + 1);           // [chunk][N][64]
-    int *wts = reinterpret_cast<int *>(tcL + chunk * N * VM_P); // [N][64]
+    float *tcL = reinterpret_cast<float *>(&L + 1);                 // [chunk][N][64]
+    uint8_t *wts = reinterpret_cast<uint8_t *>(tcL + chunk * N * VM_P);  // [N][64]
+    uint8_t *vslot = wts + N * VM_P;                                 // [N][64] pixel slots per view
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
     const APD_G Cam &cam0 = a.cams[0];
@@ -1941,6 +1948,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
             L.sel[p] = a.sel[c];
         }
         for (int v = wave; v < N; v += VM_WAVES) wts[v * VM_P + p] = a.vw[(size_t)v * a.HW + c];
+        if (wave == 0) L.pxy[p] = px | (py << 16);
         for (int k = wave; k < 36; k += VM_WAVES) {
             const int i = k / 6, j = k - 6 * (k / 6);
             L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
@@ -1974,10 +1982,74 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
     const float4 pl = L.pl[p];
     const bool geom = a.geom != 0;
     const float gf = a.gf;
+#ifndef APD_DW_PER_PIXEL
+    // Compacted (disparity, pixel) pairs: per view, only the active pixels that selected it (the
+    // others' costs are never read), packed 64 to a wave-task, disparity-major, dealt round-robin over
+    // the waves in view order -- the 4 waves sample one source image at neighbouring disparities.
+    if (wave == 0) { L.rmean[p] = rw.mean; L.rvar[p] = rw.var; }
+    for (int v = wave; v < N; v += VM_WAVES) {
+        const bool on = act && ((sv >> v) & 1u);
+        const uint64_t m = __ballot(on);
+        if (on) vslot[v * VM_P + __popcll(m & ((1ull << lane) - 1ull))] = (uint8_t)p;
+        if (lane == 0) L.vcnt[v] = __popcll(m);
+    }
+    __syncthreads();
+#endif
     for (int d0 = 0; d0 < 61; d0 += chunk) {
         const int dc = min(chunk, 61 - d0);
-        // ---- P1: (depth, view) tasks, lane = pixel
+        // ---- P1: (depth, view) tasks
         uint64_t defer = 0;
+#ifndef APD_DW_PER_PIXEL
+        {
+            int v = 0, vb = 0, nv = L.vcnt[0], tv = (dc * nv + 63) >> 6;
+            for (int j = wave, k = 0;; j += VM_WAVES, ++k) {
+                while (v < N && j >= vb + tv) {
+                    vb += tv;
+                    if (++v < N) { nv = L.vcnt[v]; tv = (dc * nv + 63) >> 6; }
+                }
+                if (v >= N) break;
+                const int t = (j - vb) * 64 + lane;
+                if (t < dc * nv) {
+                    int dd = 0, r = t;
+                    while (r >= nv) { r -= nv; ++dd; }
+                    const int q = vslot[v * VM_P + r], xy = L.pxy[q];
+                    const int qx = xy & 0xFFFF, qy = xy >> 16;
+                    const float pdepth = cam0.K[0] * L.base[q] / (L.disp[q] + (float)(d0 + dd - 30));
+                    float tc = 0.0f;
+                    if (!(pdepth < a.dmin || pdepth > a.dmax)) {
+                        float4 tp = L.pl[q];
+                        tp.w = dist2origin(cam0, qx, qy, pdepth, tp);
+                        const RefWin rwq{&L.refw[q], L.rmean[q], L.rvar[q]};
+                        bool slow;
+                        tc = ncc_old_fast<F16, VM_P>(a, qx, qy, v + 1, tp, rwq, slow);
+                        if (slow) defer |= 1ull << k;
+                        if (geom) tc = fmaf(gf, geom_cost(a, qx, qy, v + 1, tp), tc);
+                    }
+                    tcL[(dd * N + v) * VM_P + q] = tc;
+                }
+            }
+        }
+        while (defer) {
+            const int k = __builtin_ctzll(defer);
+            defer &= defer - 1;
+            const int j = wave + k * VM_WAVES;
+            int v = 0, vb = 0, nv = L.vcnt[0], tv = (dc * nv + 63) >> 6;
+            while (j >= vb + tv) { vb += tv; ++v; nv = L.vcnt[v]; tv = (dc * nv + 63) >> 6; }
+            const int t = (j - vb) * 64 + lane;
+            if (t < dc * nv) {
+                int dd = 0, r = t;
+                while (r >= nv) { r -= nv; ++dd; }
+                const int q = vslot[v * VM_P + r], xy = L.pxy[q];
+                const int qx = xy & 0xFFFF, qy = xy >> 16;
+                const float pdepth = cam0.K[0] * L.base[q] / (L.disp[q] + (float)(d0 + dd - 30));
+                float4 tp = L.pl[q];
+                tp.w = dist2origin(cam0, qx, qy, pdepth, tp);
+                float tc = ncc_old_slow<F16>(a.self, qx, qy, v + 1, tp, &L.refw[q], VM_P, L.rmean[q], L.rvar[q]);
+                if (geom) tc = fmaf(gf, geom_cost(a, qx, qy, v + 1, tp), tc);
+                tcL[(dd * N + v) * VM_P + q] = tc;
+            }
+        }
+#else
         // view-major contiguous chunk per wave (consecutive tasks on the same source image)
         const int cn = (dc * N + VM_WAVES - 1) / VM_WAVES, u0 = wave * cn, u1 = min(u0 + cn, dc * N);
 #ifdef APD_TASK_INTERLEAVE
@@ -2015,6 +2087,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
             if (geom) tc = fmaf(gf, geom_cost(a, px, py, v + 1, tp), tc);
             tcL[t * VM_P + p] = tc;
         }
+#endif
         __syncthreads();
         // ---- P2: in-order weighted view sums per (pixel, depth)
         for (int dd = wave; dd < dc; dd += VM_WAVES) {
