@@ -274,6 +274,74 @@ __global__ __launch_bounds__(BLOCK) void k_find_nearest(Args a, int n_off) {
     a.nearest[c] = out;
 }
 
+// The same result in O(r) instead of O(r^2) reads per pixel. Level L = the querying pixel's own
+// confidence; the sites of level L are the STRONG pixels with confidence >= L.
+//   k_near_columns: per (level, column), the vertical distance to the nearest site of that level in
+//                   the column, capped at 101 (= none within the window's +-100 rows).
+//   k_find_nearest_rows: D = min over |dx| <= 100 of dx^2 + g_L(x + dx, y)^2 is the smallest d^2 of a
+//                   site inside the 201x201 window, i.e. the ring at which the ring search first hits;
+//                   then that ring's offsets are visited in the table order with the ring search's
+//                   rule (max confidence, first in order). Bit-identical to k_find_nearest.
+__global__ __launch_bounds__(BLOCK) void k_near_columns(Args a, int levels, uint8_t *__restrict__ g) {
+    const int t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= levels * a.W) return;
+    const int L = t / a.W, x = t - L * a.W, W = a.W, H = a.H;
+    uint8_t *gl = g + (size_t)L * a.HW;
+    int last = -1000;
+    for (int y = 0; y < H; ++y) {
+        const int c = y * W + x;
+        if (a.weak[c] == APD_STRONG && a.conf[c] >= L) last = y;
+        gl[c] = (uint8_t)min(y - last, 101);
+    }
+    last = 1 << 20;
+    for (int y = H - 1; y >= 0; --y) {
+        const int c = y * W + x;
+        if (a.weak[c] == APD_STRONG && a.conf[c] >= L) last = y;
+        const int up = min(last - y, 101);
+        if (up < gl[c]) gl[c] = (uint8_t)up;
+    }
+}
+__global__ __launch_bounds__(BLOCK) void k_find_nearest_rows(Args a, const uint8_t *__restrict__ g,
+                                                             const int *__restrict__ ring_start) {
+    const int c = blockIdx.x * BLOCK + threadIdx.x;
+    if (c >= a.HW) return;
+    const int W = a.W, H = a.H;
+    const int py = c / W, px = c - py * W;
+    const uint8_t w = a.weak[c];
+    short2 out = make_short2(-1, -1);
+    if (w == APD_WEAK || w == APD_UNKNOWN) {
+        const uint8_t cc = a.conf[c];
+        const uint8_t *row = g + (size_t)cc * a.HW + (size_t)py * W;
+        int best = 1 << 30;
+        for (int dx = 0; dx <= 100 && dx * dx < best; ++dx) {
+            if (px + dx < W) {
+                const int gv = row[px + dx];
+                if (gv <= 100) best = min(best, dx * dx + gv * gv);
+            }
+            if (dx > 0 && px - dx >= 0) {
+                const int gv = row[px - dx];
+                if (gv <= 100) best = min(best, dx * dx + gv * gv);
+            }
+        }
+        if (best <= 20000) {
+            int bc = -1;
+            for (int k = ring_start[best], k1 = ring_start[best + 1]; k < k1; ++k) {
+                const short2 o = a.near_offsets[k];
+                const int tx = px + o.x, ty = py + o.y;
+                if (tx < 0 || tx >= W || ty < 0 || ty >= H) continue;
+                const int t = tx + ty * W;
+                if (a.weak[t] != APD_STRONG) continue;
+                const int tc = a.conf[t];
+                if (tc < cc) continue;
+                if (tc > bc) { bc = tc; out = make_short2((short)tx, (short)ty); }
+            }
+        }
+    } else if (w == APD_STRONG) {
+        out = make_short2((short)px, (short)py);
+    }
+    a.nearest[c] = out;
+}
+
 // PointinTriangle (APD.cu:122-143)
 __device__ __forceinline__ bool point_in_triangle(int ax, int ay, int bx, int by, int cx, int cy, int px, int py) {
     float ABx = (float)(bx - ax), ABy = (float)(by - ay);
@@ -2653,8 +2721,9 @@ struct apd_ctx {
     std::string err;
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
-        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals;
+        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g;
     int n_near = 0;
+    int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
     Args args{};
     bool loaded = false, prepared = false;
     bool sweep_vm = true;          // view-major Strong sweep (APD_SWEEP_LANES=1 selects k_sweep_strong)
@@ -2756,6 +2825,12 @@ static int build_near_offsets(apd_ctx *ctx) {
     int st = ensure(ctx, ctx->near_off, off.size() * sizeof(short2));
     if (st) return st;
     HIP_OK(ctx, hipMemcpy(ctx->near_off.p, off.data(), off.size() * sizeof(short2), hipMemcpyHostToDevice));
+    // ring_start[D] = first table index with d^2 >= D, D = 0 .. 20001
+    std::vector<int> ring(20002, (int)off.size());
+    for (int k = (int)off.size() - 1; k >= 0; --k) ring[off[k].x * off[k].x + off[k].y * off[k].y] = k;
+    for (int D = 20000; D >= 0; --D) ring[D] = std::min(ring[D], ring[D + 1]);
+    if ((st = ensure(ctx, ctx->near_ring, ring.size() * sizeof(int)))) return st;
+    HIP_OK(ctx, hipMemcpy(ctx->near_ring.p, ring.data(), ring.size() * sizeof(int), hipMemcpyHostToDevice));
     ctx->n_near = (int)off.size();
     return APD_OK;
 }
@@ -2847,7 +2922,7 @@ void apd_destroy(apd_ctx *ctx) {
     DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
-                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals};
+                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
@@ -2977,6 +3052,13 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
         HIP_OK(ctx, hipMemsetAsync(ctx->reliable.p, 0, HW, s));
         HIP_OK(ctx, hipMemsetAsync(ctx->fit.p, 0, HW * sizeof(float4), s));
         if ((st = build_near_offsets(ctx))) return st;
+        // per-level column distances for k_find_nearest_rows (confidence is an input here)
+        int maxc = 1;
+        if (pb->confidence)
+            for (size_t i = 0; i < HW; ++i) maxc = std::max<int>(maxc, pb->confidence[i]);
+        ctx->near_levels = maxc + 1;
+        if (getenv("APD_NEAREST_RING") || (size_t)ctx->near_levels * HW > ((size_t)4 << 30)) ctx->near_levels = 0;
+        if (ctx->near_levels && (st = ensure(ctx, ctx->near_g, (size_t)ctx->near_levels * HW))) return st;
     }
     // kernel arguments
     a.W = W; a.H = H; a.HW = (int)HW; a.N = N;
@@ -3098,7 +3180,14 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
     if (a.use_apd) {
         // anchors_map from the input WEAK mask (APD.cpp:627-640)
         if ((st = build_list(ctx, 2, 0, (int *)ctx->amap.p, (int *)ctx->totals.p + 4))) return st;
-        hipLaunchKernelGGL(k_find_nearest, dim3(gpx), dim3(BLOCK), 0, s, a, ctx->n_near);
+        if (ctx->near_levels) {
+            hipLaunchKernelGGL(k_near_columns, dim3(blocks_for((size_t)ctx->near_levels * a.W, BLOCK)), dim3(BLOCK), 0, s, a,
+                               ctx->near_levels, (uint8_t *)ctx->near_g.p);
+            hipLaunchKernelGGL(k_find_nearest_rows, dim3(gpx), dim3(BLOCK), 0, s, a, (const uint8_t *)ctx->near_g.p,
+                               (const int *)ctx->near_ring.p);
+        } else {
+            hipLaunchKernelGGL(k_find_nearest, dim3(gpx), dim3(BLOCK), 0, s, a, ctx->n_near);
+        }
         hipLaunchKernelGGL(k_gen_anchors, dim3(gpx), dim3(BLOCK), 0, s, a);
         hipLaunchKernelGGL(k_neighbour_update, dim3(gpx), dim3(BLOCK), 0, s, a);
         if ((st = check_launch(ctx, "anchors"))) return st;
