@@ -97,3 +97,22 @@ def test_cli_memory_cache_flush(scan, tmp_path):
     am = synth.read_bin_mat(os.path.join(d, "anchors_map.bin"))
     n_weak, k = np.fromfile(os.path.join(d, "anchors.bin"), np.int32, 2)
     assert k == 9 and n_weak == int((am >= 0).sum())
+
+
+def test_run_scans_drives_the_binary(tmp_path):
+    """run_scans.py (run.py's orchestration) runs the apd binary over a batch: every scan ends with
+    its depth maps and APD/APD.ply, and the log run.py would keep."""
+    import sys
+    root = tmp_path / "ETH3D"
+    root.mkdir()
+    for name, seed in (("scan_a", 3), ("scan_b", 4)):
+        sc = synth.make_scene(240, 180, 2, seed=seed)
+        HS.write_dense_folder(sc, str(root / name), ext=".png")
+    script = os.path.join(REPO, "apde-mvs_amd", "run_scans.py")
+    out = subprocess.run([sys.executable, script, "--data_dir", str(root), "--no_sam", "--memory_cache", "--flush",
+                          "--APD_path", APD_BIN], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    for name in ("scan_a", "scan_b"):
+        assert os.path.getsize(root / name / "APD" / "APD.ply") > 0
+        assert os.path.exists(root / name / "APD" / "00000000" / "depths.bin")
+        assert "RunPatchMatch time" in (root / name / "APD" / "log.txt").read_text()
