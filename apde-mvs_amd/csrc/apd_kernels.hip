@@ -1297,13 +1297,11 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const WvLdsT<F16> 
                                                const FastTex<F16, true> &T, const SrcTex<F16> &Q, float &ss,
                                                float &sss, float &srs) {
     const uint64_t fm = __ballot(live && fast), sm = __ballot(live && !fast);
-    if (fm) {
-        Hom Hp = Hm;
-        if (!(live && fast)) {
-#pragma unroll
-            for (int k = 0; k < 9; ++k) Hp.h[k] = (k == 8) ? 1.0f : 0.0f;
-        }
-        const bool acc = live && fast;
+    // only the lanes whose window is evaluated issue its gathers (the gather path's cost is per
+    // active lane); the others are exec-masked off instead of sampling a parked homography
+    if (live && fast) {
+        const Hom &Hp = Hm;
+        const bool acc = true;
 #pragma unroll
         for (int i = 0; i < NW; ++i) {
             const float x = (float)(ax - 5 + INC * i);
