@@ -1296,7 +1296,7 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const WvLdsT<F16> 
                                                const Hom &Hm, int ax, int ay, bool live, bool fast,
                                                const FastTex<F16, true> &T, const SrcTex<F16> &Q, float &ss,
                                                float &sss, float &srs) {
-    const uint64_t fm = __ballot(live && fast), sm = __ballot(live && !fast);
+    const uint64_t sm = __ballot(live && !fast);
     // only the lanes whose window is evaluated issue its gathers (the gather path's cost is per
     // active lane); the others are exec-masked off instead of sampling a parked homography
     if (live && fast) {
