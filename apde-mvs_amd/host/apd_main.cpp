@@ -323,6 +323,7 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     SAY("Image size: " << width << " * " << height);
     const size_t HW = (size_t)width * height;
     auto fit = [&](Mat m) { return (m.cols != width || m.rows != height) ? resize_nearest(m, width, height) : m; };
+    const auto t_img = std::chrono::steady_clock::now();
     // ---- priors (APD.cpp:592-684)
     std::vector<Mat> depths;
     if (P.geom_consistency || P.use_APD) {
@@ -377,6 +378,7 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
             init_planes[4 * i + 3] = d.ptr<float>()[i];
         }
     }
+    const auto t_pri = std::chrono::steady_clock::now();
     // ---- device (CudaSpaceInitialization + RunPatchMatch)
     std::vector<const float *> img_ptrs(NI), dep_ptrs(NI);
     for (int i = 0; i < NI; ++i) img_ptrs[i] = scaled[i]->img.data();
@@ -428,7 +430,9 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
         curve.resize(HW * APD_CURVE_SAMPLES);
         out.reliable_curve = curve.data();
     }
+    const auto t_run = std::chrono::steady_clock::now();
     st = apd_get_results(ctx, &out);
+    const auto t_get = std::chrono::steady_clock::now();
     if (st != APD_OK) { SAY("apd_get_results failed: " << apd_last_error(ctx)); return false; }
     if (!(P.geom_consistency || P.use_APD)) memset(confidence.bytes(), 1, confidence.size_bytes());
     apd_epilogue(width, height, planes.data(), P.depth_min, P.depth_max, depth.ptr<float>(), normal.ptr<float>(),
@@ -456,11 +460,19 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
             fclose(fc);
         }
     }
+    const auto t_epi = std::chrono::steady_clock::now();
     emit(result_folder + "/depths.bin", depth);
     emit(result_folder + "/normals.bin", normal);
     emit(result_folder + "/weak.bin", states);
     if (P.geom_consistency || P.use_APD) emit(result_folder + "/confidence.bin", confidence);
     const auto end = std::chrono::steady_clock::now();
+    if (getenv("APD_HOST_TIMING")) {  // host-side breakdown of one problem (ms)
+        auto ms_ = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::lock_guard<std::mutex> g(g_print);
+        printf("HostTiming images %.1f priors %.1f set+run %.1f (run %ld) results %.1f epilogue %.1f emit %.1f\n",
+               ms_(start, t_img), ms_(t_img, t_pri), ms_(t_pri, t_run), ms, ms_(t_run, t_get), ms_(t_get, t_epi),
+               ms_(t_epi, end));
+    }
     {
         std::lock_guard<std::mutex> g(g_print);
         std::cout << "Processing image: " << format_index(pb.ref_image_id) << " done!" << std::endl;

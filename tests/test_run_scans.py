@@ -33,8 +33,10 @@ def test_review_mode_commands(tmp_path):
     make_scan(str(root), "empty_scan", 0, subdir="other")
     stdout = run(["--data_dir", str(root), "--gpu_num", "2", "--review", "--APD_path", "/opt/apd"])
     cmds = [l for l in stdout.splitlines() if l.startswith("/opt/apd ")]
-    # largest scan first; empty_scan has no image folder among the candidates and is skipped
-    assert [re.search(r"--dense_folder (\S+)", c).group(1) for c in cmds] == [str(root / "pipes"), str(root / "office")]
+    # largest scan first (the submission order; the two slots then run concurrently); empty_scan has
+    # no image folder among the candidates and is skipped
+    assert "scans: ['pipes', 'office']" in stdout
+    assert sorted(re.search(r"--dense_folder (\S+)", c).group(1) for c in cmds) == [str(root / "office"), str(root / "pipes")]
     assert os.path.islink(root / "pipes" / "images")  # images/ -> undist/images
     for c in cmds:
         assert re.search(r"--gpu_index [01] ", c)

@@ -28,5 +28,10 @@ if out.returncode != 0:
     sys.exit(out.returncode)
 rpm = [int(x) for x in re.findall(r"RunPatchMatch time: (\d+) ms", out.stdout)]
 cost = [int(x) for x in re.findall(r"Cost time: (\d+) ms", out.stdout)][:-1]  # the last line is the total
+ht = re.findall(r"HostTiming images ([\d.]+) priors ([\d.]+) set\+run ([\d.]+) \(run (\d+)\) results ([\d.]+) epilogue ([\d.]+) emit ([\d.]+)", out.stdout)
+if ht:
+    a = np.array(ht, float).sum(0) / 1e3
+    print("host breakdown (s, summed over problems): images %.2f priors %.2f set+run %.2f (run %.2f, so set %.2f) "
+          "results %.2f epilogue %.2f emit %.2f" % (a[0], a[1], a[2], a[3], a[2] - a[3], a[4], a[5], a[6]), flush=True)
 print(f"scan {W}x{H} x{V} views: wall {wall:.1f} s, problems {len(rpm)}, RunPatchMatch total {sum(rpm)/1e3:.1f} s, "
       f"per-problem cost total {sum(cost)/1e3:.1f} s, host overhead {wall - sum(rpm)/1e3:.1f} s", flush=True)
