@@ -561,6 +561,72 @@ struct FastTex {
     __device__ __forceinline__ float sample(const Tap &t) const { return finish(t, load(t)); }
 };
 
+// The 36 taps of a ComputeBilateralNCCOld window (6x6, step 2) and their moments, for a texel source
+// TT with the FastTex interface (tap / load / finish). Accumulation order = the reference's (i outer,
+// j inner). (Factored out of ncc_old_fast; the Strong sweep measured 3 % faster with this form.)
+template <class TT, int RS>
+__device__ __forceinline__ void ncc_old_taps(const TT &T, const Hom &Hm, int px, int py, const RefWin &rw, float &ss,
+                                             float &sss, float &srs) {
+        using FT = TT;
+        auto column = [&](int i, typename FT::Tap *t) {
+            const float x = (float)(px - 5 + 2 * i);
+            const apd_f2 cxy = {fmaf(Hm.h[0], x, Hm.h[2]), fmaf(Hm.h[3], x, Hm.h[5])};
+            const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const float y = (float)(py - 5 + 2 * j);
+                const apd_f2 XY = pk_fma((apd_f2){Hm.h[1], Hm.h[4]}, (apd_f2){y, y}, cxy);
+                const float Z = fmaf(Hm.h[7], y, cz);
+                t[j] = T.tap(XY, rcp_newton(Z));
+            }
+        };
+        auto consume = [&](int i, const typename FT::Tap *t, const typename FT::Raw *q) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const float v = T.finish(t[j], q[j]);
+                ss += v;
+                // (sss, srs) = (fma(v, v, sss), fma(r, v, srs))
+                const apd_f2 acc = pk_fma((apd_f2){v, rw.r[(i * 6 + j) * RS]}, (apd_f2){v, v}, (apd_f2){sss, srs});
+                sss = acc.x;
+                srs = acc.y;
+            }
+        };
+#ifndef APD_NCC_NOPIPE
+        // software pipeline: column i+1's gathers are in flight while column i is consumed
+        typename FT::Tap ta[6], tb[6];
+        typename FT::Raw qa[6], qb[6];
+        column(0, ta);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) qa[j] = T.load(ta[j]);
+#pragma unroll
+        for (int i = 0; i < 6; i += 2) {
+            if (i + 1 < 6) {
+                column(i + 1, tb);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) qb[j] = T.load(tb[j]);
+            }
+            consume(i, ta, qa);
+            if (i + 2 < 6) {
+                column(i + 2, ta);
+#pragma unroll
+                for (int j = 0; j < 6; ++j) qa[j] = T.load(ta[j]);
+            }
+            if (i + 1 < 6) consume(i + 1, tb, qb);
+        }
+#else
+        // One window column (6 taps) per step: all 6 gathers are issued before the first is consumed.
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            typename FT::Tap t[6];
+            typename FT::Raw q[6];
+            column(i, t);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) q[j] = T.load(t[j]);
+            consume(i, t, q);
+        }
+#endif
+}
+
 // IEEE-division statement of the ComputeBilateralNCCOld window sum (taken only for windows that
 // window_rcp_ok rejects).
 template <bool F16>
@@ -650,65 +716,8 @@ __device__ __forceinline__ float ncc_old_fast(const Args &a, int px, int py, int
         for (int k = 0; k < 9; ++k) Hm.h[k] = (k == 8) ? 1.0f : 0.0f;  // every tap -> texel (0, 0)
     }
     float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-        const FastTex<F16, (RS > 1)> T(a, s);
-        using FT = FastTex<F16, (RS > 1)>;
-        auto column = [&](int i, typename FT::Tap *t) {
-            const float x = (float)(px - 5 + 2 * i);
-            const apd_f2 cxy = {fmaf(Hm.h[0], x, Hm.h[2]), fmaf(Hm.h[3], x, Hm.h[5])};
-            const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                const float y = (float)(py - 5 + 2 * j);
-                const apd_f2 XY = pk_fma((apd_f2){Hm.h[1], Hm.h[4]}, (apd_f2){y, y}, cxy);
-                const float Z = fmaf(Hm.h[7], y, cz);
-                t[j] = T.tap(XY, rcp_newton(Z));
-            }
-        };
-        auto consume = [&](int i, const typename FT::Tap *t, const typename FT::Raw *q) {
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                const float v = T.finish(t[j], q[j]);
-                ss += v;
-                // (sss, srs) = (fma(v, v, sss), fma(r, v, srs))
-                const apd_f2 acc = pk_fma((apd_f2){v, rw.r[(i * 6 + j) * RS]}, (apd_f2){v, v}, (apd_f2){sss, srs});
-                sss = acc.x;
-                srs = acc.y;
-            }
-        };
-#ifndef APD_NCC_NOPIPE
-        // software pipeline: column i+1's gathers are in flight while column i is consumed
-        typename FT::Tap ta[6], tb[6];
-        typename FT::Raw qa[6], qb[6];
-        column(0, ta);
-#pragma unroll
-        for (int j = 0; j < 6; ++j) qa[j] = T.load(ta[j]);
-#pragma unroll
-        for (int i = 0; i < 6; i += 2) {
-            if (i + 1 < 6) {
-                column(i + 1, tb);
-#pragma unroll
-                for (int j = 0; j < 6; ++j) qb[j] = T.load(tb[j]);
-            }
-            consume(i, ta, qa);
-            if (i + 2 < 6) {
-                column(i + 2, ta);
-#pragma unroll
-                for (int j = 0; j < 6; ++j) qa[j] = T.load(ta[j]);
-            }
-            if (i + 1 < 6) consume(i + 1, tb, qb);
-        }
-#else
-        // One window column (6 taps) per step: all 6 gathers are issued before the first is consumed.
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            typename FT::Tap t[6];
-            typename FT::Raw q[6];
-            column(i, t);
-#pragma unroll
-            for (int j = 0; j < 6; ++j) q[j] = T.load(t[j]);
-            consume(i, t, q);
-        }
-#endif
+    const FastTex<F16, (RS > 1)> T(a, s);
+    ncc_old_taps<FastTex<F16, (RS > 1)>, RS>(T, Hm, px, py, rw, ss, sss, srs);
     return ncc_old_finish(ss, sss, srs, rw.mean, rw.var);
 }
 

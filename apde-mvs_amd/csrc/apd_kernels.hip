@@ -2075,24 +2075,30 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 }
                 if (v >= N) break;
                 const int t = (j - vb) * 64 + lane;
-                if (t < dc * nv) {
-                    int dd = 0, r = t;
+                const bool has = t < dc * nv;
+                int dd = 0, q = 0;
+                if (has) {
+                    int r = t;
                     while (r >= nv) { r -= nv; ++dd; }
-                    const int q = vslot[v * VM_P + r], xy = L.pxy[q];
-                    const int qx = xy & 0xFFFF, qy = xy >> 16;
-                    const float pdepth = cam0.K[0] * L.base[q] / (L.disp[q] + (float)(d0 + dd - 30));
-                    float tc = 0.0f;
-                    if (!(pdepth < a.dmin || pdepth > a.dmax)) {
-                        float4 tp = L.pl[q];
+                    q = vslot[v * VM_P + r];
+                }
+                const int xy = L.pxy[q];
+                const int qx = xy & 0xFFFF, qy = xy >> 16;
+                const float pdepth = cam0.K[0] * L.base[q] / (L.disp[q] + (float)(d0 + dd - 30));
+                const bool eval = has && !(pdepth < a.dmin || pdepth > a.dmax);
+                const RefWin rwq{&L.refw[q], L.rmean[q], L.rvar[q]};
+                float4 tp = L.pl[q];
+                float tc = 0.0f;
+                {
+                    if (eval) {
                         tp.w = dist2origin(cam0, qx, qy, pdepth, tp);
-                        const RefWin rwq{&L.refw[q], L.rmean[q], L.rvar[q]};
                         bool slow;
                         tc = ncc_old_fast<F16, VM_P>(a, qx, qy, v + 1, tp, rwq, slow);
                         if (slow) defer |= 1ull << k;
-                        if (geom) tc = fmaf(gf, geom_cost(a, qx, qy, v + 1, tp), tc);
                     }
-                    tcL[(dd * N + v) * VM_P + q] = tc;
                 }
+                if (eval && geom) tc = fmaf(gf, geom_cost(a, qx, qy, v + 1, tp), tc);
+                if (has) tcL[(dd * N + v) * VM_P + q] = tc;
             }
         }
         while (defer) {
