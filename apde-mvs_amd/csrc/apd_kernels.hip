@@ -1300,35 +1300,65 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const WvLdsT<F16> 
     // only the lanes whose window is evaluated issue its gathers (the gather path's cost is per
     // active lane); the others are exec-masked off instead of sampling a parked homography
     if (live && fast) {
-        const Hom &Hp = Hm;
-        const bool acc = true;
-#pragma unroll
-        for (int i = 0; i < NW; ++i) {
+        using TT = FastTex<F16, true>;
+        auto column = [&](int i, typename TT::Tap *t) {
             const float x = (float)(ax - 5 + INC * i);
-            const apd_f2 cxy = {fmaf(Hp.h[0], x, Hp.h[2]), fmaf(Hp.h[3], x, Hp.h[5])};
-            const float cz = fmaf(Hp.h[6], x, Hp.h[8]);
-            typename FastTex<F16, true>::Tap t[NW];
-            typename FastTex<F16, true>::Raw q[NW];
+            const apd_f2 cxy = {fmaf(Hm.h[0], x, Hm.h[2]), fmaf(Hm.h[3], x, Hm.h[5])};
+            const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
 #pragma unroll
             for (int j = 0; j < NW; ++j) {
                 const float y = (float)(ay - 5 + INC * j);
-                const apd_f2 XY = pk_fma((apd_f2){Hp.h[1], Hp.h[4]}, (apd_f2){y, y}, cxy);
-                const float Z = fmaf(Hp.h[7], y, cz);
-                t[j] = T.tap(XY, rcp_newton(Z));
+                const apd_f2 XY = pk_fma((apd_f2){Hm.h[1], Hm.h[4]}, (apd_f2){y, y}, cxy);
+                t[j] = T.tap(XY, rcp_newton(fmaf(Hm.h[7], y, cz)));
             }
-#pragma unroll
-            for (int j = 0; j < NW; ++j) q[j] = T.load(t[j]);
-            // accumulate column by column, taps in (i, j) order as before
+        };
+        // taps in (i, j) order, skipping those outside the SA mask
+        auto consume = [&](int i, const typename TT::Tap *t, const typename TT::Raw *q) {
 #pragma unroll
             for (int j = 0; j < NW; ++j) {
                 const int tk = i * NW + j;
                 const float v = T.finish(t[j], q[j]);
-                if (acc && ((mask >> tk) & 1ull)) {
+                if ((mask >> tk) & 1ull) {
                     const float r = L.rref[(tap0 + tk) * VM_P + p];
                     ss += v;
                     sss = fmaf(v, v, sss);
                     srs = fmaf(r, v, srs);
                 }
+            }
+        };
+        if constexpr (NW <= 3) {
+            // an anchor window (3x3): all 9 gathers in flight before the first is consumed
+            typename TT::Tap t[NW][NW];
+            typename TT::Raw q[NW][NW];
+#pragma unroll
+            for (int i = 0; i < NW; ++i) column(i, t[i]);
+#pragma unroll
+            for (int i = 0; i < NW; ++i)
+#pragma unroll
+                for (int j = 0; j < NW; ++j) q[i][j] = T.load(t[i][j]);
+#pragma unroll
+            for (int i = 0; i < NW; ++i) consume(i, t[i], q[i]);
+        } else {
+            // the centre window (6x6): column i+1's gathers in flight while column i is consumed
+            typename TT::Tap ta[NW], tb[NW];
+            typename TT::Raw qa[NW], qb[NW];
+            column(0, ta);
+#pragma unroll
+            for (int j = 0; j < NW; ++j) qa[j] = T.load(ta[j]);
+#pragma unroll
+            for (int i = 0; i < NW; i += 2) {
+                if (i + 1 < NW) {
+                    column(i + 1, tb);
+#pragma unroll
+                    for (int j = 0; j < NW; ++j) qb[j] = T.load(tb[j]);
+                }
+                consume(i, ta, qa);
+                if (i + 2 < NW) {
+                    column(i + 2, ta);
+#pragma unroll
+                    for (int j = 0; j < NW; ++j) qa[j] = T.load(ta[j]);
+                }
+                if (i + 1 < NW) consume(i + 1, tb, qb);
             }
         }
     }
