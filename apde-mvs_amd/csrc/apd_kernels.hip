@@ -2108,8 +2108,10 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 const bool has = t < dc * nv;
                 int dd = 0, q = 0;
                 if (has) {
-                    int r = t;
-                    while (r >= nv) { r -= nv; ++dd; }
+                    // pixel-major: a wave-task's 64 lanes are ~64/dc neighbouring pixels x their dc
+                    // disparities, so one gather instruction spans a short stretch of epipolar lines
+                    const int r = t / dc;
+                    dd = t - r * dc;
                     q = vslot[v * VM_P + r];
                 }
                 const int xy = L.pxy[q];
@@ -2139,8 +2141,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
             while (j >= vb + tv) { vb += tv; ++v; nv = L.vcnt[v]; tv = (dc * nv + 63) >> 6; }
             const int t = (j - vb) * 64 + lane;
             if (t < dc * nv) {
-                int dd = 0, r = t;
-                while (r >= nv) { r -= nv; ++dd; }
+                const int r = t / dc, dd = t - r * dc;
                 const int q = vslot[v * VM_P + r], xy = L.pxy[q];
                 const int qx = xy & 0xFFFF, qy = xy >> 16;
                 const float pdepth = cam0.K[0] * L.base[q] / (L.disp[q] + (float)(d0 + dd - 30));
