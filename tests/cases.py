@@ -91,6 +91,8 @@ CASES = {
     "refine_iter_apd_geom_sa": (128, 96, 4, "apd_geom_sa"),
     "first_n12": (96, 72, 12, "first"),           # view-major P2 in several rounds, 3 tasks per wave
     "refine_iter_n16_apd_geom": (80, 60, 16, "apd_geom"),
+    "first_tiny": (21, 13, 2, "first"),          # smaller than a list tile / DepthToWeak tile, odd sizes
+    "refine_init_apd_small": (40, 28, 2, "apd"),  # anchors and RANSAC where most searches leave the image
     "first_n31": (64, 48, 31, "first"),           # the reference's maximum (32 images): largest LDS tables
     "refine_iter_n31_apd_geom": (48, 40, 31, "apd_geom"),
 }
