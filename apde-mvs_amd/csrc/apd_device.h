@@ -532,12 +532,27 @@ struct FastTex {
         const apd_f2 q = pk_fma(p, (apd_f2){256.0f, 256.0f}, (apd_f2){512.5f, 512.5f});
         const int qx = (int)q.x, qy = (int)q.y;
         Tap t;
+#ifdef APD_ABLATE_ONEROW  // timing-only build: every tap of a wave in 1-2 texel rows, wrong values
+        t.off = ((__umul24(((uint32_t)qy >> 8) & 1u, W1) + (((uint32_t)qx >> 8) & 31u)) << SHIFT) + vbase + (W1 << (SHIFT + 8));
+#else
         t.off = ((__umul24((uint32_t)qy >> 8, W1) + ((uint32_t)qx >> 8)) << SHIFT) + vbase;
+#endif
         t.f = (apd_f2){(float)(qx & 255), (float)(qy & 255)} * 0.00390625f;
         return t;
     }
     using Raw = typename std::conditional<F16, apd_u2_a4, float4>::type;
+#ifdef APD_ABLATE_DWORD  // timing-only build: 4-byte instead of 8-byte gathers, wrong values
+    __device__ __forceinline__ Raw load(const Tap &t) const {
+        if constexpr (F16) {
+            const uint32_t x = *(const APD_G uint32_t *)(base + t.off);
+            return Raw{x, x};
+        } else {
+            return *(const APD_G Raw *)(base + t.off);
+        }
+    }
+#else
     __device__ __forceinline__ Raw load(const Tap &t) const { return *(const APD_G Raw *)(base + t.off); }
+#endif
     __device__ __forceinline__ float finish(const Tap &t, const Raw &v) const {
         if constexpr (F16) {
             // F16 storage is only selected for quarter-integer texels in [0, 256) (see apd_set_problem):
