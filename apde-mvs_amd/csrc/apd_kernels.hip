@@ -683,9 +683,6 @@ __device__ __forceinline__ Cands refine_candidates(const Args &a, int px, int py
     C.dpert = dp;
     const float pert = (float)((double)0.02f * 3.14159265358979323846);
     C.npert = perturbed_normal(cam, px, py, cur, g, pert);
-#ifdef APD_ABLATE_RANDDEPTH  // timing-only build: random-depth candidates replaced by the perturbed depth
-    C.drand = C.dpert;
-#endif
     return C;
 }
 // candidate k of {depth_rand,cur,depth_rand,cur,perturbed} x {cur,rand,rand,perturbed,cur}
@@ -921,9 +918,6 @@ __global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a,
 // workgroup sample the same source image around the same pixels at the same time and share the
 // CU's 32 KiB L1 (contiguous per-wave chunks put up to 4 images per workgroup in flight; measured
 // on the Strong sweep: 13.5 -> 8.0 L1->L2 requests per gather, 16.2 -> 13.8 ms per launch).
-#ifndef APD_TASK_CHUNKED
-#define APD_TASK_INTERLEAVE
-#endif
 #define VM_P 64
 #ifndef APD_VM_LDS_PAD
 #define APD_VM_LDS_PAD 0  // experiments: extra LDS bytes per workgroup (fewer workgroups per CU)
@@ -1036,14 +1030,9 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     // this wave) and evaluated after the loop, so the hot loop holds no call.
     uint64_t defer[2] = {0, 0};  // up to 128 tasks per wave (9 * 31 / VM_WAVES)
     uint32_t issued = 0;         // NCC-Old evaluations of this lane (profiling count, a.evals)
-    // tasks in view-major order, one contiguous chunk per wave: consecutive NCCs of a wave read the
-    // same source image around the same pixels (L1 reuse); (h, v) -> table index t = h * N + v
-    const int c1n = (9 * N + VM_WAVES - 1) / VM_WAVES, u0 = wave * c1n, u1 = min(u0 + c1n, 9 * N);
-#ifdef APD_TASK_INTERLEAVE
+    // tasks in view-major order, dealt round-robin over the waves (the 4 waves of a workgroup sample
+    // one source image around the same pixels at once: L1 sharing); (h, v) -> table index h * N + v
     for (int u = wave, k = 0; u < 9 * N; u += VM_WAVES, ++k) {
-#else
-    for (int u = u0, k = 0; u < u1; ++u, ++k) {
-#endif
         const int v = u / 9, h = u - 9 * v, t = h * N + v;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;  // float cost_array[8][32] = {2.0f} (APD.cu:1120)
         const bool fh = h == 8 || L.nval[h * VM_P + p1];
@@ -1061,11 +1050,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     while (defer[w2]) {
         const int k = __builtin_ctzll(defer[w2]) + 64 * w2;
         defer[w2] &= defer[w2] - 1;
-#ifdef APD_TASK_INTERLEAVE
         const int u = wave + k * VM_WAVES, v = u / 9, h = u - 9 * v, t = h * N + v;
-#else
-        const int u = u0 + k, v = u / 9, h = u - 9 * v, t = h * N + v;
-#endif
         const float4 pl = L.hyp[h * VM_P + p1];
         float val = ncc_old_slow<F16>(a.self, px1, py1, v + 1, pl, rw.r, VM_P, rw.mean, rw.var);
         if (h == 8 && geom_imp) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
@@ -1167,21 +1152,12 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 
     // ---- P3: lane = pixel, wave = (candidate, view) tasks
     defer[0] = defer[1] = 0;
-    const int c3n = (5 * N + VM_WAVES - 1) / VM_WAVES, w0 = wave * c3n, w1 = min(w0 + c3n, 5 * N);
-#ifdef APD_TASK_INTERLEAVE
     for (int u = wave, kt = 0; u < 5 * N; u += VM_WAVES, ++kt) {
-#else
-    for (int u = w0, kt = 0; u < w1; ++u, ++kt) {
-#endif
         const int v = u / 5, k = u - 5 * v, t = k * N + v;
         float cv = 0.0f;
         // a view with sampled weight 0 contributes fmaf(0, cv, tc) == tc for every finite cv (costs are
         // clamped to [0, 2]), so its refinement NCCs are skipped without changing any result
-#ifdef APD_ABLATE_P3  // timing-only build: no refinement NCCs
-        if (false) {
-#else
         if (pv1 && wts[v * VM_P + p1] > 0) {
-#endif
             const float4 tp = VM_CAND(L)[k * VM_P + p1];
             bool slow;
             ++issued;
@@ -1195,11 +1171,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     while (defer[w2]) {
         const int kt = __builtin_ctzll(defer[w2]) + 64 * w2;
         defer[w2] &= defer[w2] - 1;
-#ifdef APD_TASK_INTERLEAVE
         const int u = wave + kt * VM_WAVES, v = u / 5, k = u - 5 * v, t = k * N + v;
-#else
-        const int u = w0 + kt, v = u / 5, k = u - 5 * v, t = k * N + v;
-#endif
         const float4 tp = VM_CAND(L)[k * VM_P + p1];
         float cv = ncc_old_slow<F16>(a.self, px1, py1, v + 1, tp, rw.r, VM_P, rw.mean, rw.var);
         if (geom_imp) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
@@ -1554,13 +1526,8 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     __syncthreads();
 
     // ---- P1: (hypothesis, view) tasks
-#ifdef APD_TASK_INTERLEAVE
     for (int u = wave; u < 9 * N; u += VM_WAVES) {  // view-major: the 4 waves share a source image
         const int v = u / 9, h = u - 9 * v, t = h * N + v;
-#else
-    for (int t = wave; t < 9 * N; t += VM_WAVES) {
-        const int h = t / N, v = t - h * N;
-#endif
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
         const bool want = pv1 && (h == 8 || ((L.flags[p1] >> h) & 1u));
         const float4 pl = L.hyp[h * VM_P + p1];
@@ -1717,13 +1684,8 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     __syncthreads();
 
     // ---- P5: candidate tasks (views with weight > 0)
-#ifdef APD_TASK_INTERLEAVE
     for (int u = wave; u < 5 * N; u += VM_WAVES) {
         const int v = u / 5, k = u - 5 * v, t = k * N + v;
-#else
-    for (int t = wave; t < 5 * N; t += VM_WAVES) {
-        const int k = t / N, v = t - k * N;
-#endif
         float cv = 0.0f;
         const bool want = refine && wts[v * VM_P + p1] > 0;
         const float4 tp = WV_CAND(L)[k * VM_P + p1];
@@ -2078,7 +2040,6 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
     const float4 pl = L.pl[p];
     const bool geom = a.geom != 0;
     const float gf = a.gf;
-#ifndef APD_DW_PER_PIXEL
     // Compacted (disparity, pixel) pairs: per view, only the active pixels that selected it (the
     // others' costs are never read), packed 64 to a wave-task, disparity-major, dealt round-robin over
     // the waves in view order -- the 4 waves sample one source image at neighbouring disparities.
@@ -2090,12 +2051,10 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
         if (lane == 0) L.vcnt[v] = __popcll(m);
     }
     __syncthreads();
-#endif
     for (int d0 = 0; d0 < 61; d0 += chunk) {
         const int dc = min(chunk, 61 - d0);
         // ---- P1: (depth, view) tasks
         uint64_t defer = 0;
-#ifndef APD_DW_PER_PIXEL
         {
             int v = 0, vb = 0, nv = L.vcnt[0], tv = (dc * nv + 63) >> 6;
             for (int j = wave, k = 0;; j += VM_WAVES, ++k) {
@@ -2152,45 +2111,6 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 tcL[(dd * N + v) * VM_P + q] = tc;
             }
         }
-#else
-        // view-major contiguous chunk per wave (consecutive tasks on the same source image)
-        const int cn = (dc * N + VM_WAVES - 1) / VM_WAVES, u0 = wave * cn, u1 = min(u0 + cn, dc * N);
-#ifdef APD_TASK_INTERLEAVE
-        for (int u = wave, k = 0; u < dc * N; u += VM_WAVES, ++k) {
-#else
-        for (int u = u0, k = 0; u < u1; ++u, ++k) {
-#endif
-            const int v = u / dc, dd = u - dc * v, t = dd * N + v;
-            const int d = d0 + dd;
-            const float pdepth = cam0.K[0] * base / (disp + (float)(d - 30));
-            const bool in_range = !(pdepth < a.dmin || pdepth > a.dmax);
-            float tc = 0.0f;
-            if (act && in_range && ((sv >> v) & 1u)) {
-                float4 tp = pl;
-                tp.w = dist2origin(cam0, px, py, pdepth, tp);
-                bool slow;
-                tc = ncc_old_fast<F16, VM_P>(a, px, py, v + 1, tp, rw, slow);
-                if (slow) defer |= 1ull << k;
-                if (geom) tc = fmaf(gf, geom_cost(a, px, py, v + 1, tp), tc);
-            }
-            tcL[t * VM_P + p] = tc;
-        }
-        while (defer) {
-            const int k = __builtin_ctzll(defer);
-            defer &= defer - 1;
-#ifdef APD_TASK_INTERLEAVE
-            const int u = wave + k * VM_WAVES, v = u / dc, dd = u - dc * v, t = dd * N + v;
-#else
-            const int u = u0 + k, v = u / dc, dd = u - dc * v, t = dd * N + v;
-#endif
-            const float pdepth = cam0.K[0] * base / (disp + (float)(d0 + dd - 30));
-            float4 tp = pl;
-            tp.w = dist2origin(cam0, px, py, pdepth, tp);
-            float tc = ncc_old_slow<F16>(a.self, px, py, v + 1, tp, rw.r, VM_P, rw.mean, rw.var);
-            if (geom) tc = fmaf(gf, geom_cost(a, px, py, v + 1, tp), tc);
-            tcL[t * VM_P + p] = tc;
-        }
-#endif
         __syncthreads();
         // ---- P2: in-order weighted view sums per (pixel, depth)
         for (int dd = wave; dd < dc; dd += VM_WAVES) {
@@ -2466,12 +2386,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, i
     for (int d0 = 0; d0 < 11; d0 += chunk) {
         const int dc = min(chunk, 11 - d0);
         uint64_t defer = 0;
-        const int cn = (dc * N + VM_WAVES - 1) / VM_WAVES, u0 = wave * cn, u1 = min(u0 + cn, dc * N);
-#ifdef APD_TASK_INTERLEAVE
         for (int u = wave, k = 0; u < dc * N; u += VM_WAVES, ++k) {
-#else
-        for (int u = u0, k = 0; u < u1; ++u, ++k) {
-#endif
             const int v = u / dc, dd = u - dc * v, t = dd * N + v;
             const int d = d0 + dd - 5;
             const float pdepth = cam0.K[0] * base / (disp + (float)d);
@@ -2491,11 +2406,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, i
         while (defer) {
             const int k = __builtin_ctzll(defer);
             defer &= defer - 1;
-#ifdef APD_TASK_INTERLEAVE
             const int u = wave + k * VM_WAVES, v = u / dc, dd = u - dc * v, t = dd * N + v;
-#else
-            const int u = u0 + k, v = u / dc, dd = u - dc * v, t = dd * N + v;
-#endif
             const float pdepth = cam0.K[0] * base / (disp + (float)(d0 + dd - 5));
             float4 tp = pl;
             tp.w = dist2origin(cam0, px, py, pdepth, tp);
