@@ -1361,6 +1361,44 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const WvLdsT<F16> 
     }
 }
 
+// NCC-New reference side of pixel slot p (APD.cu:448-575): the 9 windows' reference taps, SA tap
+// masks and moments; wave w builds windows w, w + VM_WAVES, ... (tap order = the reference's).
+template <bool F16>
+__device__ __forceinline__ void wv_build_windows(const Args &a, WvLdsT<F16> &L, int p, const APD_G short2 *anc, int cid,
+                                                 int wave) {
+    const bool use_sa = cid != 0;
+    const int p1 = p;
+    for (int k = wave; k < 9; k += VM_WAVES) {
+        const short2 ap = anc[k];
+        if (ap.x == -1 || ap.y == -1) continue;
+        const int ax = ap.x, ay = ap.y;
+        const int n1 = (k == 0) ? 6 : 3, inc = (k == 0) ? 2 : 5;
+        const int tap0 = (k == 0) ? 0 : 36 + 9 * (k - 1);
+        float sr = 0.0f, srr = 0.0f, ws = 0.0f;
+        uint64_t mask = 0;
+        for (int i = 0; i < n1; ++i)
+            for (int j = 0; j < n1; ++j) {
+                const int rx = ax - 5 + inc * i, ry = ay - 5 + inc * j;
+                const int tk = i * n1 + j;
+                if (use_sa && sa_at_dev(a, rx, ry) != cid) {
+                    L.rref[(tap0 + tk) * VM_P + p1] = 0.0f;
+                    continue;
+                }
+                const float r = tex_ref(a, rx, ry);
+                L.rref[(tap0 + tk) * VM_P + p1] = r;
+                mask |= 1ull << tk;
+                sr += r;
+                srr = fmaf(r, r, srr);
+                ws += 1.0f;
+            }
+        L.wsr[k * VM_P + p1] = sr;
+        L.wsrr[k * VM_P + p1] = srr;
+        L.wsum[k * VM_P + p1] = (uint8_t)ws;
+        if (k == 0) L.tmask0[p1] = mask;
+        else L.tmask[(k - 1) * VM_P + p1] = (uint16_t)mask;
+    }
+}
+
 // ComputeBilateralNCCNew + Softmax focal weighting (APD.cu:448-593, 431-446) for pixel slot p, source
 // view s, plane pl, with the reference side from WvLds. Called by every lane of the wave (converged);
 // `want` = the lane evaluates this task. Same operations, in the same order, as ncc_new.
@@ -1492,36 +1530,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             L.flags[p1] = hflag | (awin << 16);
             L.hyp[8 * VM_P + p1] = a.plane[c1];
         }
-        // reference windows: wave w builds windows w, w + VM_WAVES, ... (tap order = the reference's)
-        for (int k = wave; k < 9; k += VM_WAVES) {
-            const short2 ap = anc[k];
-            if (ap.x == -1 || ap.y == -1) continue;
-            const int ax = ap.x, ay = ap.y;
-            const int n1 = (k == 0) ? 6 : 3, inc = (k == 0) ? 2 : 5;
-            const int tap0 = (k == 0) ? 0 : 36 + 9 * (k - 1);
-            float sr = 0.0f, srr = 0.0f, ws = 0.0f;
-            uint64_t mask = 0;
-            for (int i = 0; i < n1; ++i)
-                for (int j = 0; j < n1; ++j) {
-                    const int rx = ax - 5 + inc * i, ry = ay - 5 + inc * j;
-                    const int tk = i * n1 + j;
-                    if (use_sa && sa_at_dev(a, rx, ry) != cid) {
-                        L.rref[(tap0 + tk) * VM_P + p1] = 0.0f;
-                        continue;
-                    }
-                    const float r = tex_ref(a, rx, ry);
-                    L.rref[(tap0 + tk) * VM_P + p1] = r;
-                    mask |= 1ull << tk;
-                    sr += r;
-                    srr = fmaf(r, r, srr);
-                    ws += 1.0f;
-                }
-            L.wsr[k * VM_P + p1] = sr;
-            L.wsrr[k * VM_P + p1] = srr;
-            L.wsum[k * VM_P + p1] = (uint8_t)ws;
-            if (k == 0) L.tmask0[p1] = mask;
-            else L.tmask[(k - 1) * VM_P + p1] = (uint16_t)mask;
-        }
+        wv_build_windows<F16>(a, L, p1, anc, cid, wave);
     }
     __syncthreads();
 
@@ -2188,12 +2197,21 @@ struct RiLds {
     float refw[36 * VM_P];
     float4 pl[VM_P];
 };
-static inline size_t ri_lds_bytes(int N) { return sizeof(RiLds) + (size_t)N * VM_P * sizeof(float); }
+// RandomInitialization when use_APD: the WEAK pixels' NCC-New through ncc_new_vm (reference side
+// built once per pixel in LDS, as in the Weak sweep) instead of the per-call ncc_new
 template <bool F16>
+struct RiApdLds {
+    WvLdsT<F16> w;
+    RiLds r;
+};
+static inline size_t ri_lds_bytes(int N) { return sizeof(RiLds) + (size_t)N * VM_P * sizeof(float); }
+template <bool F16, bool APD>
 __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, int tw) {
     const int N = a.N;
-    RiLds &L = *reinterpret_cast<RiLds *>(apd_dyn_lds);
-    float *cvL = reinterpret_cast<float *>(&L + 1);  // [N][64]
+    WvLdsT<F16> *W = APD ? &reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds)->w : nullptr;
+    RiLds &L = APD ? reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds)->r : *reinterpret_cast<RiLds *>(apd_dyn_lds);
+    float *cvL = APD ? reinterpret_cast<float *>(reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds) + 1)
+                     : reinterpret_cast<float *>(&L + 1);  // [N][64]
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (WAVE - 1);
     const TilePix T = tile_pix(a, tw, lane);
     const int p = lane, px = T.px, py = T.py, c = T.c;
@@ -2217,6 +2235,23 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, in
             const int i = k / 6, j = k - 6 * (k / 6);
             L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
         }
+        if constexpr (APD) {
+            if (a.weak[c] == APD_WEAK) {  // the NCC-New reference side (anchors, windows, SA masks)
+                const APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
+                const int cid = a.sa_any ? a.sa[c] : 0;
+                if (wave == 0) {
+                    uint32_t awin = 0;
+                    for (int k = 0; k < 9; ++k) {
+                        const short2 ap = anc[k];
+                        const bool ok = !(ap.x == -1 || ap.y == -1);
+                        W->anc[k * VM_P + p] = ok ? ((int)(uint16_t)ap.x | ((int)ap.y << 16)) : -1;
+                        if (ok && !(cid != 0 && sa_at_dev(a, ap.x, ap.y) != cid)) awin |= 1u << k;
+                    }
+                    W->flags[p] = awin << 16;
+                }
+                wv_build_windows<F16>(a, *W, p, anc, cid, wave);
+            }
+        }
     }
     __syncthreads();
     const RefWin rw = refwin_from_lds<VM_P>(&L.refw[p]);
@@ -2225,9 +2260,12 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, in
     uint64_t defer = 0;
     for (int v = wave, k = 0; v < N; v += VM_WAVES, ++k) {
         float cv = 0.0f;
+        float nv = 0.0f;
+        if constexpr (APD) nv = ncc_new_vm<F16>(a, *W, p, px, py, v + 1, pl, T.pv && use_new);  // all lanes
         if (T.pv) {
             if (use_new) {
-                cv = ncc_new<F16>(a.self, px, py, v + 1, pl);
+                if constexpr (APD) cv = nv;
+                else cv = ncc_new<F16>(a.self, px, py, v + 1, pl);
             } else {
                 bool slow;
                 cv = ncc_old_fast<F16, VM_P>(a, px, py, v + 1, pl, rw, slow);
@@ -2850,9 +2888,13 @@ apd_ctx *apd_create(int32_t device) {
                               160 * 1024);
     (void)hipFuncSetAttribute((const void *)k_local_refine_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_random_init_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void *)k_random_init_vm<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_random_init_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void *)k_random_init_vm<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_random_init_vm<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_random_init_vm<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     (void)hipFuncSetAttribute((const void *)k_sweep_weak_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
@@ -3157,7 +3199,14 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
     if (ctx->sweep_vm) {
         const int tw = ctx->dw_tile_w, th = VM_P / tw;
         const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
-        LAUNCH_TEX(k_random_init_vm, dim3(nb), dim3(VM_BLOCK), ri_lds_bytes(a.N), s, a, tw);
+        if (a.use_apd) {
+            const size_t lds = (a.tex_f16 ? sizeof(RiApdLds<true>) : sizeof(RiApdLds<false>)) + (size_t)a.N * VM_P * sizeof(float);
+            if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, true>), dim3(nb), dim3(VM_BLOCK), lds, s, a, tw);
+            else hipLaunchKernelGGL((k_random_init_vm<false, true>), dim3(nb), dim3(VM_BLOCK), lds, s, a, tw);
+        } else {
+            if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, false>), dim3(nb), dim3(VM_BLOCK), ri_lds_bytes(a.N), s, a, tw);
+            else hipLaunchKernelGGL((k_random_init_vm<false, false>), dim3(nb), dim3(VM_BLOCK), ri_lds_bytes(a.N), s, a, tw);
+        }
     } else {
         LAUNCH_TEX(k_random_init, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);
     }
