@@ -533,7 +533,9 @@ struct FastTex {
         const int qx = (int)q.x, qy = (int)q.y;
         Tap t;
 #ifdef APD_ABLATE_ONEROW  // timing-only build: every tap of a wave in 1-2 texel rows, wrong values
-        t.off = ((__umul24(((uint32_t)qy >> 8) & 1u, W1) + (((uint32_t)qx >> 8) & 31u)) << SHIFT) + vbase + (W1 << (SHIFT + 8));
+        // padded rows 1..2, columns 1..32 of view s: inside the view for W >= 30 (vbase removes one row
+        // and one texel of the pitch)
+        t.off = ((__umul24((((uint32_t)qy >> 8) & 1u) + 1u, W1) + (((uint32_t)qx >> 8) & 31u) + 1u) << SHIFT) + vbase;
 #else
         t.off = ((__umul24((uint32_t)qy >> 8, W1) + ((uint32_t)qx >> 8)) << SHIFT) + vbase;
 #endif

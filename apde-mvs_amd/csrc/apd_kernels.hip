@@ -1227,26 +1227,32 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 //   P5  (candidate, view) tasks for views with weight > 0
 //   P6  lane = pixel: acceptance, writes
 // ---------------------------------------------------------------------------------------------
-// 52.2 KiB with the cost table at N = 8 (fp16 reference taps): three workgroups per CU.
+// NCC-New reference side of a pixel slot (anchors, window taps, SA tap masks, moments): shared by the
+// Weak sweep and RandomInitialization under APD
 template <bool F16>
-struct WvLdsT {
-    float4 hyp[9 * VM_P];        // [h][p]: anchor planes 1..8 (if STRONG) + current; P4 overwrites [0..4]
-                                 // with the refinement candidates (WV_CAND) after P2's last read
-    float4 pnow[VM_P];
+struct WvRefT {
     uint64_t tmask0[VM_P];       // SA tap masks (all ones without SA)
     float wsr[9 * VM_P], wsrr[9 * VM_P];  // per window moments over its valid taps
     int anc[9 * VM_P];           // packed (x, y) of anchors 0..8, -1 = none
-    float st[4 * VM_P];          // depth_now, cost_now, cost_init, weight norm
     uint32_t flags[VM_P];        // bits 0-8: hypothesis h present (anchor STRONG); 16-24: window k evaluated
                                  // (anchor present and SA label matches); 31: refine (fit normal != 0)
     // [tap][p]: window 0 taps 0..35 (6x6, step 2), anchor k taps 36+9(k-1).. (3x3, step 5); fp16 when
     // the images are (exactly) fp16-representable, see apd_set_problem
     typename std::conditional<F16, _Float16, float>::type rref[108 * VM_P];
     uint16_t tmask[8 * VM_P];
-    uint16_t rng_n[VM_P];
     uint8_t wsum[9 * VM_P];      // valid taps per window (<= 36)
 };
+// the Weak sweep's per-workgroup state: the reference side plus the hypotheses and per-pixel state
+template <bool F16>
+struct WvLdsT : WvRefT<F16> {
+    float4 hyp[9 * VM_P];        // [h][p]: anchor planes 1..8 (if STRONG) + current; P4 overwrites [0..4]
+                                 // with the refinement candidates (WV_CAND) after P2's last read
+    float4 pnow[VM_P];
+    float st[4 * VM_P];          // depth_now, cost_now, cost_init, weight norm
+    uint16_t rng_n[VM_P];
+};
 #define WV_CAND(L) ((L).hyp)
+// 52.2 KiB with the cost table at N = 8 (fp16 reference taps): three workgroups per CU.
 static_assert(sizeof(WvLdsT<true>) + 9 * 8 * VM_P * sizeof(float) + 8 * VM_P <= 53 * 1024,
               "k_sweep_weak_vm at N = 8 must fit three workgroups per CU (160 KiB LDS)");
 template <bool F16>
@@ -1264,7 +1270,7 @@ __device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
 // statement. Every lane of the wave executes the same instruction stream; lanes that do not need
 // this window (`live` false) run on a parked homography and discard the sums.
 template <bool F16, int NW, int INC>
-__device__ __forceinline__ void ncc_new_window(const Args &a, const WvLdsT<F16> &L, int p, int tap0, uint64_t mask,
+__device__ __forceinline__ void ncc_new_window(const Args &a, const WvRefT<F16> &L, int p, int tap0, uint64_t mask,
                                                const Hom &Hm, int ax, int ay, bool live, bool fast,
                                                const FastTex<F16, true> &T, const SrcTex<F16> &Q, float &ss,
                                                float &sss, float &srs) {
@@ -1364,7 +1370,7 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const WvLdsT<F16> 
 // NCC-New reference side of pixel slot p (APD.cu:448-575): the 9 windows' reference taps, SA tap
 // masks and moments; wave w builds windows w, w + VM_WAVES, ... (tap order = the reference's).
 template <bool F16>
-__device__ __forceinline__ void wv_build_windows(const Args &a, WvLdsT<F16> &L, int p, const APD_G short2 *anc, int cid,
+__device__ __forceinline__ void wv_build_windows(const Args &a, WvRefT<F16> &L, int p, const APD_G short2 *anc, int cid,
                                                  int wave) {
     const bool use_sa = cid != 0;
     const int p1 = p;
@@ -1403,7 +1409,7 @@ __device__ __forceinline__ void wv_build_windows(const Args &a, WvLdsT<F16> &L, 
 // view s, plane pl, with the reference side from WvLds. Called by every lane of the wave (converged);
 // `want` = the lane evaluates this task. Same operations, in the same order, as ncc_new.
 template <bool F16>
-__device__ __forceinline__ float ncc_new_vm(const Args &a, const WvLdsT<F16> &L, int p, int px, int py, int s, float4 pl,
+__device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L, int p, int px, int py, int s, float4 pl,
                                             bool want) {
     const int W = a.W, H = a.H;
     const Hom Hm = homography(a, s, pl);
@@ -2201,14 +2207,18 @@ struct RiLds {
 // built once per pixel in LDS, as in the Weak sweep) instead of the per-call ncc_new
 template <bool F16>
 struct RiApdLds {
-    WvLdsT<F16> w;
+    WvRefT<F16> w;
     RiLds r;
 };
-static inline size_t ri_lds_bytes(int N) { return sizeof(RiLds) + (size_t)N * VM_P * sizeof(float); }
+// dynamic LDS of k_random_init_vm<F16, APD>: the layout struct, then the [N][64] cost table
+template <bool F16, bool APD>
+static inline size_t ri_lds_bytes(int N) {
+    return (APD ? sizeof(RiApdLds<F16>) : sizeof(RiLds)) + (size_t)N * VM_P * sizeof(float);
+}
 template <bool F16, bool APD>
 __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, int tw) {
     const int N = a.N;
-    WvLdsT<F16> *W = APD ? &reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds)->w : nullptr;
+    WvRefT<F16> *W = APD ? &reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds)->w : nullptr;
     RiLds &L = APD ? reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds)->r : *reinterpret_cast<RiLds *>(apd_dyn_lds);
     float *cvL = APD ? reinterpret_cast<float *>(reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds) + 1)
                      : reinterpret_cast<float *>(&L + 1);  // [N][64]
@@ -2870,7 +2880,11 @@ apd_ctx *apd_create(int32_t device) {
     }
     for (auto &e : ctx->ev) (void)hipEventCreate(&e);
     ctx->sweep_vm = getenv("APD_SWEEP_LANES") == nullptr;
-    if (const char *e = getenv("APD_DW_TILE_W")) ctx->dw_tile_w = std::max(1, std::min(64, atoi(e)));
+    // tile_pix needs the tile width to divide the 64-pixel tile (otherwise two workgroups share pixels)
+    if (const char *e = getenv("APD_DW_TILE_W")) {
+        const int t = atoi(e);
+        if (t == 1 || t == 2 || t == 4 || t == 8 || t == 16 || t == 32 || t == 64) ctx->dw_tile_w = t;
+    }
     if (const char *e = getenv("APD_TILE_W")) {
         const int t = atoi(e);
         if (t == 4 || t == 8 || t == 16 || t == 32 || t == 64) ctx->tile_w = t;
@@ -3200,12 +3214,11 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         const int tw = ctx->dw_tile_w, th = VM_P / tw;
         const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
         if (a.use_apd) {
-            const size_t lds = (a.tex_f16 ? sizeof(RiApdLds<true>) : sizeof(RiApdLds<false>)) + (size_t)a.N * VM_P * sizeof(float);
-            if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, true>), dim3(nb), dim3(VM_BLOCK), lds, s, a, tw);
-            else hipLaunchKernelGGL((k_random_init_vm<false, true>), dim3(nb), dim3(VM_BLOCK), lds, s, a, tw);
+            if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, true>(a.N)), s, a, tw);
+            else hipLaunchKernelGGL((k_random_init_vm<false, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, true>(a.N)), s, a, tw);
         } else {
-            if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, false>), dim3(nb), dim3(VM_BLOCK), ri_lds_bytes(a.N), s, a, tw);
-            else hipLaunchKernelGGL((k_random_init_vm<false, false>), dim3(nb), dim3(VM_BLOCK), ri_lds_bytes(a.N), s, a, tw);
+            if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, false>(a.N)), s, a, tw);
+            else hipLaunchKernelGGL((k_random_init_vm<false, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, false>(a.N)), s, a, tw);
         }
     } else {
         LAUNCH_TEX(k_random_init, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);
