@@ -28,6 +28,7 @@
 #include <sstream>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "fusion.h"
@@ -223,6 +224,24 @@ struct ImageCache {
     }
 };
 
+// run f(0..n-1) on up to `threads` host threads
+template <class F>
+void parallel_for(size_t n, unsigned threads, F f) {
+    threads = std::max(1u, std::min<unsigned>(threads, (unsigned)n));
+    std::atomic<size_t> next{0};
+    auto body = [&] {
+        for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < threads; ++t) th.emplace_back(body);
+    body();
+    for (auto &t : th) t.join();
+}
+unsigned host_threads() {
+    const unsigned hw = std::thread::hardware_concurrency();
+    return std::max(1u, std::min(16u, hw ? hw : 4u));
+}
+
 struct Pending {  // Jacobi ordering: outputs committed at the end of the pass
     std::string path;
     Mat mat;
@@ -238,6 +257,23 @@ struct Driver {
     std::mutex pend_mu;
     std::vector<Pending> pending;
 
+    // INTER_NEAREST resizes of priors (APD.cpp:605-609, 619-625, 669-673) at a round's first pass: every
+    // problem that reads view j's map resizes the same Mat to the same size, so each (Mat, size) is
+    // resized once per pass (entries keep their source alive, so a buffer address is never reused
+    // while it is a key; cleared at every pass).
+    std::mutex fit_mu;
+    std::map<std::tuple<const uint8_t *, int, int>, std::pair<Mat, Mat>> fitted;
+    Mat fit_cached(const Mat &m, int w, int h) {
+        const auto key = std::make_tuple(m.bytes(), w, h);
+        {
+            std::lock_guard<std::mutex> g(fit_mu);
+            auto it = fitted.find(key);
+            if (it != fitted.end()) return it->second.second;
+        }
+        Mat r = resize_nearest(m, w, h);
+        std::lock_guard<std::mutex> g(fit_mu);
+        return fitted.emplace(key, std::make_pair(m, r)).first->second.second;
+    }
     void emit(const std::string &path, const Mat &m) {
         if (jacobi) {
             std::lock_guard<std::mutex> g(pend_mu);
@@ -249,10 +285,33 @@ struct Driver {
     void commit() {
         for (auto &p : pending) store->write(p.path, p.mat, flush);
         pending.clear();
+        std::lock_guard<std::mutex> g(fit_mu);
+        fitted.clear();
     }
 
     // APD::InuputInitialization + CudaSpaceInitialization + RunPatchMatch + ProcessProblem
     bool process(apd_ctx *ctx, Job &job);
+    // decode (once) and resize (once per round) every image the round's problems read, on host
+    // threads in parallel; process() then finds them in the ImageCache. Same decoder and resize, so
+    // the same pixels; a file that fails to decode is reported by process() as before.
+    void prefetch_round(int scale, const std::vector<Problem> &problems) {
+        std::vector<std::pair<int, std::string>> files;  // (id, extension of the problem naming it)
+        std::map<int, bool> seen;
+        for (const Problem &p : problems) {
+            std::vector<int> ids{p.ref_image_id};
+            ids.insert(ids.end(), p.src_image_ids.begin(), p.src_image_ids.end());
+            for (int id : ids)
+                if (!seen[id]) { seen[id] = true; files.push_back({id, p.img_ext}); }
+        }
+        parallel_for(files.size(), host_threads(), [&](size_t k) {
+            const std::string path = dense + "/images/" + format_index(files[k].first) + files[k].second;
+            auto d = images.decode(path);
+            if (!d->ok) return;
+            // every image of a problem is resized from the reference image's size (APD.cpp:567), and
+            // all images of a scan have one size (CheckImages), so (own size) is the key process() uses
+            images.image(path, scale, d->g.width, d->g.height, d->g);
+        });
+    }
 };
 
 bool Driver::process(apd_ctx *ctx, Job &job) {
@@ -322,7 +381,7 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     }
     SAY("Image size: " << width << " * " << height);
     const size_t HW = (size_t)width * height;
-    auto fit = [&](Mat m) { return (m.cols != width || m.rows != height) ? resize_nearest(m, width, height) : m; };
+    auto fit = [&](Mat m) { return (m.cols != width || m.rows != height) ? fit_cached(m, width, height) : m; };
     const auto t_img = std::chrono::steady_clock::now();
     // ---- priors (APD.cpp:592-684)
     std::vector<Mat> depths;
@@ -346,8 +405,21 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
         if (weak.empty() || conf.empty()) { SAY("Error: missing weak/confidence prior"); return false; }
         if (weak.cols != width || weak.rows != height) { SAY("resize weak info to target size"); weak = fit(weak); }
         if (conf.cols != width || conf.rows != height) { SAY("resize confidence to target size"); conf = fit(conf); }
-        anchors_map = Mat(height, width, CV_32SC1);
-        for (size_t i = 0; i < HW; ++i) anchors_map.ptr<int32_t>()[i] = weak.ptr<uint8_t>()[i] == APD_WEAK ? weak_count++ : -1;
+        // anchors_map (APD.cpp:627-640) is built on the device; the host copy only feeds --export_anchor
+        const uint8_t *wp = weak.ptr<uint8_t>();
+        if (job.export_anchor) {
+            anchors_map = Mat(height, width, CV_32SC1);
+            for (size_t i = 0; i < HW; ++i) anchors_map.ptr<int32_t>()[i] = wp[i] == APD_WEAK ? weak_count++ : -1;
+        } else {
+            const size_t chunk = 1 << 20, nc = (HW + chunk - 1) / chunk;
+            std::vector<int> part(nc, 0);
+            parallel_for(nc, host_threads(), [&](size_t b) {
+                int c = 0;
+                for (size_t i = b * chunk, e = std::min(HW, i + chunk); i < e; ++i) c += wp[i] == APD_WEAK;
+                part[b] = c;
+            });
+            for (int c : part) weak_count += c;
+        }
         if (P.use_sa) {
             const std::string sa_dir = dense + "/sa_masks";
             if (file_exists(sa_dir)) {
@@ -359,7 +431,7 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
         }
         SAY("Weak count: " << weak_count << " / " << HW << " = " << (float)weak_count / (float)HW * 100 << "%");
     }
-    std::vector<float> init_planes;
+    std::shared_ptr<uint8_t[]> init_planes;  // pooled, not zero-filled: every element is written below
     if (P.state != APD_FIRST_INIT) {
         Mat d, n;
         store->read(result_folder + "/depths.bin", d);
@@ -370,13 +442,18 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
             d = fit(d);
             n = fit(n);
         }
-        init_planes.resize(HW * 4);
-        for (size_t i = 0; i < HW; ++i) {
-            init_planes[4 * i + 0] = n.ptr<float>()[3 * i + 0];
-            init_planes[4 * i + 1] = n.ptr<float>()[3 * i + 1];
-            init_planes[4 * i + 2] = n.ptr<float>()[3 * i + 2];
-            init_planes[4 * i + 3] = d.ptr<float>()[i];
-        }
+        init_planes = pool_buffer(HW * 4 * sizeof(float));
+        float *ip = reinterpret_cast<float *>(init_planes.get());
+        const float *np_ = n.ptr<float>(), *dp = d.ptr<float>();
+        const size_t chunk = 1 << 18;
+        parallel_for((HW + chunk - 1) / chunk, host_threads(), [&](size_t b) {
+            for (size_t i = b * chunk, e = std::min(HW, i + chunk); i < e; ++i) {
+                ip[4 * i + 0] = np_[3 * i + 0];
+                ip[4 * i + 1] = np_[3 * i + 1];
+                ip[4 * i + 2] = np_[3 * i + 2];
+                ip[4 * i + 3] = dp[i];
+            }
+        });
     }
     const auto t_pri = std::chrono::steady_clock::now();
     // ---- device (CudaSpaceInitialization + RunPatchMatch)
@@ -391,7 +468,7 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     prob.cameras = cams.data();
     prob.params = P;
     prob.depths = depths.empty() ? nullptr : dep_ptrs.data();
-    prob.init_planes = init_planes.empty() ? nullptr : init_planes.data();
+    prob.init_planes = reinterpret_cast<const float *>(init_planes.get());
     prob.weak_info = P.use_APD ? weak.ptr<uint8_t>() : nullptr;
     prob.confidence = P.use_APD ? conf.ptr<uint8_t>() : nullptr;
     prob.sa_mask = (P.use_APD && !sa.empty()) ? sa.ptr<uint8_t>() : nullptr;
@@ -411,14 +488,15 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     }
     job.used_ms += ms;
     // ---- results
-    std::vector<float> planes(HW * 4);
+    std::shared_ptr<uint8_t[]> planes_buf = pool_buffer(HW * 4 * sizeof(float));  // filled by apd_get_results
+    float *planes = reinterpret_cast<float *>(planes_buf.get());
     Mat depth(height, width, CV_32FC1), normal(height, width, CV_32FC3), states(height, width, CV_8UC1),
         confidence(height, width, CV_8UC1);
     std::vector<int16_t> anchors;
     std::vector<float> curve;
     int32_t wc = 0;
     apd_outputs out{};
-    out.planes = planes.data();
+    out.planes = planes;
     out.weak_info = states.ptr<uint8_t>();
     out.confidence = confidence.ptr<uint8_t>();
     out.weak_count = &wc;
@@ -435,8 +513,15 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     const auto t_get = std::chrono::steady_clock::now();
     if (st != APD_OK) { SAY("apd_get_results failed: " << apd_last_error(ctx)); return false; }
     if (!(P.geom_consistency || P.use_APD)) memset(confidence.bytes(), 1, confidence.size_bytes());
-    apd_epilogue(width, height, planes.data(), P.depth_min, P.depth_max, depth.ptr<float>(), normal.ptr<float>(),
-                 states.ptr<uint8_t>());
+    {  // the epilogue is element-wise: row chunks on host threads
+        const int rows = 64;
+        parallel_for((size_t)(height + rows - 1) / rows, host_threads(), [&](size_t b) {
+            const int r0 = (int)b * rows, nr = std::min(rows, height - r0);
+            const size_t o = (size_t)r0 * width;
+            apd_epilogue(width, nr, planes + 4 * o, P.depth_min, P.depth_max, depth.ptr<float>() + o,
+                         normal.ptr<float>() + 3 * o, states.ptr<uint8_t>() + o);
+        });
+    }
     // ---- exports (APD.cu:2614-2626, 2649-2660); written immediately, they are not priors
     if (job.export_anchor && P.use_APD) {
         write_binmat_file(result_folder + "/anchors_map.bin", anchors_map);
@@ -545,21 +630,28 @@ int main(int argc, char **argv) {
         return -1;
     }
     for (auto &p : problems) make_dir(dense + "/APD/" + format_index(p.ref_image_id));
-    // CheckImages (main.cpp:104-127) + ComputeRoundNum (main.cpp:129-146)
+    Driver drv;
+    // CheckImages (main.cpp:104-127) + ComputeRoundNum (main.cpp:129-146). The reference decodes every
+    // reference image here and again per problem; the decodes go to the run's ImageCache instead
+    // (host threads in parallel), so the schedule below never decodes a reference image again.
     int W0 = 0, H0 = 0;
-    for (size_t i = 0; i < problems.size(); ++i) {
-        Gray8 g;
-        if (!read_gray8(dense + "/images/" + format_index(problems[i].ref_image_id) + problems[i].img_ext, g, err) ||
-            (i > 0 && (g.width != W0 || g.height != H0))) {
-            std::cout << "Images may error, check it!\n";
-            return EXIT_FAILURE;
-        }
-        W0 = g.width;
-        H0 = g.height;
-    }
     if (problems.empty()) {
         std::cout << "Images may error, check it!\n";
         return EXIT_FAILURE;
+    }
+    {
+        std::vector<std::shared_ptr<ImageCache::Decoded>> dec(problems.size());
+        parallel_for(problems.size(), host_threads(), [&](size_t i) {
+            dec[i] = drv.images.decode(dense + "/images/" + format_index(problems[i].ref_image_id) + problems[i].img_ext);
+        });
+        for (size_t i = 0; i < problems.size(); ++i) {
+            if (!dec[i]->ok || (i > 0 && (dec[i]->g.width != W0 || dec[i]->g.height != H0))) {
+                std::cout << "Images may error, check it!\n";
+                return EXIT_FAILURE;
+            }
+            W0 = dec[i]->g.width;
+            H0 = dec[i]->g.height;
+        }
     }
     std::cout << "There are " << problems.size() << " problems needed to be processed!" << std::endl;
     auto fuse = [&]() -> bool {
@@ -594,7 +686,6 @@ int main(int argc, char **argv) {
     std::cout << "Round nums: " << round_num << std::endl;
     const float geom_factor = (dataset == "TaT_a" || dataset == "TaT_i") ? 0.05f : 0.2f;
 
-    Driver drv;
     drv.dense = dense;
     drv.use_sa = use_sa;
     drv.flush = flush;
@@ -653,6 +744,7 @@ int main(int argc, char **argv) {
     const auto start = std::chrono::steady_clock::now();
     for (int i = 0; i < round_num && ok; ++i) {
         drv.images.drop_scaled();  // each round uses one scale
+        drv.prefetch_round((int)std::pow(2, round_num - 1 - i), problems);
         std::cout << "========================== Round " << i << " ==========================" << std::endl;
         std::cout << "======== iteration " << iteration_index << "========" << std::endl;
         for (auto &job : jobs) {

@@ -1,6 +1,9 @@
 // io.cpp — bin-mat / cam.txt / pair.txt I/O of the `apd` driver (see io.h for the reference lines).
 #include "io.h"
 
+#include <map>
+#include <mutex>
+
 #include <sys/stat.h>
 
 #include <cstdio>
@@ -22,6 +25,47 @@ int cv_elem_size(int type) {
         case CV_32FC3: return 12;
         default: return 0;
     }
+}
+
+namespace {
+struct BufferPool {
+    std::mutex mu;
+    std::multimap<size_t, uint8_t *> free_;
+    size_t pooled = 0;
+    static constexpr size_t kCap = (size_t)8 << 30;   // bytes kept for reuse
+    static constexpr size_t kMin = (size_t)1 << 20;   // smaller buffers use plain new/delete
+    uint8_t *take(size_t n) {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = free_.find(n);
+        if (it == free_.end()) return nullptr;
+        uint8_t *p = it->second;
+        free_.erase(it);
+        pooled -= n;
+        return p;
+    }
+    void give(uint8_t *p, size_t n) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (pooled + n <= kCap) {
+                free_.emplace(n, p);
+                pooled += n;
+                return;
+            }
+        }
+        delete[] p;
+    }
+};
+BufferPool &pool() {
+    static BufferPool *p = new BufferPool();  // never destroyed: buffers may be released at exit
+    return *p;
+}
+}  // namespace
+
+std::shared_ptr<uint8_t[]> pool_buffer(size_t bytes) {
+    if (bytes < BufferPool::kMin) return std::shared_ptr<uint8_t[]>(new uint8_t[bytes]);
+    uint8_t *p = pool().take(bytes);
+    if (!p) p = new uint8_t[bytes];
+    return std::shared_ptr<uint8_t[]>(p, [bytes](uint8_t *q) { pool().give(q, bytes); });
 }
 
 Mat resize_nearest(const Mat &m, int w, int h) {
@@ -77,7 +121,15 @@ bool MatStore::write(const std::string &path, const Mat &m, bool flush) {
         std::lock_guard<std::mutex> g(mu_);
         mats_[path] = m;
     }
-    if (flush || !cache_) {
+    if (cache_ && flush) {
+        std::lock_guard<std::mutex> g(qmu_);
+        if (!writer_.joinable()) writer_ = std::thread(&MatStore::writer_loop, this);
+        queue_.emplace_back(path, m);
+        ++inflight_;
+        qcv_.notify_one();
+        return true;
+    }
+    if (!cache_) {
         if (!write_binmat_file(path, m)) {
             std::cout << "Error opening file: \"" << path << "\"" << std::endl;
             return false;
@@ -86,7 +138,38 @@ bool MatStore::write(const std::string &path, const Mat &m, bool flush) {
     return true;
 }
 
+void MatStore::writer_loop() {
+    std::unique_lock<std::mutex> l(qmu_);
+    for (;;) {
+        qcv_.wait(l, [&] { return stop_ || !queue_.empty(); });
+        if (queue_.empty()) return;  // stop_ and drained
+        auto job = std::move(queue_.front());
+        queue_.pop_front();
+        l.unlock();
+        if (!write_binmat_file(job.first, job.second))
+            std::cout << "Error opening file: \"" << job.first << "\"" << std::endl;
+        job.second = Mat();
+        l.lock();
+        if (--inflight_ == 0) qdone_.notify_all();
+    }
+}
+
+void MatStore::drain() {
+    std::unique_lock<std::mutex> l(qmu_);
+    qdone_.wait(l, [&] { return inflight_ == 0; });
+}
+
+MatStore::~MatStore() {
+    {
+        std::lock_guard<std::mutex> g(qmu_);
+        stop_ = true;
+        qcv_.notify_all();
+    }
+    if (writer_.joinable()) writer_.join();
+}
+
 void MatStore::flush_all() {
+    drain();
     std::lock_guard<std::mutex> g(mu_);
     for (auto &kv : mats_) write_binmat_file(kv.first, kv.second);
     mats_.clear();

@@ -9,6 +9,9 @@
 #include <mutex>
 #include <string>
 #include <vector>
+#include <condition_variable>
+#include <deque>
+#include <thread>
 
 #include "../../include/apd_hip.h"
 
@@ -20,16 +23,23 @@ int cv_elem_size(int type);
 
 // Pixels are reference-counted like a cv::Mat's: copying a Mat (MemoryCache reads and writes,
 // priors) shares the buffer instead of copying hundreds of MB per problem. Every writer fills a
-// freshly constructed Mat, so sharing never exposes a partial write.
+// freshly constructed Mat, so sharing never exposes a partial write. Like cv::Mat::create, the
+// buffer is not zero-filled (every writer fills all of it; a 3024x2016 problem's four result Mats
+// would otherwise cost ~100 MB of memset).
+// Large host buffers come from a process-wide pool: a released buffer is kept (up to a byte cap)
+// and handed to the next request of the same size, so the per-problem result Mats and staging
+// buffers of a scan reuse resident pages instead of faulting in (and zeroing) fresh ones.
+std::shared_ptr<uint8_t[]> pool_buffer(size_t bytes);
 struct Mat {
     int rows = 0, cols = 0, type = CV_8UC1;
-    std::shared_ptr<std::vector<uint8_t>> buf;  // row-major, rows * cols * elem bytes
+    size_t nbytes = 0;
+    std::shared_ptr<uint8_t[]> buf;  // row-major, rows * cols * elem bytes
     Mat() = default;
     Mat(int r, int c, int t)
-        : rows(r), cols(c), type(t), buf(std::make_shared<std::vector<uint8_t>>((size_t)r * c * cv_elem_size(t))) {}
-    uint8_t *bytes() { return buf ? buf->data() : nullptr; }
-    const uint8_t *bytes() const { return buf ? buf->data() : nullptr; }
-    size_t size_bytes() const { return buf ? buf->size() : 0; }
+        : rows(r), cols(c), type(t), nbytes((size_t)r * c * cv_elem_size(t)), buf(pool_buffer(nbytes)) {}
+    uint8_t *bytes() { return buf.get(); }
+    const uint8_t *bytes() const { return buf.get(); }
+    size_t size_bytes() const { return buf ? nbytes : 0; }
     template <class T> T *ptr() { return reinterpret_cast<T *>(bytes()); }
     template <class T> const T *ptr() const { return reinterpret_cast<const T *>(bytes()); }
     bool empty() const { return rows == 0 || cols == 0; }
@@ -38,18 +48,31 @@ Mat resize_nearest(const Mat &m, int w, int h);
 
 // MemoryCache (APD.cpp:3-16): when enabled, bin-mat writes land in memory and reach the disk only
 // when flushed; reads check the cache first. Thread-safe.
+// With the cache on, a flushed write (--flush / --no_fuse) only persists a Mat that every read is
+// served from memory anyway, so the file is written by a background thread (in submission order;
+// drained by flush_all and the destructor) instead of on the problem's critical path. Without the
+// cache, reads come from the files and writes stay synchronous.
 class MatStore {
 public:
     explicit MatStore(bool cache) : cache_(cache) {}
+    ~MatStore();
     bool read(const std::string &path, Mat &m);                    // ReadBinMat   APD.cpp:18-56
     bool write(const std::string &path, const Mat &m, bool flush);  // WriteBinMat  APD.cpp:58-83
     void flush_all();                                              // main.cpp:381-393
+    void drain();                                                  // wait for queued file writes
     bool cached() const { return cache_; }
 
 private:
+    void writer_loop();
     bool cache_;
     std::mutex mu_;
     std::map<std::string, Mat> mats_;
+    std::mutex qmu_;
+    std::condition_variable qcv_, qdone_;
+    std::deque<std::pair<std::string, Mat>> queue_;
+    size_t inflight_ = 0;
+    bool stop_ = false;
+    std::thread writer_;
 };
 
 bool read_binmat_file(const std::string &path, Mat &m);
