@@ -1269,10 +1269,11 @@ __device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
 // `fast` = window_rcp_ok for this lane (Newton reciprocal + packed taps); otherwise the IEEE
 // statement. Every lane of the wave executes the same instruction stream; lanes that do not need
 // this window (`live` false) run on a parked homography and discard the sums.
+// Reference taps: tap tk of the window at rb[tk * rs] (WvRefT: &rref[tap0 * VM_P + p], VM_P).
 template <bool F16, int NW, int INC>
-__device__ __forceinline__ void ncc_new_window(const Args &a, const WvRefT<F16> &L, int p, int tap0, uint64_t mask,
-                                               const Hom &Hm, int ax, int ay, bool live, bool fast,
-                                               const FastTex<F16, true> &T, const SrcTex<F16> &Q, float &ss,
+__device__ __forceinline__ void ncc_new_window(const Args &a, const typename std::conditional<F16, _Float16, float>::type *rb,
+                                               int rs, uint64_t mask, const Hom &Hm, int ax, int ay, bool live,
+                                               bool fast, const FastTex<F16, true> &T, const SrcTex<F16> &Q, float &ss,
                                                float &sss, float &srs) {
     const uint64_t sm = __ballot(live && !fast);
     // only the lanes whose window is evaluated issue its gathers (the gather path's cost is per
@@ -1297,7 +1298,7 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const WvRefT<F16> 
                 const int tk = i * NW + j;
                 const float v = T.finish(t[j], q[j]);
                 if ((mask >> tk) & 1ull) {
-                    const float r = L.rref[(tap0 + tk) * VM_P + p];
+                    const float r = rb[tk * rs];
                     ss += v;
                     sss = fmaf(v, v, sss);
                     srs = fmaf(r, v, srs);
@@ -1358,7 +1359,7 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const WvRefT<F16> 
                 const float iz = 1.0f / Z;
                 const QuadTap t = quad_tap(Wm1, Hm1, W1, X * iz, Y * iz);
                 const float v = bilerp(Q.fetch(t.idx), t.ax, t.ay);
-                const float r = L.rref[(tap0 + tk) * VM_P + p];
+                const float r = rb[tk * rs];
                 ss += v;
                 sss = fmaf(v, v, sss);
                 srs = fmaf(r, v, srs);
@@ -1451,9 +1452,9 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
         const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
         float ss = 0.0f, sss = 0.0f, srs = 0.0f;
         if (k == 0)
-            ncc_new_window<F16, 6, 2>(a, L, p, 0, L.tmask0[p], Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            ncc_new_window<F16, 6, 2>(a, &L.rref[p], VM_P, L.tmask0[p], Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
         else
-            ncc_new_window<F16, 3, 5>(a, L, p, 36 + 9 * (k - 1), (uint64_t)L.tmask[(k - 1) * VM_P + p], Hm, ax, ay,
+            ncc_new_window<F16, 3, 5>(a, &L.rref[(36 + 9 * (k - 1)) * VM_P + p], VM_P, (uint64_t)L.tmask[(k - 1) * VM_P + p], Hm, ax, ay,
                                       live, fast, T, Q, ss, sss, srs);
         if (!live) continue;
         const float wsum = (float)L.wsum[k * VM_P + p];
@@ -1495,7 +1496,7 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
 #endif
 template <bool F16>
 __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
-                                                                int iter) {
+                                                                int iter, const float *__restrict__ cand) {
     const int N = a.N, W = a.W;
     WvLdsT<F16> &L = *reinterpret_cast<WvLdsT<F16> *>(apd_dyn_lds);
     float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64], later [5][N][64]
@@ -1540,11 +1541,17 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     }
     __syncthreads();
 
-    // ---- P1: (hypothesis, view) tasks
+    // ---- P1: (hypothesis, view) tasks; with `cand` (k_weak_cand_vm ran on this list) the anchor
+    // candidates' costs are read, and only the current plane is evaluated here
     for (int u = wave; u < 9 * N; u += VM_WAVES) {  // view-major: the 4 waves share a source image
         const int v = u / 9, h = u - 9 * v, t = h * N + v;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
         const bool want = pv1 && (h == 8 || ((L.flags[p1] >> h) & 1u));
+        if (cand && h < 8) {
+            if (want) val = cand[((size_t)v * 8 + h) * (size_t)count + first + p1];
+            costL[t * VM_P + p1] = val;
+            continue;
+        }
         const float4 pl = L.hyp[h * VM_P + p1];
         const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want);
         if (want) {
@@ -1741,6 +1748,444 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
                 a.plane[c1] = pnow;
             }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Candidate costs of the Weak sweep with the anchor windows shared across pixels (no SA masks).
+// For a WEAK pixel, candidate h is the plane of its STRONG anchor h+1, and ComputeBilateralNCCNew
+// (APD.cu:448-593) of that plane is the centre window (at anchor 0, pixel-specific) combined by the
+// focal softmax with the 3x3 windows at anchors 1..8. Without SA masks an anchor window's cost is a
+// function of (window anchor, candidate plane, view) only -- the out-of-frame rule reads the
+// anchor's selected_views, which only the Strong sweep writes -- and neighbouring WEAK pixels share
+// anchors: a 64-pixel group at 3024x2016 (N = 8) holds ~1.8k distinct (window anchor, candidate
+// anchor) pairs of ~4.0k evaluations (2.2x; 2.6x at 6048x4032). This kernel evaluates every
+// distinct pair once per view, the centre windows per pixel, and writes each (candidate, view,
+// pixel) cost -- bit-identical to ncc_new_vm (same statements, same softmax order) -- for the
+// sweep's P1, which then evaluates only the current plane.
+//   A/B  hash the group's anchors 1..8 into distinct ids (deterministic slot order), build their
+//        3x3 reference windows and the pixels' 6x6 centre windows (wv_build_windows's statements)
+//   C    hash the (window anchor, candidate anchor) pairs, pair ids in slot order
+//   D    per view: pair windows (lane = pair), centre windows (lane = pixel), then per (candidate,
+//        pixel) the focal combination in anchor order
+// ---------------------------------------------------------------------------------------------
+#define PK_D 512    // distinct anchors per group (<= 8 per pixel)
+#define PK_P 4096   // distinct pairs per group (<= 64 per pixel)
+#define PK_AH 1024  // anchor hash slots
+#define PK_NONE 0xFFFFu
+#ifndef PK_WAVES
+#define PK_WAVES 8  // 8-wave workgroups: 2 per CU (LDS) still give 16 waves per CU
+#endif
+#define PK_BLOCK (PK_WAVES * WAVE)
+template <bool F16>
+struct PkLds {
+    using RT = typename std::conditional<F16, _Float16, float>::type;
+    union {
+        int hash[PK_P];             // C: pair key + 1 (19 bits) | pair id << 19
+        float pcost[PK_P];          // D: per-view pair cost (< 0: window absent)
+    } u;
+    uint32_t plist[PK_P];           // pair id -> window anchor id | candidate anchor id << 16
+    uint16_t pidx[64 * VM_P];       // [h * 8 + k - 1][p]: pair id of (anchor k window, candidate h)
+    RT aref[9 * PK_D];              // [tap][d] anchor window reference taps
+    float4 apl[PK_D];               // plane of anchor d (candidates)
+    int apos[PK_D];                 // packed (x, y) of anchor d
+    float asr[PK_D], asrr[PK_D];    // window moments
+    int ahash[PK_AH];               // anchor hash: packed position + 1 (0 = empty)
+    RT cref[36 * VM_P];             // [tap][p] centre window reference taps
+    float csr[VM_P], csrr[VM_P];
+    float ccost[8 * VM_P];          // [h][p] centre window cost of candidate h (per view)
+    uint16_t aid[8 * VM_P];         // [k-1][p]: id of anchor k, PK_NONE if invalid
+    int anc0[VM_P];                 // packed anchor 0, -1 if invalid
+    uint8_t astrong[PK_D], aws[PK_D];
+    uint8_t cws[VM_P];
+    uint8_t cand[VM_P];             // bit h: candidate h present (anchor h+1 valid and STRONG)
+    uint8_t cstat[8 * VM_P];        // [h][p]: bit 0 dead (centre or its anchor out of frame), bit 1 centre window present
+    int kcnt[PK_D];                 // pairs per window anchor, then their offsets
+    int scan[PK_BLOCK / WAVE + 1];
+    int nD, nP;
+};
+template <bool F16>
+static inline size_t pk_lds_bytes() { return sizeof(PkLds<F16>); }
+
+// anchors are packed as x | y << 16 with x, y < 32768: hash keys are that + 1 (0 = empty slot)
+__device__ __forceinline__ uint32_t pk_mix(uint32_t k) {
+    k ^= k >> 15;
+    k *= 0x2C1B3C6Du;
+    k ^= k >> 12;
+    return k;
+}
+// Block-wide ordered compaction of hash slots: every thread owns `per` consecutive slots; returns
+// the id of slot (tid * per + i) through ids[] (valid where the slot is used) and the total.
+template <int PER>
+__device__ __forceinline__ int pk_compact(const bool (&used)[PER], int (&ids)[PER], int *scan_lds) {
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid >> 6;
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) cnt += used[i];
+    // inclusive scan over the wave, then over the waves
+    int x = cnt;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == WAVE - 1) scan_lds[wave] = x;
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < wave; ++w) base += scan_lds[w];
+    int total = 0;
+    for (int w = 0; w < PK_BLOCK / WAVE; ++w) total += scan_lds[w];
+    int next = base + x - cnt;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        ids[i] = next;
+        next += used[i];
+    }
+    __syncthreads();
+    return total;
+}
+
+template <bool F16>
+__global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a, const int *__restrict__ list, int count,
+                                                           float *__restrict__ out) {
+    const int N = a.N, W = a.W, H = a.H;
+    PkLds<F16> &L = *reinterpret_cast<PkLds<F16> *>(apd_dyn_lds);
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int first = blk * VM_P;
+    const int np = min(VM_P, count - first);
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
+    const int p1 = lane;
+    const bool pv1 = p1 < np;
+    const int c1 = list[first + min(p1, np - 1)];
+    const int py1 = c1 / W, px1 = c1 - py1 * W;
+
+    // ---- A: anchors into the hash
+    for (int i = tid; i < PK_P; i += PK_BLOCK) L.u.hash[i] = 0;
+    for (int i = tid; i < PK_AH; i += PK_BLOCK) L.ahash[i] = 0;
+    __syncthreads();
+    const APD_G short2 *anc1 = a.anchors + (size_t)a.amap[c1] * 9;
+    if (pv1 && wave == 0) {
+        const short2 a0 = anc1[0];
+        L.anc0[p1] = (a0.x == -1 || a0.y == -1) ? -1 : ((int)(uint16_t)a0.x | ((int)a0.y << 16));
+    }
+    if (pv1 && wave < 2) {  // waves 0/1: anchors 1-4 / 5-8
+        for (int k = 1 + 4 * wave; k < 5 + 4 * wave; ++k) {
+            const short2 ap = anc1[k];
+            if (ap.x == -1 || ap.y == -1) continue;
+            const int key = ((int)(uint16_t)ap.x | ((int)ap.y << 16)) + 1;
+            uint32_t slot = pk_mix((uint32_t)key) & (PK_AH - 1);
+            for (;;) {
+                const int old = atomicCAS(&L.ahash[slot], 0, key);
+                if (old == 0 || old == key) break;
+                slot = (slot + 1) & (PK_AH - 1);
+            }
+        }
+    }
+    __syncthreads();
+    // ---- B: anchor ids in raster order of the anchors (bitonic sort of the group's keys), so the
+    // pairs of one window anchor, and of nearby ones, take neighbouring lanes (gather locality);
+    // their windows; the pixels' centre windows
+    {
+        constexpr int PER = PK_AH / PK_BLOCK;
+        bool used[PER];
+        int ids[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) used[i] = L.ahash[tid * PER + i] != 0;
+        const int nd = pk_compact<PER>(used, ids, L.scan);
+        int *keys = reinterpret_cast<int *>(L.plist);  // plist is free until C: keys[0..511] sorted
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+            if (used[i]) keys[ids[i]] = L.ahash[tid * PER + i];
+        for (int i = nd + tid; i < PK_D; i += PK_BLOCK) keys[i] = 0x7FFFFFFF;
+        if (tid == 0) L.nD = nd;
+        __syncthreads();
+        for (int k = 2; k <= PK_D; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = tid; i < PK_D; i += PK_BLOCK) {
+                    const int ixj = i ^ j;
+                    if (ixj > i) {
+                        const int x = keys[i], y = keys[ixj];
+                        if (((i & k) == 0) == (x > y)) { keys[i] = y; keys[ixj] = x; }
+                    }
+                }
+                __syncthreads();
+            }
+        // slot -> id (binary search of the slot's key), kept in plist[PK_D + slot]
+        int *slot_id = keys + PK_D;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int key = L.ahash[tid * PER + i];
+            int id = PK_NONE;
+            if (key != 0) {
+                int lo = 0, hi = nd - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (keys[mid] < key) lo = mid + 1; else hi = mid;
+                }
+                id = lo;
+            }
+            slot_id[tid * PER + i] = id;
+        }
+        for (int d = tid; d < nd; d += PK_BLOCK) L.apos[d] = keys[d] - 1;
+    }
+    __syncthreads();
+    if (pv1 && wave < 2) {
+        for (int k = 1 + 4 * wave; k < 5 + 4 * wave; ++k) {
+            const short2 ap = anc1[k];
+            uint16_t id = PK_NONE;
+            if (!(ap.x == -1 || ap.y == -1)) {
+                const int key = ((int)(uint16_t)ap.x | ((int)ap.y << 16)) + 1;
+                uint32_t slot = pk_mix((uint32_t)key) & (PK_AH - 1);
+                while (L.ahash[slot] != key) slot = (slot + 1) & (PK_AH - 1);
+                id = (uint16_t)L.plist[PK_D + slot];
+            }
+            L.aid[(k - 1) * VM_P + p1] = id;
+        }
+    }
+    const int nD = L.nD;
+    for (int d = tid; d < nD; d += PK_BLOCK) {  // distinct anchor windows (wv_build_windows, k >= 1, no SA)
+        const int pk = L.apos[d];
+        const int ax = pk & 0xFFFF, ay = pk >> 16;
+        const int q = ax + ay * W;
+        L.astrong[d] = a.weak[q] == APD_STRONG;
+        L.apl[d] = a.plane[q];
+        float sr = 0.0f, srr = 0.0f, ws = 0.0f;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                const float r = tex_ref(a, ax - 5 + 5 * i, ay - 5 + 5 * j);
+                L.aref[(i * 3 + j) * PK_D + d] = r;
+                sr += r;
+                srr = fmaf(r, r, srr);
+                ws += 1.0f;
+            }
+        L.asr[d] = sr;
+        L.asrr[d] = srr;
+        L.aws[d] = (uint8_t)ws;
+    }
+    if (pv1 && wave == 2) {  // centre windows (k = 0: 6x6, step 2)
+        const int pk = L.anc0[p1];
+        float sr = 0.0f, srr = 0.0f, ws = 0.0f;
+        if (pk >= 0) {
+            const int ax = pk & 0xFFFF, ay = pk >> 16;
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j < 6; ++j) {
+                    const float r = tex_ref(a, ax - 5 + 2 * i, ay - 5 + 2 * j);
+                    L.cref[(i * 6 + j) * VM_P + p1] = r;
+                    sr += r;
+                    srr = fmaf(r, r, srr);
+                    ws += 1.0f;
+                }
+        }
+        L.csr[p1] = sr;
+        L.csrr[p1] = srr;
+        L.cws[p1] = (uint8_t)ws;
+    }
+    __syncthreads();
+    // ---- C: candidate bits, pairs into the hash
+    if (pv1 && wave == 3) {
+        uint32_t cb = 0;
+        for (int h = 0; h < 8; ++h) {
+            const uint16_t id = L.aid[h * VM_P + p1];
+            if (id != PK_NONE && L.astrong[id]) cb |= 1u << h;
+        }
+        L.cand[p1] = (uint8_t)cb;
+    }
+    __syncthreads();
+    if (pv1) {
+        const uint32_t cb = L.cand[p1];
+        for (int h = wave; h < 8; h += PK_WAVES) {
+            if (!((cb >> h) & 1u)) continue;
+            const uint32_t hid = L.aid[h * VM_P + p1];
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t kid = L.aid[k * VM_P + p1];
+                if (kid == PK_NONE) continue;
+                const int key = (int)(kid | (hid << 9)) + 1;  // <= 2^18
+                uint32_t slot = pk_mix((uint32_t)key) & (PK_P - 1);
+                for (;;) {
+                    const int old = atomicCAS(&L.u.hash[slot], 0, key);
+                    if (old == 0 || old == key) break;
+                    slot = (slot + 1) & (PK_P - 1);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // pair ids ordered by window anchor (counting sort; the order inside one anchor's run does not
+    // matter: a pair id only labels a window cost)
+    for (int d = tid; d < PK_D; d += PK_BLOCK) L.kcnt[d] = 0;
+    __syncthreads();
+    {
+        constexpr int PER = PK_P / PK_BLOCK;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int hv = L.u.hash[tid * PER + i];
+            if (hv != 0) {
+                const int r = atomicAdd(&L.kcnt[(hv - 1) & 511], 1);
+                L.u.hash[tid * PER + i] = hv | (r << 19);
+            }
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {  // exclusive scan of the 512 anchor counts, 8 per lane
+        int c[8], sum = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { c[i] = L.kcnt[lane * 8 + i]; sum += c[i]; }
+        int x = sum;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        int off = x - sum;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { L.kcnt[lane * 8 + i] = off; off += c[i]; }
+        if (lane == WAVE - 1) L.nP = x;
+    }
+    __syncthreads();
+    {
+        constexpr int PER = PK_P / PK_BLOCK;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int hv = L.u.hash[tid * PER + i];
+            if (hv != 0) {
+                const int key = (hv & 0x7FFFF) - 1, r = hv >> 19;
+                const int pid = L.kcnt[key & 511] + r;
+                L.plist[pid] = (uint32_t)(key & 511) | ((uint32_t)(key >> 9) << 16);
+                L.u.hash[tid * PER + i] = (key + 1) | (pid << 19);
+            }
+        }
+    }
+    __syncthreads();
+    if (pv1) {
+        const uint32_t cb = L.cand[p1];
+        for (int h = wave; h < 8; h += PK_WAVES) {
+            const uint32_t hid = L.aid[h * VM_P + p1];
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t kid = L.aid[k * VM_P + p1];
+                uint16_t pid = PK_NONE;
+                if (((cb >> h) & 1u) && kid != PK_NONE) {
+                    const int key = (int)(kid | (hid << 9)) + 1;
+                    uint32_t slot = pk_mix((uint32_t)key) & (PK_P - 1);
+                    while ((L.u.hash[slot] & 0x7FFFF) != key) slot = (slot + 1) & (PK_P - 1);
+                    pid = (uint16_t)(L.u.hash[slot] >> 19);
+                }
+                L.pidx[(h * 8 + k) * VM_P + p1] = pid;
+            }
+        }
+    }
+    __syncthreads();
+    const int nP = L.nP;
+
+    // ---- D: per view
+    for (int v = 0; v < N; ++v) {
+        const int s = v + 1;
+        const FastTex<F16, true> T(a, s);
+        const SrcTex<F16> Q(a, s);
+        // pair windows: ComputeBilateralNCCNew's k >= 1 iteration for a live pixel (APD.cu:500-575)
+        for (int base = 0; base < nP; base += PK_BLOCK) {
+            const int pid = base + tid;
+            const bool act = pid < nP;
+            const uint32_t pr = act ? L.plist[pid] : 0u;
+            const int kid = pr & 0xFFFF, hid = pr >> 16;
+            const int pk = L.apos[kid];
+            const int ax = pk & 0xFFFF, ay = pk >> 16;
+            const Hom Hm = homography(a, s, L.apl[hid]);
+            float asx, asy;
+            project(Hm, (float)ax, (float)ay, asx, asy);
+            bool live = act;
+            float res = -1.0f;  // absent
+            if (act && (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H)) {
+                live = false;
+                if ((a.sel[ax + ay * W] >> (s - 1)) & 1u) res = APD_COST_MAX;
+            }
+            if (__ballot(live)) {
+                const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
+                float ss = 0.0f, sss = 0.0f, srs = 0.0f;
+                ncc_new_window<F16, 3, 5>(a, &L.aref[kid], PK_D, 0x1FFull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+                if (live) {
+                    const float wsum = (float)L.aws[kid];
+                    if (wsum != 0.0f) res = ncc_finalize(L.asr[kid], L.asrr[kid], ss, sss, srs, wsum);
+                }
+            }
+            if (act) L.u.pcost[pid] = res;
+        }
+        // centre windows: lane = pixel, wave = candidate
+        {
+            const uint32_t cb = pv1 ? L.cand[p1] : 0u;
+            for (int h = wave; h < 8; h += PK_WAVES) {
+                const bool want = (cb >> h) & 1u;
+                const uint16_t hid = L.aid[h * VM_P + p1];
+                const float4 pl = want ? L.apl[hid] : make_float4(0.0f, 0.0f, 1.0f, 1.0f);
+                const Hom Hm = homography(a, s, pl);
+                float ptx, pty;
+                project(Hm, (float)px1, (float)py1, ptx, pty);
+                const bool alive = want && !(ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f);
+                const int pk = L.anc0[p1];
+                const bool has = alive && pk >= 0;
+                const int ax = has ? (pk & 0xFFFF) : px1, ay = has ? (pk >> 16) : py1;
+                bool live = has, dead = !alive;
+                if (has) {
+                    float asx, asy;
+                    project(Hm, (float)ax, (float)ay, asx, asy);
+                    if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) { live = false; dead = true; }
+                }
+                float cc = 0.0f;
+                bool present = false;
+                if (__ballot(live)) {
+                    const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
+                    float ss = 0.0f, sss = 0.0f, srs = 0.0f;
+                    ncc_new_window<F16, 6, 2>(a, &L.cref[p1], VM_P, ~0ull >> 28, Hm, ax, ay, live, fast, T, Q, ss, sss,
+                                              srs);
+                    if (live) {
+                        const float wsum = (float)L.cws[p1];
+                        if (wsum != 0.0f) { cc = ncc_finalize(L.csr[p1], L.csrr[p1], ss, sss, srs, wsum); present = true; }
+                    }
+                }
+                L.ccost[h * VM_P + p1] = cc;
+                L.cstat[h * VM_P + p1] = (uint8_t)(dead ? 1 : 0) | (present ? 2 : 0);
+            }
+        }
+        __syncthreads();
+        // focal combination (APD.cu:576-593, Softmax 431-446) per (candidate, pixel)
+        if (pv1) {
+            const uint32_t cb = L.cand[p1];
+            for (int h = wave; h < 8; h += PK_WAVES) {
+                if (!((cb >> h) & 1u)) continue;
+                float cost;
+                if (L.cstat[h * VM_P + p1] & 1u) {
+                    cost = APD_COST_MAX;
+                } else {
+                    const float center_cost = L.ccost[h * VM_P + p1];
+                    float sc[8];
+                    int ns = 0;
+                    float strong_weight = 0.0f;
+                    for (int k = 0; k < 8; ++k) {
+                        const uint16_t pid = L.pidx[(h * 8 + k) * VM_P + p1];
+                        if (pid == PK_NONE) continue;
+                        const float pc = L.u.pcost[pid];
+                        if (pc < 0.0f) continue;
+                        sc[ns++] = pc;
+                        strong_weight += 1.0f;
+                    }
+                    if (strong_weight <= 1e-6f) {
+                        cost = center_cost;
+                    } else {
+                        float mx = -1e10f;
+                        for (int t = 0; t < ns; ++t) if (sc[t] > mx) mx = sc[t];
+                        float e[8];
+                        float sum = 0.0f;
+                        for (int t = 0; t < ns; ++t) { e[t] = d_expf(sc[t] - mx); sum += e[t]; }
+                        float acc = 0.0f;
+                        for (int t = 0; t < ns; ++t) { const float w = e[t] / sum; acc = fmaf(w, sc[t], acc); }
+                        acc = (acc > APD_COST_MAX) ? APD_COST_MAX : acc;
+                        cost = (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
+                    }
+                }
+                out[((size_t)v * 8 + h) * (size_t)count + first + p1] = cost;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -2715,7 +3160,7 @@ struct apd_ctx {
     std::string err;
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
-        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g;
+        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand;
     int n_near = 0;
     int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
     Args args{};
@@ -2723,6 +3168,7 @@ struct apd_ctx {
     bool sweep_vm = true;          // view-major Strong sweep (APD_SWEEP_LANES=1 selects k_sweep_strong)
     int dw_tile_w = 8;             // DepthToWeak pixel tile width (64 / tile height); APD_DW_TILE_W
     int tile_w = 8;                // sweep list tile width (tile = tile_w x 256/tile_w positions); APD_TILE_W
+    bool cand_pairs = true;        // Weak sweep candidates through k_weak_cand_vm; APD_NO_CAND_PAIRS=1 disables
     int weak_count = 0;
     int cnt[4] = {0, 0, 0, 0};     // strong black, strong red, weak black, weak red
     size_t list_cap = 0;
@@ -2880,6 +3326,7 @@ apd_ctx *apd_create(int32_t device) {
     }
     for (auto &e : ctx->ev) (void)hipEventCreate(&e);
     ctx->sweep_vm = getenv("APD_SWEEP_LANES") == nullptr;
+    ctx->cand_pairs = getenv("APD_NO_CAND_PAIRS") == nullptr;
     // tile_pix needs the tile width to divide the 64-pixel tile (otherwise two workgroups share pixels)
     if (const char *e = getenv("APD_DW_TILE_W")) {
         const int t = atoi(e);
@@ -2891,6 +3338,10 @@ apd_ctx *apd_create(int32_t device) {
     }
     // the view-major sweep's LDS grows with N (> 64 KiB from N = 15 on); gfx950 has 160 KiB per CU
     (void)hipFuncSetAttribute((const void *)k_sweep_strong_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_weak_cand_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_weak_cand_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     (void)hipFuncSetAttribute((const void *)k_sweep_strong_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
@@ -2924,7 +3375,7 @@ void apd_destroy(apd_ctx *ctx) {
     DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
-                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g};
+                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
@@ -3205,6 +3656,9 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         HIP_OK(ctx, hipMemcpyAsync(host_tot, tot, 4 * sizeof(int), hipMemcpyDeviceToHost, s));
         HIP_OK(ctx, hipStreamSynchronize(s));
         for (int i = 0; i < 4; ++i) ctx->cnt[i] = host_tot[i];
+        if (a.use_apd && ctx->sweep_vm && ctx->cand_pairs && !a.sa_any &&
+            (st = ensure(ctx, ctx->wcand, (size_t)a.N * 8 * (size_t)std::max(ctx->cnt[2], ctx->cnt[3]) * sizeof(float))))
+            return st;
         for (int i = 0; i < 4; ++i) {
             if ((st = build_tile_list(ctx, modes[i][0], modes[i][1], list_ptr(ctx, i), tot + i))) return st;
         }
@@ -3265,9 +3719,21 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
         for (int colour = 0; colour < 2; ++colour) {
             const int n = ctx->cnt[2 + colour];
             if (n <= 0) continue;
+            const float *cand = nullptr;
+            if (ctx->sweep_vm && ctx->cand_pairs && !a.sa_any) {
+                // anchor-window sharing needs no SA masks (an SA label makes a window pixel-specific)
+                if (ctx->wcand.bytes < (size_t)a.N * 8 * (size_t)n * sizeof(float)) {
+                    ctx->err = "candidate cost buffer not sized by apd_stage_prepare";
+                    return APD_ESTATE;
+                }
+                LAUNCH_TEX(k_weak_cand_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(PK_BLOCK),
+                           (ctx->args.tex_f16 ? pk_lds_bytes<true>() : pk_lds_bytes<false>()), s, a,
+                           (const int *)list_ptr(ctx, 2 + colour), n, (float *)ctx->wcand.p);
+                cand = (const float *)ctx->wcand.p;
+            }
             if (ctx->sweep_vm)
                 LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N) : wv_lds_bytes<false>(a.N)), s,
-                           a, (const int *)list_ptr(ctx, 2 + colour), n, iter);
+                           a, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand);
             else
                 LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
                            (const int *)list_ptr(ctx, 2 + colour), n, iter);
