@@ -1897,12 +1897,14 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
 #pragma unroll
         for (int i = 0; i < PER; ++i)
             if (used[i]) keys[ids[i]] = L.ahash[tid * PER + i];
-        for (int i = nd + tid; i < PK_D; i += PK_BLOCK) keys[i] = 0x7FFFFFFF;
+        int sz = 2;  // sort the next power of two >= nd (padded)
+        while (sz < nd) sz <<= 1;
+        for (int i = nd + tid; i < sz; i += PK_BLOCK) keys[i] = 0x7FFFFFFF;
         if (tid == 0) L.nD = nd;
         __syncthreads();
-        for (int k = 2; k <= PK_D; k <<= 1)
+        for (int k = 2; k <= sz; k <<= 1)
             for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = tid; i < PK_D; i += PK_BLOCK) {
+                for (int i = tid; i < sz; i += PK_BLOCK) {
                     const int ixj = i ^ j;
                     if (ixj > i) {
                         const int x = keys[i], y = keys[ixj];
@@ -2157,27 +2159,34 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
                     cost = APD_COST_MAX;
                 } else {
                     const float center_cost = L.ccost[h * VM_P + p1];
+                    // the windows present, in anchor order: a compacted list in the reference, a
+                    // presence mask here (same values, same order; no dynamically indexed arrays)
                     float sc[8];
-                    int ns = 0;
+                    uint32_t pm = 0;
                     float strong_weight = 0.0f;
+#pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         const uint16_t pid = L.pidx[(h * 8 + k) * VM_P + p1];
-                        if (pid == PK_NONE) continue;
-                        const float pc = L.u.pcost[pid];
-                        if (pc < 0.0f) continue;
-                        sc[ns++] = pc;
-                        strong_weight += 1.0f;
+                        sc[k] = pid == PK_NONE ? -1.0f : L.u.pcost[pid];
+                        if (sc[k] >= 0.0f) { pm |= 1u << k; strong_weight += 1.0f; }
                     }
                     if (strong_weight <= 1e-6f) {
                         cost = center_cost;
                     } else {
                         float mx = -1e10f;
-                        for (int t = 0; t < ns; ++t) if (sc[t] > mx) mx = sc[t];
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) if (((pm >> k) & 1u) && sc[k] > mx) mx = sc[k];
                         float e[8];
                         float sum = 0.0f;
-                        for (int t = 0; t < ns; ++t) { e[t] = d_expf(sc[t] - mx); sum += e[t]; }
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            e[k] = 0.0f;
+                            if ((pm >> k) & 1u) { e[k] = d_expf(sc[k] - mx); sum += e[k]; }
+                        }
                         float acc = 0.0f;
-                        for (int t = 0; t < ns; ++t) { const float w = e[t] / sum; acc = fmaf(w, sc[t], acc); }
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            if ((pm >> k) & 1u) { const float w = e[k] / sum; acc = fmaf(w, sc[k], acc); }
                         acc = (acc > APD_COST_MAX) ? APD_COST_MAX : acc;
                         cost = (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
                     }
