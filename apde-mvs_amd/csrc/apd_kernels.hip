@@ -1369,13 +1369,13 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const typename std
 }
 
 // NCC-New reference side of pixel slot p (APD.cu:448-575): the 9 windows' reference taps, SA tap
-// masks and moments; wave w builds windows w, w + VM_WAVES, ... (tap order = the reference's).
+// masks and moments; wave w builds windows w, w + nwaves, ... (tap order = the reference's).
 template <bool F16>
 __device__ __forceinline__ void wv_build_windows(const Args &a, WvRefT<F16> &L, int p, const APD_G short2 *anc, int cid,
-                                                 int wave) {
+                                                 int wave, int nwaves) {
     const bool use_sa = cid != 0;
     const int p1 = p;
-    for (int k = wave; k < 9; k += VM_WAVES) {
+    for (int k = wave; k < 9; k += nwaves) {
         const short2 ap = anc[k];
         if (ap.x == -1 || ap.y == -1) continue;
         const int ax = ap.x, ay = ap.y;
@@ -1494,8 +1494,12 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
 #ifndef VM_WEAK_MINW
 #define VM_WEAK_MINW 3
 #endif
+#ifndef WV_WAVES
+#define WV_WAVES 4  // waves per Weak-sweep workgroup (64 pixels)
+#endif
+#define WV_BLOCK (WV_WAVES * WAVE)
 template <bool F16>
-__global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
+__global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
                                                                 int iter, const float *__restrict__ cand) {
     const int N = a.N, W = a.W;
     WvLdsT<F16> &L = *reinterpret_cast<WvLdsT<F16> *>(apd_dyn_lds);
@@ -1537,13 +1541,13 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             L.flags[p1] = hflag | (awin << 16);
             L.hyp[8 * VM_P + p1] = a.plane[c1];
         }
-        wv_build_windows<F16>(a, L, p1, anc, cid, wave);
+        wv_build_windows<F16>(a, L, p1, anc, cid, wave, WV_WAVES);
     }
     __syncthreads();
 
     // ---- P1: (hypothesis, view) tasks; with `cand` (k_weak_cand_vm ran on this list) the anchor
     // candidates' costs are read, and only the current plane is evaluated here
-    for (int u = wave; u < 9 * N; u += VM_WAVES) {  // view-major: the 4 waves share a source image
+    for (int u = wave; u < 9 * N; u += WV_WAVES) {  // view-major: the waves share a source image
         const int v = u / 9, h = u - 9 * v, t = h * N + v;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
         const bool want = pv1 && (h == 8 || ((L.flags[p1] >> h) & 1u));
@@ -1564,7 +1568,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
 
     // ---- P2: lane = (pixel, view) groups
     const int Gp = WAVE / N;
-    const int ppr = VM_WAVES * Gp;
+    const int ppr = WV_WAVES * Gp;
     for (int r0 = 0; r0 < np; r0 += ppr) {
         int g = lane / N;
         const bool lane_ok = g < Gp;
@@ -1662,7 +1666,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     const float4 fit1 = a.fit[c1];
 
     // ---- P3: fit-plane tasks (views with weight > 0)
-    for (int v = wave; v < N; v += VM_WAVES) {
+    for (int v = wave; v < N; v += WV_WAVES) {
         float cv = 0.0f;
         const bool want = refine && wts[v * VM_P + p1] > 0;
         const float4 fit = fit1;
@@ -1706,7 +1710,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     __syncthreads();
 
     // ---- P5: candidate tasks (views with weight > 0)
-    for (int u = wave; u < 5 * N; u += VM_WAVES) {
+    for (int u = wave; u < 5 * N; u += WV_WAVES) {
         const int v = u / 5, k = u - 5 * v, t = k * N + v;
         float cv = 0.0f;
         const bool want = refine && wts[v * VM_P + p1] > 0;
@@ -1722,7 +1726,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
 
     // ---- P6: acceptance, writes
     if (pv1) {
-        for (int v = wave; v < N; v += VM_WAVES) a.vw[(size_t)v * a.HW + c1] = (uint8_t)wts[v * VM_P + p1];
+        for (int v = wave; v < N; v += WV_WAVES) a.vw[(size_t)v * a.HW + c1] = (uint8_t)wts[v * VM_P + p1];
         if (wave == 0) {
             float cost_now = L.st[1 * VM_P + p1];
             const float cost_init = L.st[2 * VM_P + p1], wn = L.st[3 * VM_P + p1];
@@ -1883,9 +1887,9 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
         }
     }
     __syncthreads();
-    // ---- B: anchor ids in raster order of the anchors (bitonic sort of the group's keys), so the
-    // pairs of one window anchor, and of nearby ones, take neighbouring lanes (gather locality);
-    // their windows; the pixels' centre windows
+    // ---- B: anchor ids in raster order of the anchors (the rank of each key), so the pairs of one
+    // window anchor, and of nearby ones, take neighbouring lanes (gather locality); their windows;
+    // the pixels' centre windows
     {
         constexpr int PER = PK_AH / PK_BLOCK;
         bool used[PER];
@@ -1893,43 +1897,31 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
 #pragma unroll
         for (int i = 0; i < PER; ++i) used[i] = L.ahash[tid * PER + i] != 0;
         const int nd = pk_compact<PER>(used, ids, L.scan);
-        int *keys = reinterpret_cast<int *>(L.plist);  // plist is free until C: keys[0..511] sorted
+        int *keys = reinterpret_cast<int *>(L.plist);  // plist is free until C: keys[0..nd) unordered
 #pragma unroll
         for (int i = 0; i < PER; ++i)
             if (used[i]) keys[ids[i]] = L.ahash[tid * PER + i];
-        int sz = 2;  // sort the next power of two >= nd (padded)
-        while (sz < nd) sz <<= 1;
-        for (int i = nd + tid; i < sz; i += PK_BLOCK) keys[i] = 0x7FFFFFFF;
         if (tid == 0) L.nD = nd;
         __syncthreads();
-        for (int k = 2; k <= sz; k <<= 1)
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = tid; i < sz; i += PK_BLOCK) {
-                    const int ixj = i ^ j;
-                    if (ixj > i) {
-                        const int x = keys[i], y = keys[ixj];
-                        if (((i & k) == 0) == (x > y)) { keys[i] = y; keys[ixj] = x; }
-                    }
-                }
-                __syncthreads();
-            }
-        // slot -> id (binary search of the slot's key), kept in plist[PK_D + slot]
+        // id = rank of the key among the group's keys (distinct, so ranks are a permutation):
+        // raster order without a sort network (each rank is nd broadcast LDS reads)
         int *slot_id = keys + PK_D;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int key = L.ahash[tid * PER + i];
             int id = PK_NONE;
             if (key != 0) {
-                int lo = 0, hi = nd - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (keys[mid] < key) lo = mid + 1; else hi = mid;
-                }
-                id = lo;
+                id = 0;
+                for (int j = 0; j < nd; ++j) id += keys[j] < key;
             }
             slot_id[tid * PER + i] = id;
         }
-        for (int d = tid; d < nd; d += PK_BLOCK) L.apos[d] = keys[d] - 1;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int key = L.ahash[tid * PER + i];
+            if (key != 0) L.apos[slot_id[tid * PER + i]] = key - 1;
+        }
     }
     __syncthreads();
     if (pv1 && wave < 2) {
@@ -1965,25 +1957,31 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
         L.asrr[d] = srr;
         L.aws[d] = (uint8_t)ws;
     }
-    if (pv1 && wave == 2) {  // centre windows (k = 0: 6x6, step 2)
+    if (pv1) {  // centre windows (k = 0: 6x6, step 2): taps fetched by all waves, summed below
         const int pk = L.anc0[p1];
-        float sr = 0.0f, srr = 0.0f, ws = 0.0f;
         if (pk >= 0) {
             const int ax = pk & 0xFFFF, ay = pk >> 16;
-            for (int i = 0; i < 6; ++i)
-                for (int j = 0; j < 6; ++j) {
-                    const float r = tex_ref(a, ax - 5 + 2 * i, ay - 5 + 2 * j);
-                    L.cref[(i * 6 + j) * VM_P + p1] = r;
-                    sr += r;
-                    srr = fmaf(r, r, srr);
-                    ws += 1.0f;
-                }
+            for (int t = wave; t < 36; t += PK_WAVES) {
+                const int i = t / 6, j = t - 6 * i;
+                L.cref[t * VM_P + p1] = tex_ref(a, ax - 5 + 2 * i, ay - 5 + 2 * j);
+            }
+        }
+    }
+    __syncthreads();
+    if (pv1 && wave == 2) {  // the moments in wv_build_windows's tap order (texels are exact in RT)
+        float sr = 0.0f, srr = 0.0f, ws = 0.0f;
+        if (L.anc0[p1] >= 0) {
+            for (int t = 0; t < 36; ++t) {
+                const float r = (float)L.cref[t * VM_P + p1];
+                sr += r;
+                srr = fmaf(r, r, srr);
+                ws += 1.0f;
+            }
         }
         L.csr[p1] = sr;
         L.csrr[p1] = srr;
         L.cws[p1] = (uint8_t)ws;
     }
-    __syncthreads();
     // ---- C: candidate bits, pairs into the hash
     if (pv1 && wave == 3) {
         uint32_t cb = 0;
@@ -2713,7 +2711,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, in
                     }
                     W->flags[p] = awin << 16;
                 }
-                wv_build_windows<F16>(a, *W, p, anc, cid, wave);
+                wv_build_windows<F16>(a, *W, p, anc, cid, wave, VM_WAVES);
             }
         }
     }
@@ -3741,7 +3739,7 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
                 cand = (const float *)ctx->wcand.p;
             }
             if (ctx->sweep_vm)
-                LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N) : wv_lds_bytes<false>(a.N)), s,
+                LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N) : wv_lds_bytes<false>(a.N)), s,
                            a, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand);
             else
                 LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
