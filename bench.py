@@ -17,6 +17,8 @@ Besides the headline line the JSON carries:
                 rocprofv3 PMC summary under profiles/ when present.
   cpu_baseline  the C oracle (oracle/liboracle.so, OpenMP) on a bounded sample: the same scene rendered
                 at 756x504 (same cameras/texture statistics, same N), one sweep iteration.
+  apd_pass      (rank 0) the same metric for an APD + geometric-consistency pass (main.cpp rounds >= 1)
+                on the same view, priors from FIRST_INIT runs of every view of the scene.
 """
 from __future__ import annotations
 
@@ -83,6 +85,33 @@ def cpu_baseline(scene_args, n_src, threads):
                       f"FIRST_INIT, one sweep iteration (t_iter={t_iter:.2f}s; prepare {times[0]:.2f}s untimed)"}
 
 
+def apd_pass(eng, sc, ref, N):
+    """One REFINE_ITER problem with APD (deformable NCC, focal weights, anchors) and geometric
+    consistency on -- what main.cpp runs in rounds >= 1 -- on the same scene, priors from FIRST_INIT
+    runs of every view (the data flow of round 0). Per-iteration Mpix/s as the headline metric
+    (loop body = Strong B+R, RANSAC fit, candidate costs, Weak B+R), median over the 3 iterations."""
+    import apd_abi as A
+    import cases
+    import statistics
+    W, H = sc.width, sc.height
+    priors = []
+    for r in range(len(sc.images)):
+        arr = A.scene_problem(sc, r, [j for j, _ in sc.pairs[r]][:N], seed=0x5EED ^ r)
+        eng.set_problem(arr)
+        eng.run()
+        priors.append(eng.results(A.Outputs(W, H, N)))
+    arr = cases.refine_problem(sc, priors, ref, N, state=A.REFINE_ITER, geom=True, apd=True)
+    eng.set_problem(arr)
+    eng.run()
+    tm = eng.timing()
+    iters = list(tm.iter_ms)[: tm.iterations]
+    return {"mpix_s_iter": round(W * H / (statistics.median(iters) * 1e-3) / 1e6, 3),
+            "iter_ms": [round(x, 2) for x in iters], "run_patchmatch_ms": round(tm.total_ms, 2),
+            "mpix_s_end_to_end": round(W * H * tm.iterations / (tm.total_ms * 1e-3) / 1e6, 3),
+            "anchors_ms": round(tm.anchors_ms, 2), "init_ms": round(tm.init_ms, 2), "sweep_ms": round(tm.sweep_ms, 2),
+            "post_ms": round(tm.post_ms, 2), "weak_frac": round(float((arr.weak_info == A.WEAK).mean()), 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,6 +123,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--end-to-end", type=int, default=1, help="also time one full RunPatchMatch (0/1)")
+    ap.add_argument("--apd-pass", type=int, default=1,
+                    help="also time one APD + geometric-consistency pass (REFINE_ITER, rounds >= 1) (0/1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -200,6 +231,7 @@ def main():
                    "iter_ms": [round(x, 3) for x in list(tm.iter_ms)[:iters]],
                    "gt_median_rel_depth_err": round(float(np.median(rel)), 5),
                    "gt_frac_within_1pct": round(float((rel < 0.01).mean()), 4)}
+        apd = apd_pass(eng, sc, ref, N) if args.apd_pass else None
         cpu = None if args.no_cpu_baseline else cpu_baseline(scene_args, N, args.cpu_threads)
         line = {
             "metric": METRIC,
@@ -231,6 +263,7 @@ def main():
                          "hbm_peak_gbs": PEAK_HBM_GBS},
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "apd_pass": apd,
             "scene_gen_s": round(t_scene, 2),
         }
     eng.close()
