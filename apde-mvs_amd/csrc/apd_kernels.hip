@@ -1500,7 +1500,8 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
 #define WV_BLOCK (WV_WAVES * WAVE)
 template <bool F16>
 __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
-                                                                int iter, const float *__restrict__ cand) {
+                                                                int iter, const float *__restrict__ cand,
+                                                                const uint8_t *__restrict__ cand_done) {
     const int N = a.N, W = a.W;
     WvLdsT<F16> &L = *reinterpret_cast<WvLdsT<F16> *>(apd_dyn_lds);
     float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64], later [5][N][64]
@@ -1545,13 +1546,14 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     }
     __syncthreads();
 
-    // ---- P1: (hypothesis, view) tasks; with `cand` (k_weak_cand_vm ran on this list) the anchor
-    // candidates' costs are read, and only the current plane is evaluated here
+    // ---- P1: (hypothesis, view) tasks; where k_weak_cand_vm handled this group (`cand_done`), the
+    // anchor candidates' costs are read, and only the current plane is evaluated here
+    const bool cand_ok = cand && cand_done[blk];
     for (int u = wave; u < 9 * N; u += WV_WAVES) {  // view-major: the waves share a source image
         const int v = u / 9, h = u - 9 * v, t = h * N + v;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
         const bool want = pv1 && (h == 8 || ((L.flags[p1] >> h) & 1u));
-        if (cand && h < 8) {
+        if (cand_ok && h < 8) {
             if (want) val = cand[((size_t)v * 8 + h) * (size_t)count + first + p1];
             costL[t * VM_P + p1] = val;
             continue;
@@ -1756,17 +1758,19 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
 }
 
 // ---------------------------------------------------------------------------------------------
-// Candidate costs of the Weak sweep with the anchor windows shared across pixels (no SA masks).
+// Candidate costs of the Weak sweep with the anchor windows shared across pixels.
 // For a WEAK pixel, candidate h is the plane of its STRONG anchor h+1, and ComputeBilateralNCCNew
 // (APD.cu:448-593) of that plane is the centre window (at anchor 0, pixel-specific) combined by the
-// focal softmax with the 3x3 windows at anchors 1..8. Without SA masks an anchor window's cost is a
-// function of (window anchor, candidate plane, view) only -- the out-of-frame rule reads the
+// focal softmax with the 3x3 windows at anchors 1..8. An anchor window's cost is a function of
+// (window anchor, candidate plane, view, SA label) only -- the out-of-frame rule reads the
 // anchor's selected_views, which only the Strong sweep writes -- and neighbouring WEAK pixels share
 // anchors: a 64-pixel group at 3024x2016 (N = 8) holds ~1.8k distinct (window anchor, candidate
 // anchor) pairs of ~4.0k evaluations (2.2x; 2.6x at 6048x4032). This kernel evaluates every
 // distinct pair once per view, the centre windows per pixel, and writes each (candidate, view,
 // pixel) cost -- bit-identical to ncc_new_vm (same statements, same softmax order) -- for the
-// sweep's P1, which then evaluates only the current plane.
+// sweep's P1, which then evaluates only the current plane. With SA masks anchors are keyed by
+// (position, the pixel's label slot); a group holding more than 3 labels is left to the sweep
+// (done[group] = 0).
 //   A/B  hash the group's anchors 1..8 into distinct ids (deterministic slot order), build their
 //        3x3 reference windows and the pixels' 6x6 centre windows (wv_build_windows's statements)
 //   C    hash the (window anchor, candidate anchor) pairs, pair ids in slot order
@@ -1794,24 +1798,36 @@ struct PkLds {
     float4 apl[PK_D];               // plane of anchor d (candidates)
     int apos[PK_D];                 // packed (x, y) of anchor d
     float asr[PK_D], asrr[PK_D];    // window moments
-    int ahash[PK_AH];               // anchor hash: packed position + 1 (0 = empty)
+    uint32_t ahash[PK_AH];          // anchor hash: pk_key + 1 (0 = empty)
     RT cref[36 * VM_P];             // [tap][p] centre window reference taps
     float csr[VM_P], csrr[VM_P];
-    float ccost[8 * VM_P];          // [h][p] centre window cost of candidate h (per view)
-    uint16_t aid[8 * VM_P];         // [k-1][p]: id of anchor k, PK_NONE if invalid
+    uint64_t cmask[VM_P];           // centre window tap mask (SA)
+    union {
+        int kcnt[PK_D];             // C: pairs per window anchor, then their offsets
+        struct {
+            float ccost[8 * VM_P];  // D: [h][p] centre window cost of candidate h (per view)
+            uint8_t cstat[8 * VM_P];  // D: [h][p] bit 0 dead (centre or its anchor out of frame)
+        } d;
+    } w;
+    uint16_t aid[8 * VM_P];         // [k-1][p]: id of (anchor k, the pixel's SA label), PK_NONE if invalid
+    uint16_t amask[PK_D];           // anchor window tap mask (SA)
+    uint16_t awin[VM_P];            // bit k: window k present (anchor valid, SA label matches; APD.cu:455-470)
     int anc0[VM_P];                 // packed anchor 0, -1 if invalid
-    uint8_t astrong[PK_D], aws[PK_D];
+    uint8_t alc[PK_D], aws[PK_D];   // alc: SA label slot (bits 0-1) | anchor STRONG (bit 7)
     uint8_t cws[VM_P];
     uint8_t cand[VM_P];             // bit h: candidate h present (anchor h+1 valid and STRONG)
-    uint8_t cstat[8 * VM_P];        // [h][p]: bit 0 dead (centre or its anchor out of frame), bit 1 centre window present
-    int kcnt[PK_D];                 // pairs per window anchor, then their offsets
+    uint8_t plc[VM_P];              // the pixel's SA label slot
+    int gcid[4];                    // SA labels of the group (+1; 0 = free slot), at most 3
+    int ovf;                        // more than 3 SA labels: the sweep evaluates this group itself
     int scan[PK_BLOCK / WAVE + 1];
     int nD, nP;
 };
+static_assert(sizeof(PkLds<true>) <= 80 * 1024, "k_weak_cand_vm: two 8-wave workgroups per CU (160 KiB LDS)");
 template <bool F16>
 static inline size_t pk_lds_bytes() { return sizeof(PkLds<F16>); }
 
-// anchors are packed as x | y << 16 with x, y < 32768: hash keys are that + 1 (0 = empty slot)
+// anchor keys: x | y << 15 | SA label slot << 30 (x, y < 32768), + 1 in the hash (0 = empty slot);
+// their order (the anchor ids) is raster order within a label slot
 __device__ __forceinline__ uint32_t pk_mix(uint32_t k) {
     k ^= k >> 15;
     k *= 0x2C1B3C6Du;
@@ -1851,7 +1867,7 @@ __device__ __forceinline__ int pk_compact(const bool (&used)[PER], int (&ids)[PE
 
 template <bool F16>
 __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a, const int *__restrict__ list, int count,
-                                                           float *__restrict__ out) {
+                                                           float *__restrict__ out, uint8_t *__restrict__ done) {
     const int N = a.N, W = a.W, H = a.H;
     PkLds<F16> &L = *reinterpret_cast<PkLds<F16> *>(apd_dyn_lds);
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
@@ -1864,10 +1880,29 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
     const int c1 = list[first + min(p1, np - 1)];
     const int py1 = c1 / W, px1 = c1 - py1 * W;
 
-    // ---- A: anchors into the hash
+    // ---- A: SA label slots, anchors into the hash
     for (int i = tid; i < PK_P; i += PK_BLOCK) L.u.hash[i] = 0;
     for (int i = tid; i < PK_AH; i += PK_BLOCK) L.ahash[i] = 0;
+    if (tid < 4) L.gcid[tid] = 0;
+    if (tid == 0) L.ovf = 0;
     __syncthreads();
+    const int cid1 = a.sa_any ? a.sa[c1] : 0;  // the pixel's label (0: no SA masking)
+    if (pv1 && wave == 0) {
+        int slot = -1;
+        for (int k = 0; k < 3 && slot < 0; ++k) {
+            const int old = atomicCAS(&L.gcid[k], 0, cid1 + 1);
+            if (old == 0 || old == cid1 + 1) slot = k;
+        }
+        if (slot < 0) L.ovf = 1;
+        L.plc[p1] = (uint8_t)max(slot, 0);
+    }
+    __syncthreads();
+    if (L.ovf) {  // uniform: the Weak sweep evaluates this group's candidates itself
+        if (tid == 0) done[blk] = 0;
+        return;
+    }
+    const uint32_t lc1 = L.plc[p1];
+    auto pk_key = [](int x, int y, uint32_t lc) { return (uint32_t)x | ((uint32_t)y << 15) | (lc << 30); };
     const APD_G short2 *anc1 = a.anchors + (size_t)a.amap[c1] * 9;
     if (pv1 && wave == 0) {
         const short2 a0 = anc1[0];
@@ -1877,11 +1912,11 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
         for (int k = 1 + 4 * wave; k < 5 + 4 * wave; ++k) {
             const short2 ap = anc1[k];
             if (ap.x == -1 || ap.y == -1) continue;
-            const int key = ((int)(uint16_t)ap.x | ((int)ap.y << 16)) + 1;
-            uint32_t slot = pk_mix((uint32_t)key) & (PK_AH - 1);
+            const uint32_t key = pk_key(ap.x, ap.y, lc1) + 1u;
+            uint32_t slot = pk_mix(key) & (PK_AH - 1);
             for (;;) {
-                const int old = atomicCAS(&L.ahash[slot], 0, key);
-                if (old == 0 || old == key) break;
+                const uint32_t old = atomicCAS(&L.ahash[slot], 0u, key);
+                if (old == 0u || old == key) break;
                 slot = (slot + 1) & (PK_AH - 1);
             }
         }
@@ -1897,7 +1932,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
 #pragma unroll
         for (int i = 0; i < PER; ++i) used[i] = L.ahash[tid * PER + i] != 0;
         const int nd = pk_compact<PER>(used, ids, L.scan);
-        int *keys = reinterpret_cast<int *>(L.plist);  // plist is free until C: keys[0..nd) unordered
+        uint32_t *keys = L.plist;  // plist is free until C: keys[0..nd) unordered
 #pragma unroll
         for (int i = 0; i < PER; ++i)
             if (used[i]) keys[ids[i]] = L.ahash[tid * PER + i];
@@ -1905,11 +1940,11 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
         __syncthreads();
         // id = rank of the key among the group's keys (distinct, so ranks are a permutation):
         // raster order without a sort network (each rank is nd broadcast LDS reads)
-        int *slot_id = keys + PK_D;
+        uint32_t *slot_id = keys + PK_D;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
-            const int key = L.ahash[tid * PER + i];
-            int id = PK_NONE;
+            const uint32_t key = L.ahash[tid * PER + i];
+            uint32_t id = PK_NONE;
             if (key != 0) {
                 id = 0;
                 for (int j = 0; j < nd; ++j) id += keys[j] < key;
@@ -1919,8 +1954,12 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
-            const int key = L.ahash[tid * PER + i];
-            if (key != 0) L.apos[slot_id[tid * PER + i]] = key - 1;
+            const uint32_t key = L.ahash[tid * PER + i];
+            if (key != 0) {
+                const uint32_t k0 = key - 1u, d = slot_id[tid * PER + i];
+                L.apos[d] = (int)((k0 & 0x7FFFu) | (((k0 >> 15) & 0x7FFFu) << 16));
+                L.alc[d] = (uint8_t)(k0 >> 30);
+            }
         }
     }
     __syncthreads();
@@ -1929,26 +1968,43 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
             const short2 ap = anc1[k];
             uint16_t id = PK_NONE;
             if (!(ap.x == -1 || ap.y == -1)) {
-                const int key = ((int)(uint16_t)ap.x | ((int)ap.y << 16)) + 1;
-                uint32_t slot = pk_mix((uint32_t)key) & (PK_AH - 1);
+                const uint32_t key = pk_key(ap.x, ap.y, lc1) + 1u;
+                uint32_t slot = pk_mix(key) & (PK_AH - 1);
                 while (L.ahash[slot] != key) slot = (slot + 1) & (PK_AH - 1);
                 id = (uint16_t)L.plist[PK_D + slot];
             }
             L.aid[(k - 1) * VM_P + p1] = id;
         }
     }
+    if (pv1 && wave == PK_WAVES - 1) {  // windows present (APD.cu:455-470: anchor valid and, with SA, its label matches)
+        uint32_t aw = 0;
+        for (int k = 0; k < 9; ++k) {
+            const short2 ap = anc1[k];
+            if (!(ap.x == -1 || ap.y == -1) && !(cid1 != 0 && sa_at_dev(a, ap.x, ap.y) != cid1)) aw |= 1u << k;
+        }
+        L.awin[p1] = (uint16_t)aw;
+    }
     const int nD = L.nD;
-    for (int d = tid; d < nD; d += PK_BLOCK) {  // distinct anchor windows (wv_build_windows, k >= 1, no SA)
+    for (int d = tid; d < nD; d += PK_BLOCK) {  // distinct anchor windows (wv_build_windows, k >= 1)
         const int pk = L.apos[d];
         const int ax = pk & 0xFFFF, ay = pk >> 16;
         const int q = ax + ay * W;
-        L.astrong[d] = a.weak[q] == APD_STRONG;
+        const int cid = L.gcid[L.alc[d]] - 1;
+        const bool use_sa = cid != 0;
+        L.alc[d] |= (uint8_t)((a.weak[q] == APD_STRONG) << 7);
         L.apl[d] = a.plane[q];
         float sr = 0.0f, srr = 0.0f, ws = 0.0f;
+        uint32_t mask = 0;
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) {
-                const float r = tex_ref(a, ax - 5 + 5 * i, ay - 5 + 5 * j);
+                const int rx = ax - 5 + 5 * i, ry = ay - 5 + 5 * j;
+                if (use_sa && sa_at_dev(a, rx, ry) != cid) {
+                    L.aref[(i * 3 + j) * PK_D + d] = 0.0f;
+                    continue;
+                }
+                const float r = tex_ref(a, rx, ry);
                 L.aref[(i * 3 + j) * PK_D + d] = r;
+                mask |= 1u << (i * 3 + j);
                 sr += r;
                 srr = fmaf(r, r, srr);
                 ws += 1.0f;
@@ -1956,6 +2012,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
         L.asr[d] = sr;
         L.asrr[d] = srr;
         L.aws[d] = (uint8_t)ws;
+        L.amask[d] = (uint16_t)mask;
     }
     if (pv1) {  // centre windows (k = 0: 6x6, step 2): taps fetched by all waves, summed below
         const int pk = L.anc0[p1];
@@ -1963,16 +2020,23 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
             const int ax = pk & 0xFFFF, ay = pk >> 16;
             for (int t = wave; t < 36; t += PK_WAVES) {
                 const int i = t / 6, j = t - 6 * i;
-                L.cref[t * VM_P + p1] = tex_ref(a, ax - 5 + 2 * i, ay - 5 + 2 * j);
+                const int rx = ax - 5 + 2 * i, ry = ay - 5 + 2 * j;
+                L.cref[t * VM_P + p1] = (cid1 != 0 && sa_at_dev(a, rx, ry) != cid1) ? 0.0f : tex_ref(a, rx, ry);
             }
         }
     }
     __syncthreads();
-    if (pv1 && wave == 2) {  // the moments in wv_build_windows's tap order (texels are exact in RT)
+    if (pv1 && wave == 2) {  // the moments and tap mask in wv_build_windows's tap order (texels are exact in RT)
         float sr = 0.0f, srr = 0.0f, ws = 0.0f;
-        if (L.anc0[p1] >= 0) {
+        uint64_t mask = 0;
+        const int pk = L.anc0[p1];
+        if (pk >= 0) {
+            const int ax = pk & 0xFFFF, ay = pk >> 16;
             for (int t = 0; t < 36; ++t) {
+                const int i = t / 6, j = t - 6 * i;
+                if (cid1 != 0 && sa_at_dev(a, ax - 5 + 2 * i, ay - 5 + 2 * j) != cid1) continue;
                 const float r = (float)L.cref[t * VM_P + p1];
+                mask |= 1ull << t;
                 sr += r;
                 srr = fmaf(r, r, srr);
                 ws += 1.0f;
@@ -1981,13 +2045,14 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
         L.csr[p1] = sr;
         L.csrr[p1] = srr;
         L.cws[p1] = (uint8_t)ws;
+        L.cmask[p1] = mask;
     }
     // ---- C: candidate bits, pairs into the hash
     if (pv1 && wave == 3) {
         uint32_t cb = 0;
         for (int h = 0; h < 8; ++h) {
             const uint16_t id = L.aid[h * VM_P + p1];
-            if (id != PK_NONE && L.astrong[id]) cb |= 1u << h;
+            if (id != PK_NONE && (L.alc[id] >> 7)) cb |= 1u << h;
         }
         L.cand[p1] = (uint8_t)cb;
     }
@@ -1997,9 +2062,10 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
         for (int h = wave; h < 8; h += PK_WAVES) {
             if (!((cb >> h) & 1u)) continue;
             const uint32_t hid = L.aid[h * VM_P + p1];
+            const uint32_t aw = L.awin[p1];
             for (int k = 0; k < 8; ++k) {
                 const uint32_t kid = L.aid[k * VM_P + p1];
-                if (kid == PK_NONE) continue;
+                if (kid == PK_NONE || !((aw >> (k + 1)) & 1u)) continue;
                 const int key = (int)(kid | (hid << 9)) + 1;  // <= 2^18
                 uint32_t slot = pk_mix((uint32_t)key) & (PK_P - 1);
                 for (;;) {
@@ -2013,7 +2079,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
     __syncthreads();
     // pair ids ordered by window anchor (counting sort; the order inside one anchor's run does not
     // matter: a pair id only labels a window cost)
-    for (int d = tid; d < PK_D; d += PK_BLOCK) L.kcnt[d] = 0;
+    for (int d = tid; d < PK_D; d += PK_BLOCK) L.w.kcnt[d] = 0;
     __syncthreads();
     {
         constexpr int PER = PK_P / PK_BLOCK;
@@ -2021,7 +2087,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
         for (int i = 0; i < PER; ++i) {
             const int hv = L.u.hash[tid * PER + i];
             if (hv != 0) {
-                const int r = atomicAdd(&L.kcnt[(hv - 1) & 511], 1);
+                const int r = atomicAdd(&L.w.kcnt[(hv - 1) & 511], 1);
                 L.u.hash[tid * PER + i] = hv | (r << 19);
             }
         }
@@ -2030,7 +2096,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
     if (wave == 0) {  // exclusive scan of the 512 anchor counts, 8 per lane
         int c[8], sum = 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { c[i] = L.kcnt[lane * 8 + i]; sum += c[i]; }
+        for (int i = 0; i < 8; ++i) { c[i] = L.w.kcnt[lane * 8 + i]; sum += c[i]; }
         int x = sum;
 #pragma unroll
         for (int o = 1; o < WAVE; o <<= 1) {
@@ -2039,7 +2105,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
         }
         int off = x - sum;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { L.kcnt[lane * 8 + i] = off; off += c[i]; }
+        for (int i = 0; i < 8; ++i) { L.w.kcnt[lane * 8 + i] = off; off += c[i]; }
         if (lane == WAVE - 1) L.nP = x;
     }
     __syncthreads();
@@ -2050,7 +2116,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
             const int hv = L.u.hash[tid * PER + i];
             if (hv != 0) {
                 const int key = (hv & 0x7FFFF) - 1, r = hv >> 19;
-                const int pid = L.kcnt[key & 511] + r;
+                const int pid = L.w.kcnt[key & 511] + r;
                 L.plist[pid] = (uint32_t)(key & 511) | ((uint32_t)(key >> 9) << 16);
                 L.u.hash[tid * PER + i] = (key + 1) | (pid << 19);
             }
@@ -2064,7 +2130,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
             for (int k = 0; k < 8; ++k) {
                 const uint32_t kid = L.aid[k * VM_P + p1];
                 uint16_t pid = PK_NONE;
-                if (((cb >> h) & 1u) && kid != PK_NONE) {
+                if (((cb >> h) & 1u) && kid != PK_NONE && ((L.awin[p1] >> (k + 1)) & 1u)) {
                     const int key = (int)(kid | (hid << 9)) + 1;
                     uint32_t slot = pk_mix((uint32_t)key) & (PK_P - 1);
                     while ((L.u.hash[slot] & 0x7FFFF) != key) slot = (slot + 1) & (PK_P - 1);
@@ -2077,6 +2143,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
     __syncthreads();
     const int nP = L.nP;
 
+    if (tid == 0) done[blk] = 1;
     // ---- D: per view
     for (int v = 0; v < N; ++v) {
         const int s = v + 1;
@@ -2102,7 +2169,8 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
             if (__ballot(live)) {
                 const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
                 float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-                ncc_new_window<F16, 3, 5>(a, &L.aref[kid], PK_D, 0x1FFull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+                ncc_new_window<F16, 3, 5>(a, &L.aref[kid], PK_D, (uint64_t)L.amask[kid], Hm, ax, ay, live, fast, T, Q, ss,
+                                          sss, srs);
                 if (live) {
                     const float wsum = (float)L.aws[kid];
                     if (wsum != 0.0f) res = ncc_finalize(L.asr[kid], L.asrr[kid], ss, sss, srs, wsum);
@@ -2122,7 +2190,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
                 project(Hm, (float)px1, (float)py1, ptx, pty);
                 const bool alive = want && !(ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f);
                 const int pk = L.anc0[p1];
-                const bool has = alive && pk >= 0;
+                const bool has = alive && pk >= 0 && (L.awin[p1] & 1u);
                 const int ax = has ? (pk & 0xFFFF) : px1, ay = has ? (pk >> 16) : py1;
                 bool live = has, dead = !alive;
                 if (has) {
@@ -2135,15 +2203,15 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
                 if (__ballot(live)) {
                     const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
                     float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-                    ncc_new_window<F16, 6, 2>(a, &L.cref[p1], VM_P, ~0ull >> 28, Hm, ax, ay, live, fast, T, Q, ss, sss,
-                                              srs);
+                    ncc_new_window<F16, 6, 2>(a, &L.cref[p1], VM_P, L.cmask[p1], Hm, ax, ay, live, fast, T, Q, ss,
+                                              sss, srs);
                     if (live) {
                         const float wsum = (float)L.cws[p1];
                         if (wsum != 0.0f) { cc = ncc_finalize(L.csr[p1], L.csrr[p1], ss, sss, srs, wsum); present = true; }
                     }
                 }
-                L.ccost[h * VM_P + p1] = cc;
-                L.cstat[h * VM_P + p1] = (uint8_t)(dead ? 1 : 0) | (present ? 2 : 0);
+                L.w.d.ccost[h * VM_P + p1] = cc;
+                L.w.d.cstat[h * VM_P + p1] = (uint8_t)(dead ? 1 : 0) | (present ? 2 : 0);
             }
         }
         __syncthreads();
@@ -2153,10 +2221,10 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
             for (int h = wave; h < 8; h += PK_WAVES) {
                 if (!((cb >> h) & 1u)) continue;
                 float cost;
-                if (L.cstat[h * VM_P + p1] & 1u) {
+                if (L.w.d.cstat[h * VM_P + p1] & 1u) {
                     cost = APD_COST_MAX;
                 } else {
-                    const float center_cost = L.ccost[h * VM_P + p1];
+                    const float center_cost = L.w.d.ccost[h * VM_P + p1];
                     // the windows present, in anchor order: a compacted list in the reference, a
                     // presence mask here (same values, same order; no dynamically indexed arrays)
                     float sc[8];
@@ -3167,7 +3235,7 @@ struct apd_ctx {
     std::string err;
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
-        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand;
+        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, wdone;
     int n_near = 0;
     int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
     Args args{};
@@ -3382,7 +3450,7 @@ void apd_destroy(apd_ctx *ctx) {
     DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
-                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand};
+                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand, &ctx->wdone};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
@@ -3663,9 +3731,11 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         HIP_OK(ctx, hipMemcpyAsync(host_tot, tot, 4 * sizeof(int), hipMemcpyDeviceToHost, s));
         HIP_OK(ctx, hipStreamSynchronize(s));
         for (int i = 0; i < 4; ++i) ctx->cnt[i] = host_tot[i];
-        if (a.use_apd && ctx->sweep_vm && ctx->cand_pairs && !a.sa_any &&
-            (st = ensure(ctx, ctx->wcand, (size_t)a.N * 8 * (size_t)std::max(ctx->cnt[2], ctx->cnt[3]) * sizeof(float))))
-            return st;
+        if (a.use_apd && ctx->sweep_vm && ctx->cand_pairs) {
+            const size_t nmax = (size_t)std::max(ctx->cnt[2], ctx->cnt[3]);
+            if ((st = ensure(ctx, ctx->wcand, (size_t)a.N * 8 * nmax * sizeof(float)))) return st;
+            if ((st = ensure(ctx, ctx->wdone, blocks_for(nmax, VM_P)))) return st;
+        }
         for (int i = 0; i < 4; ++i) {
             if ((st = build_tile_list(ctx, modes[i][0], modes[i][1], list_ptr(ctx, i), tot + i))) return st;
         }
@@ -3727,20 +3797,19 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             const int n = ctx->cnt[2 + colour];
             if (n <= 0) continue;
             const float *cand = nullptr;
-            if (ctx->sweep_vm && ctx->cand_pairs && !a.sa_any) {
-                // anchor-window sharing needs no SA masks (an SA label makes a window pixel-specific)
-                if (ctx->wcand.bytes < (size_t)a.N * 8 * (size_t)n * sizeof(float)) {
+            if (ctx->sweep_vm && ctx->cand_pairs) {
+                if (ctx->wcand.bytes < (size_t)a.N * 8 * (size_t)n * sizeof(float) || ctx->wdone.bytes < blocks_for((size_t)n, VM_P)) {
                     ctx->err = "candidate cost buffer not sized by apd_stage_prepare";
                     return APD_ESTATE;
                 }
                 LAUNCH_TEX(k_weak_cand_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(PK_BLOCK),
                            (ctx->args.tex_f16 ? pk_lds_bytes<true>() : pk_lds_bytes<false>()), s, a,
-                           (const int *)list_ptr(ctx, 2 + colour), n, (float *)ctx->wcand.p);
+                           (const int *)list_ptr(ctx, 2 + colour), n, (float *)ctx->wcand.p, (uint8_t *)ctx->wdone.p);
                 cand = (const float *)ctx->wcand.p;
             }
             if (ctx->sweep_vm)
                 LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N) : wv_lds_bytes<false>(a.N)), s,
-                           a, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand);
+                           a, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, (const uint8_t *)ctx->wdone.p);
             else
                 LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
                            (const int *)list_ptr(ctx, 2 + colour), n, iter);
