@@ -11,21 +11,35 @@ import synth, host_schedule as HS
 W, H, V = (int(x) for x in sys.argv[1:4]) if len(sys.argv) >= 4 else (3024, 2016, 9)
 extra = sys.argv[4:]
 sc = synth.make_scene(W, H, V - 1)
+print("scene generated", flush=True)
 folder = tempfile.mkdtemp(prefix="apd_scan_")
 HS.write_dense_folder(sc, folder, ext=".png", masks=True)
 from PIL import Image
 for f in sorted(os.listdir(os.path.join(folder, "images"))):  # re-encode as baseline JPEG
     p = os.path.join(folder, "images", f)
     Image.open(p).save(p[:-4] + ".jpg", quality=95)
+    print("jpeg", f, flush=True)
     os.remove(p)
 apd = os.path.join(REPO, "apde-mvs_amd", "host", "build", "apd")
 cmd = [apd, "-d", folder, "--dataset", "ETH3D", "--no_fuse", "true"] + extra
+# the apd stdout goes to a file as it runs (TIME_SCAN_LOG, default under /tmp): a long scan keeps
+# writing, so a watchdog on the output directory sees progress
+log = os.environ.get("TIME_SCAN_LOG", os.path.join(folder, "apd_stdout.log"))
+print(f"scene written ({W}x{H}, {V} views); apd log: {log}", flush=True)
 t0 = time.time()
-out = subprocess.run(cmd, capture_output=True, text=True)
+with open(log, "w") as lf:
+    rc = subprocess.run(cmd, stdout=lf, stderr=subprocess.STDOUT).returncode
 wall = time.time() - t0
-if out.returncode != 0:
-    print(out.stdout[-3000:], out.stderr[-3000:])
-    sys.exit(out.returncode)
+
+
+class _Out:
+    stdout = open(log).read()
+
+
+out = _Out()
+if rc != 0:
+    print(out.stdout[-3000:])
+    sys.exit(rc)
 rpm = [int(x) for x in re.findall(r"RunPatchMatch time: (\d+) ms", out.stdout)]
 cost = [int(x) for x in re.findall(r"Cost time: (\d+) ms", out.stdout)][:-1]  # the last line is the total
 ht = re.findall(r"HostTiming images ([\d.]+) priors ([\d.]+) set\+run ([\d.]+) \(run (\d+)\) results ([\d.]+) epilogue ([\d.]+) emit ([\d.]+)", out.stdout)
