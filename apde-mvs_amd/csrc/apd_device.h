@@ -374,9 +374,17 @@ __device__ __forceinline__ float ncc_finalize(float sr, float srr, float ss, flo
 // Reference-side window of ComputeBilateralNCCOld (6x6, radius 5, step 2): fixed per pixel, so it is
 // gathered once per pixel into LDS (one copy per pixel, each of the pixel's N lanes fetching a share)
 // and read back by broadcast across all 14*N NCC evaluations of a sweep.
+// SA quadrant window of ComputeBilateralNCCOld (APD.cu:664-719) for one reference pixel: which of the
+// 36 visiting slots (quadrant-major, see sa_dx/sa_dy) the branch visits -- it depends only on the
+// image bounds and the SA labels around the pixel -- and its reference moments in visiting order.
+struct alignas(16) SaWin {
+    uint32_t mlo, mhi;  // visited slots: bit k of (mhi:mlo)
+    float sr, srr;      // sum r, sum r*r over the visited slots, in visiting order
+};
 struct RefWin {
     const float *r;    // 36 values in LDS, column-major (i*6 + j), element k at r[k * stride]
     float mean, var;   // sum_ref/36 and sum_ref_ref/36 - mean^2, same op order as the oracle
+    const SaWin *sa = nullptr;  // view-major kernels with SA masks: the pixel's SaWin in LDS
 };
 // mean / variance of a reference window already in LDS (element k at r[k * RS])
 template <int RS>
@@ -419,7 +427,43 @@ __device__ __forceinline__ void build_refwin(const Args &a, int px, int py, floa
     w.var = fmaf(-sr, sr, srr);
 }
 
-// SA quadrant branch of ComputeBilateralNCCOld (APD.cu:664-719); rarely taken, kept out of line.
+// Visiting slot k (0..35) of the SA branch: quadrant q = k / 9 with signs (+,+), (-,-), (+,-), (-,+)
+// (sign[] of APD.cu:664-719), tap j = k % 9 at the odd offsets off[] of that branch.
+__host__ __device__ constexpr int sa_off(int j, int c) {
+    constexpr int off[18] = {1, 1, 3, 1, 1, 3, 1, 5, 3, 3, 5, 1, 5, 3, 3, 5, 5, 5};
+    return off[2 * j + c];
+}
+__host__ __device__ constexpr int sa_dx(int k) { return sa_off(k % 9, 0) * ((k / 9 == 0 || k / 9 == 2) ? 1 : -1); }
+__host__ __device__ constexpr int sa_dy(int k) { return sa_off(k % 9, 1) * ((k / 9 == 0 || k / 9 == 3) ? 1 : -1); }
+// grid index (i*6 + j) of slot k in the 6x6 NCC-Old reference window
+__host__ __device__ constexpr int sa_grid(int k) { return ((sa_dx(k) + 5) / 2) * 6 + (sa_dy(k) + 5) / 2; }
+
+template <class AT>
+__device__ __forceinline__ SaWin sa_window(const AT &a, int px, int py) {
+    const uint8_t cid = a.sa[py * a.W + px];
+    uint64_t m = 0;
+    float sr = 0.0f, srr = 0.0f;
+    for (int q = 0; q < 4; ++q) {
+        for (int j = 0; j < 9; ++j) {
+            const int k = q * 9 + j;
+            const int rx = px + sa_dx(k), ry = py + sa_dy(k);
+            if (rx < 0 || rx >= a.W || ry < 0 || ry >= a.H) continue;
+            if (a.sa[ry * a.W + rx] != cid) break;
+            const float r = tex_ref(a, rx, ry);
+            sr += r;
+            srr = fmaf(r, r, srr);
+            m |= 1ull << k;
+        }
+    }
+    SaWin w;
+    w.mlo = (uint32_t)m;
+    w.mhi = (uint32_t)(m >> 32);
+    w.sr = sr;
+    w.srr = srr;
+    return w;
+}
+
+// SA quadrant branch of ComputeBilateralNCCOld (APD.cu:664-719), IEEE taps: out of line (ncc_old_slow).
 template <bool F16>
 __device__ __forceinline__ float ncc_old_sa(const APD_G Args *ap, int px, int py, int s, const Hom &H, uint8_t cid) {
     const APD_G Args &a = *ap;
@@ -644,6 +688,56 @@ __device__ __forceinline__ void ncc_old_taps(const TT &T, const Hom &Hm, int px,
 #endif
 }
 
+// The SA quadrant branch's source moments on the fast taps: all 36 slots in visiting order (groups of
+// 6, software-pipelined as ncc_old_taps), the slots the pixel's SaWin does not visit contributing
+// exact zeros: the partial sums start at +0 and are never -0, so x + (+-0) == x bit-for-bit.
+// Same (X, Y, Z) expressions as project().
+template <class TT, int RS>
+__device__ __forceinline__ void ncc_old_sa_taps(const TT &T, const Hom &Hm, int px, int py, const float *r,
+                                                const SaWin &w, float &ss, float &sss, float &srs) {
+    auto group = [&](int g, typename TT::Tap *t) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const int k = 6 * g + j;
+            const float x = (float)(px + sa_dx(k)), y = (float)(py + sa_dy(k));
+            const apd_f2 cxy = {fmaf(Hm.h[0], x, Hm.h[2]), fmaf(Hm.h[3], x, Hm.h[5])};
+            const apd_f2 XY = pk_fma((apd_f2){Hm.h[1], Hm.h[4]}, (apd_f2){y, y}, cxy);
+            const float Z = fmaf(Hm.h[7], y, fmaf(Hm.h[6], x, Hm.h[8]));
+            t[j] = T.tap(XY, rcp_newton(Z));
+        }
+    };
+    auto consume = [&](int g, const typename TT::Tap *t, const typename TT::Raw *q) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const int k = 6 * g + j;
+            const uint32_t on = k < 32 ? (w.mlo >> k) & 1u : (w.mhi >> (k - 32)) & 1u;
+            const float v = on ? T.finish(t[j], q[j]) : 0.0f;
+            ss += v;
+            const apd_f2 acc = pk_fma((apd_f2){v, r[sa_grid(k) * RS]}, (apd_f2){v, v}, (apd_f2){sss, srs});
+            sss = acc.x;
+            srs = acc.y;
+        }
+    };
+    typename TT::Tap ta[6], tb[6];
+    typename TT::Raw qa[6], qb[6];
+    group(0, ta);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) qa[j] = T.load(ta[j]);
+#pragma unroll
+    for (int g = 0; g < 6; g += 2) {
+        group(g + 1, tb);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) qb[j] = T.load(tb[j]);
+        consume(g, ta, qa);
+        if (g + 2 < 6) {
+            group(g + 2, ta);
+#pragma unroll
+            for (int j = 0; j < 6; ++j) qa[j] = T.load(ta[j]);
+        }
+        consume(g + 1, tb, qb);
+    }
+}
+
 // IEEE-division statement of the ComputeBilateralNCCOld window sum (taken only for windows that
 // window_rcp_ok rejects).
 template <bool F16>
@@ -720,9 +814,13 @@ __device__ __forceinline__ float ncc_old_fast(const Args &a, int px, int py, int
     project(Hm, (float)px, (float)py, ptx, pty);
     slow = false;
     if (ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f) return APD_COST_MAX;
+    bool sa_win = false;  // SA quadrant branch on the fast taps (view-major kernels: rw.sa set)
     if (a.sa_any) {
         int pidx = clampi((int)fmaf(pty, (float)W, ptx), 0, a.HW - 1);
-        if (a.sa[pidx] != 0) slow = true;
+        if (a.sa[pidx] != 0) {
+            if (RS > 1 && rw.sa != nullptr) sa_win = true;
+            else slow = true;
+        }
     }
 #ifdef APD_ABLATE_NCC  // timing-only build: skeleton without the window sums
     return fabsf(Hm.h[0] + Hm.h[8]) * 0.001f;
@@ -734,6 +832,19 @@ __device__ __forceinline__ float ncc_old_fast(const Args &a, int px, int py, int
     }
     float ss = 0.0f, sss = 0.0f, srs = 0.0f;
     const FastTex<F16, (RS > 1)> T(a, s);
+    if constexpr (RS > 1) {
+        if (rw.sa != nullptr) {
+            // each branch runs only if some lane of the wave needs it
+            if (__builtin_amdgcn_ballot_w64(!sa_win)) ncc_old_taps<FastTex<F16, true>, RS>(T, Hm, px, py, rw, ss, sss, srs);
+            if (__builtin_amdgcn_ballot_w64(sa_win)) {
+                const SaWin w = *rw.sa;
+                float s2 = 0.0f, ss2 = 0.0f, rs2 = 0.0f;
+                ncc_old_sa_taps<FastTex<F16, true>, RS>(T, Hm, px, py, rw.r, w, s2, ss2, rs2);
+                if (sa_win) return ncc_finalize(w.sr, w.srr, s2, ss2, rs2, (float)(__popc(w.mlo) + __popc(w.mhi)));
+            }
+            return ncc_old_finish(ss, sss, srs, rw.mean, rw.var);
+        }
+    }
     ncc_old_taps<FastTex<F16, (RS > 1)>, RS>(T, Hm, px, py, rw, ss, sss, srs);
     return ncc_old_finish(ss, sss, srs, rw.mean, rw.var);
 }

@@ -931,7 +931,10 @@ struct VmLds {  // static part; the cost table [9][N][64] and the weights [N][64
     float4 pnow[VM_P];
     float st[4 * VM_P];          // depth_now, cost_now, cost_init, weight_norm
 };
-#define VM_CAND(L) ((L).hyp)     // [k][p], k < 5: refinement candidates (t.w = distance)
+#define VM_CAND(L) ((L).hyp)
+// per-pixel SaWin table appended to the view-major kernels' dynamic LDS when the problem has SA masks
+static inline size_t sa_lds_bytes(const Args &a) { return a.sa_any ? VM_P * sizeof(SaWin) + 16 : 0; }
+__device__ __forceinline__ void *sa_lds_align(void *p) { return (void *)(((uintptr_t)p + 15) & ~(uintptr_t)15); }     // [k][p], k < 5: refinement candidates (t.w = distance)
 static inline size_t vm_lds_bytes(int N) {
     return APD_VM_LDS_PAD + sizeof(VmLds) + (size_t)9 * N * VM_P * sizeof(float) + (size_t)N * VM_P;
 }
@@ -981,7 +984,7 @@ __device__ __forceinline__ int scan_direction(const APD_G float *__restrict__ co
     return best;
 }
 
-template <bool F16>
+template <bool F16, bool SA>
 #ifndef VM_MINW
 #define VM_MINW 3  // waves per SIMD -> VGPR budget 512 / VM_MINW
 #endif
@@ -991,6 +994,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     VmLds &L = *reinterpret_cast<VmLds *>(apd_dyn_lds);
     float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64], later [5][N][64]
     uint8_t *wts = reinterpret_cast<uint8_t *>(costL + 9 * N * VM_P);    // [N][64] view weights
+    SaWin *saw = reinterpret_cast<SaWin *>(wts + N * VM_P);              // [64] when a.sa_any
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int first = blk * VM_P;
     const int np = min(VM_P, count - first);
@@ -1016,6 +1020,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
                 const int i = k / 6, j = k - 6 * (k / 6);
                 L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
             }
+            if (SA && wave == VM_WAVES - 1) saw[p] = sa_window(a, px, py);
         }
     }
     __syncthreads();
@@ -1025,7 +1030,8 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     const bool pv1 = p1 < np;
     int c1 = 0, px1 = 0, py1 = 0;
     if (pv1) { c1 = list[first + p1]; py1 = c1 / W; px1 = c1 - py1 * W; }
-    const RefWin rw = refwin_from_lds<VM_P>(&L.refw[p1]);
+    RefWin rw = refwin_from_lds<VM_P>(&L.refw[p1]);
+    if (SA) rw.sa = &saw[p1];
     // tasks whose window needs the out-of-line path are collected in `defer` (bit k = k-th task of
     // this wave) and evaluated after the loop, so the hot loop holds no call.
     uint64_t defer[2] = {0, 0};  // up to 128 tasks per wave (9 * 31 / VM_WAVES)
@@ -2515,13 +2521,14 @@ static inline int dw_chunk(int N) { return std::max(1, std::min(61, DW_CHUNK_BYT
 static inline size_t dw_lds_bytes(int N) {
     return sizeof(DwLds) + (size_t)dw_chunk(N) * N * VM_P * sizeof(float) + (size_t)2 * N * VM_P;
 }
-template <bool F16>
+template <bool F16, bool SA>
 __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, int chunk, int tw) {
     const int N = a.N, W = a.W, H = a.H;
     DwLds &L = *reinterpret_cast<DwLds *>(apd_dyn_lds);
     float *tcL = reinterpret_cast<float *>(&L + 1);                 // [chunk][N][64]
     uint8_t *wts = reinterpret_cast<uint8_t *>(tcL + chunk * N * VM_P);  // [N][64]
     uint8_t *vslot = wts + N * VM_P;                                 // [N][64] pixel slots per view
+    SaWin *saw = reinterpret_cast<SaWin *>(vslot + N * VM_P);         // [64] when a.sa_any
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
     const APD_G Cam &cam0 = a.cams[0];
@@ -2546,6 +2553,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
             const int i = k / 6, j = k - 6 * (k / 6);
             L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
         }
+        if (SA && wave == VM_WAVES - 1) saw[p] = sa_window(a, px, py);
     }
     __syncthreads();
     if (wave == 0 && pv) {  // baseline / weight norm over the selected views, in view order
@@ -2612,7 +2620,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 const int qx = xy & 0xFFFF, qy = xy >> 16;
                 const float pdepth = cam0.K[0] * L.base[q] / (L.disp[q] + (float)(d0 + dd - 30));
                 const bool eval = has && !(pdepth < a.dmin || pdepth > a.dmax);
-                const RefWin rwq{&L.refw[q], L.rmean[q], L.rvar[q]};
+                const RefWin rwq{&L.refw[q], L.rmean[q], L.rvar[q], SA ? &saw[q] : nullptr};
                 float4 tp = L.pl[q];
                 float tc = 0.0f;
                 {
@@ -2735,13 +2743,14 @@ template <bool F16, bool APD>
 static inline size_t ri_lds_bytes(int N) {
     return (APD ? sizeof(RiApdLds<F16>) : sizeof(RiLds)) + (size_t)N * VM_P * sizeof(float);
 }
-template <bool F16, bool APD>
+template <bool F16, bool APD, bool SA>
 __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, int tw) {
     const int N = a.N;
     WvRefT<F16> *W = APD ? &reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds)->w : nullptr;
     RiLds &L = APD ? reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds)->r : *reinterpret_cast<RiLds *>(apd_dyn_lds);
     float *cvL = APD ? reinterpret_cast<float *>(reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds) + 1)
                      : reinterpret_cast<float *>(&L + 1);  // [N][64]
+    SaWin *saw = reinterpret_cast<SaWin *>(sa_lds_align(cvL + N * VM_P));  // [64] when a.sa_any
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (WAVE - 1);
     const TilePix T = tile_pix(a, tw, lane);
     const int p = lane, px = T.px, py = T.py, c = T.c;
@@ -2765,6 +2774,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, in
             const int i = k / 6, j = k - 6 * (k / 6);
             L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
         }
+        if (SA && wave == VM_WAVES - 1) saw[p] = sa_window(a, px, py);
         if constexpr (APD) {
             if (a.weak[c] == APD_WEAK) {  // the NCC-New reference side (anchors, windows, SA masks)
                 const APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
@@ -2784,7 +2794,8 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, in
         }
     }
     __syncthreads();
-    const RefWin rw = refwin_from_lds<VM_P>(&L.refw[p]);
+    RefWin rw = refwin_from_lds<VM_P>(&L.refw[p]);
+    if (SA) rw.sa = &saw[p];
     const bool use_new = a.use_apd && a.weak[c] == APD_WEAK;
     const float4 pl = L.pl[p];
     uint64_t defer = 0;
@@ -2866,7 +2877,7 @@ static inline int lr_chunk(int N) { return std::max(1, std::min(11, 32768 / (2 *
 static inline size_t lr_lds_bytes(int N) {
     return sizeof(LrLds) + (size_t)(2 * lr_chunk(N) + 1) * N * VM_P * sizeof(float) + (size_t)N * VM_P * sizeof(int);
 }
-template <bool F16>
+template <bool F16, bool SA>
 __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, int chunk, int tw) {
     const int N = a.N;
     LrLds &L = *reinterpret_cast<LrLds *>(apd_dyn_lds);
@@ -2874,6 +2885,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, i
     float *nvL = t0L + N * VM_P;                      // [chunk][N][64] NCC
     float *gvL = nvL + chunk * N * VM_P;              // [chunk][N][64] gf * geometric
     int *wts = reinterpret_cast<int *>(gvL + chunk * N * VM_P);
+    SaWin *saw = reinterpret_cast<SaWin *>(wts + N * VM_P);           // [64] when a.sa_any
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (WAVE - 1);
     const TilePix T = tile_pix(a, tw, lane);
     const int p = lane, px = T.px, py = T.py, c = T.c;
@@ -2890,9 +2902,11 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, i
             const int i = k / 6, j = k - 6 * (k / 6);
             L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
         }
+        if (SA && wave == VM_WAVES - 1) saw[p] = sa_window(a, px, py);
     }
     __syncthreads();
-    const RefWin rw = refwin_from_lds<VM_P>(&L.refw[p]);
+    RefWin rw = refwin_from_lds<VM_P>(&L.refw[p]);
+    if (SA) rw.sa = &saw[p];
     const float4 pl = L.pl[p];
     const float od = pl.w;
     const uint32_t sv = L.sel[p];
@@ -3361,6 +3375,19 @@ static inline T devptr(const void *p) { return reinterpret_cast<T>(reinterpret_c
         else hipLaunchKernelGGL((kern<false>), grid, block, lds, stream, __VA_ARGS__);            \
     } while (0)
 
+// ... and of its SA-masked (SA quadrant windows on the fast taps) or unmasked form
+#define LAUNCH_TEX_SA(kern, grid, block, lds, stream, ...)                                          \
+    do {                                                                                         \
+        const bool sa_ = ctx->args.sa_any != 0;                                                  \
+        if (ctx->args.tex_f16) {                                                                 \
+            if (sa_) hipLaunchKernelGGL((kern<true, true>), grid, block, lds, stream, __VA_ARGS__); \
+            else hipLaunchKernelGGL((kern<true, false>), grid, block, lds, stream, __VA_ARGS__);  \
+        } else {                                                                                 \
+            if (sa_) hipLaunchKernelGGL((kern<false, true>), grid, block, lds, stream, __VA_ARGS__); \
+            else hipLaunchKernelGGL((kern<false, false>), grid, block, lds, stream, __VA_ARGS__); \
+        }                                                                                        \
+    } while (0)
+
 static inline unsigned blocks_for(size_t n, int per_block) { return (unsigned)((n + per_block - 1) / per_block); }
 static inline unsigned group_blocks(int n_pixels, int N) {
     const int P = WAVE / N;
@@ -3412,34 +3439,20 @@ apd_ctx *apd_create(int32_t device) {
         if (t == 4 || t == 8 || t == 16 || t == 32 || t == 64) ctx->tile_w = t;
     }
     // the view-major sweep's LDS grows with N (> 64 KiB from N = 15 on); gfx950 has 160 KiB per CU
-    (void)hipFuncSetAttribute((const void *)k_sweep_strong_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_weak_cand_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_weak_cand_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_sweep_strong_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_depth_to_weak_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_depth_to_weak_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_local_refine_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_local_refine_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_random_init_vm<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_random_init_vm<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_random_init_vm<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_random_init_vm<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_sweep_weak_vm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void *)k_sweep_weak_vm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    const void *vm_kernels[] = {
+        (const void *)k_sweep_strong_vm<true, false>, (const void *)k_sweep_strong_vm<false, false>,
+        (const void *)k_sweep_strong_vm<true, true>, (const void *)k_sweep_strong_vm<false, true>,
+        (const void *)k_weak_cand_vm<true>, (const void *)k_weak_cand_vm<false>,
+        (const void *)k_sweep_weak_vm<true>, (const void *)k_sweep_weak_vm<false>,
+        (const void *)k_depth_to_weak_vm<true, false>, (const void *)k_depth_to_weak_vm<false, false>,
+        (const void *)k_depth_to_weak_vm<true, true>, (const void *)k_depth_to_weak_vm<false, true>,
+        (const void *)k_local_refine_vm<true, false>, (const void *)k_local_refine_vm<false, false>,
+        (const void *)k_local_refine_vm<true, true>, (const void *)k_local_refine_vm<false, true>,
+        (const void *)k_random_init_vm<true, false, false>, (const void *)k_random_init_vm<false, false, false>,
+        (const void *)k_random_init_vm<true, true, false>, (const void *)k_random_init_vm<false, true, false>,
+        (const void *)k_random_init_vm<true, false, true>, (const void *)k_random_init_vm<false, false, true>,
+        (const void *)k_random_init_vm<true, true, true>, (const void *)k_random_init_vm<false, true, true>};
+    for (const void *k : vm_kernels) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return ctx;
 }
 
@@ -3745,11 +3758,21 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         const int tw = ctx->dw_tile_w, th = VM_P / tw;
         const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
         if (a.use_apd) {
-            if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, true>(a.N)), s, a, tw);
-            else hipLaunchKernelGGL((k_random_init_vm<false, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, true>(a.N)), s, a, tw);
+            if (a.sa_any) {
+                if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, true, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, true>(a.N) + sa_lds_bytes(a)), s, a, tw);
+                else hipLaunchKernelGGL((k_random_init_vm<false, true, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, true>(a.N) + sa_lds_bytes(a)), s, a, tw);
+            } else {
+                if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, true, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, true>(a.N)), s, a, tw);
+                else hipLaunchKernelGGL((k_random_init_vm<false, true, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, true>(a.N)), s, a, tw);
+            }
         } else {
-            if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, false>(a.N)), s, a, tw);
-            else hipLaunchKernelGGL((k_random_init_vm<false, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, false>(a.N)), s, a, tw);
+            if (a.sa_any) {
+                if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, false, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, false>(a.N) + sa_lds_bytes(a)), s, a, tw);
+                else hipLaunchKernelGGL((k_random_init_vm<false, false, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, false>(a.N) + sa_lds_bytes(a)), s, a, tw);
+            } else {
+                if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, false, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, false>(a.N)), s, a, tw);
+                else hipLaunchKernelGGL((k_random_init_vm<false, false, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, false>(a.N)), s, a, tw);
+            }
         }
     } else {
         LAUNCH_TEX(k_random_init, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);
@@ -3779,7 +3802,7 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
         Args ak = a;
         if (ctx->prof && ctx->evals.p) ak.evals = (APD_G unsigned long long *)ctx->evals.p;
         if (ctx->sweep_vm)
-            LAUNCH_TEX(k_sweep_strong_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), vm_lds_bytes(a.N), s,
+            LAUNCH_TEX_SA(k_sweep_strong_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), vm_lds_bytes(a.N) + sa_lds_bytes(a), s,
                        ak, (const int *)list_ptr(ctx, colour), n, iter);
         else
             LAUNCH_TEX(k_sweep_strong, dim3(group_blocks(n, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a,
@@ -3838,7 +3861,7 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
         if (ctx->sweep_vm) {
             const int tw = ctx->dw_tile_w, th = VM_P / tw;
             const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
-            LAUNCH_TEX(k_depth_to_weak_vm, dim3(nb), dim3(VM_BLOCK), dw_lds_bytes(a.N), s, a, dw_chunk(a.N), tw);
+            LAUNCH_TEX_SA(k_depth_to_weak_vm, dim3(nb), dim3(VM_BLOCK), dw_lds_bytes(a.N) + sa_lds_bytes(a), s, a, dw_chunk(a.N), tw);
         } else {
             const size_t lds = group_lds_bytes(a.N, 61 + 36);
             LAUNCH_TEX(k_depth_to_weak, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), lds, s, a);
@@ -3848,7 +3871,7 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
     if (ctx->sweep_vm) {
         const int tw = ctx->dw_tile_w, th = VM_P / tw;
         const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
-        LAUNCH_TEX(k_local_refine_vm, dim3(nb), dim3(VM_BLOCK), lr_lds_bytes(a.N), s, a, lr_chunk(a.N), tw);
+        LAUNCH_TEX_SA(k_local_refine_vm, dim3(nb), dim3(VM_BLOCK), lr_lds_bytes(a.N) + sa_lds_bytes(a), s, a, lr_chunk(a.N), tw);
     } else {
         LAUNCH_TEX(k_local_refine, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);
     }

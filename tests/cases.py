@@ -75,6 +75,8 @@ def refine_problem(sc, priors, ref=0, n_src=None, state=A.REFINE_ITER, geom=True
         arr.params.ransac_threshold = 0.01 - 1 * 0.00125
     if sa:
         arr.sa_mask = sc.labels[ref].copy()
+        if sa == "zero_band":  # label 0 (no SA window) over a column band: waves mix both window forms
+            arr.sa_mask[:, sc.width // 3: sc.width // 2] = 0
     for k, v in params.items():
         setattr(arr.params, k, v)
     return arr
@@ -95,6 +97,9 @@ CASES = {
     "refine_init_apd_small": (40, 28, 2, "apd"),  # anchors and RANSAC where most searches leave the image
     "first_n31": (64, 48, 31, "first"),           # the reference's maximum (32 images): largest LDS tables
     "refine_iter_n31_apd_geom": (48, 40, 31, "apd_geom"),
+    "first_n6_sa0": (112, 84, 6, "first_sa0"),          # SA quadrant windows in init + Strong sweep
+    "refine_iter_geom_sa0": (128, 96, 4, "geom_sa0"),   # ... and in DepthToWeak / LocalRefine
+    "refine_iter_apd_geom_sa0": (96, 72, 4, "apd_geom_sa0"),
 }
 
 
@@ -103,6 +108,11 @@ def make_case(name, oracle_run):
     sc = scene(w, h, max(n, 4))
     if kind == "first":
         return base_problem(sc, 0, n)
+    if kind == "first_sa0":
+        arr = base_problem(sc, 0, n)
+        arr.sa_mask = sc.labels[0].copy()
+        arr.sa_mask[:, w // 3: w // 2] = 0
+        return arr
     priors = first_pass(oracle_run, sc, n)
     if kind == "geom":
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True)
@@ -110,6 +120,10 @@ def make_case(name, oracle_run):
         return refine_problem(sc, priors, 0, n, state=A.REFINE_INIT, geom=False, apd=True)
     if kind == "apd_geom_sa":
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, sa=True)
+    if kind == "geom_sa0":
+        return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, sa="zero_band")
+    if kind == "apd_geom_sa0":
+        return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, sa="zero_band")
     if kind == "apd_geom":
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True)
     raise KeyError(kind)
