@@ -584,6 +584,13 @@ struct FastTex {
         t.off = ((__umul24((uint32_t)qy >> 8, W1) + ((uint32_t)qx >> 8)) << SHIFT) + vbase;
 #endif
         t.f = (apd_f2){(float)(qx & 255), (float)(qy & 255)} * 0.00390625f;
+#ifdef APD_ABLATE_VALU  // timing-only build: APD_ABLATE_VALU extra (dead) VALU instructions per tap, same values
+#pragma unroll
+        for (int i = 0; i < APD_ABLATE_VALU; ++i) {
+            float d;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(d) : "v"(p.x));
+        }
+#endif
         return t;
     }
     using Raw = typename std::conditional<F16, apd_u2_a4, float4>::type;
