@@ -2536,6 +2536,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
     // the workgroup's pixels: a tw x (64/tw) tile (XCD-aware tile order); pixels outside the image idle
     const int th = VM_P / tw, tiles_x = (W + tw - 1) / tw;
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const size_t lr_slots = (size_t)gridDim.x * VM_P;  // LocalRefine hand-over: one slot per tile lane
     const int tx = blk % tiles_x, ty = blk / tiles_x;
     const int gx = tx * tw + (p % tw), gy = ty * th + (p / tw);
     const bool pv = gx < W && gy < H;
@@ -2623,15 +2624,20 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 const RefWin rwq{&L.refw[q], L.rmean[q], L.rvar[q], SA ? &saw[q] : nullptr};
                 float4 tp = L.pl[q];
                 float tc = 0.0f;
-                {
-                    if (eval) {
-                        tp.w = dist2origin(cam0, qx, qy, pdepth, tp);
-                        bool slow;
-                        tc = ncc_old_fast<F16, VM_P>(a, qx, qy, v + 1, tp, rwq, slow);
-                        if (slow) defer |= 1ull << k;
-                    }
+                bool slow = false;
+                if (eval) {
+                    tp.w = dist2origin(cam0, qx, qy, pdepth, tp);
+                    tc = ncc_old_fast<F16, VM_P>(a, qx, qy, v + 1, tp, rwq, slow);
+                    if (slow) defer |= 1ull << k;
                 }
-                if (eval && geom) tc = fmaf(gf, geom_cost(a, qx, qy, v + 1, tp), tc);
+                const float g = (eval && geom) ? geom_cost(a, qx, qy, v + 1, tp) : 0.0f;
+                const int pd = d0 + dd - 30;
+                if (a.lr_ncc && eval && !slow && pd >= -5 && pd <= 5) {
+                    const size_t i = (size_t)((pd + 5) * N + v) * lr_slots + (size_t)blk * VM_P + q;
+                    a.lr_ncc[i] = tc;
+                    if (geom) a.lr_geo[i] = g;
+                }
+                if (eval && geom) tc = fmaf(gf, g, tc);
                 if (has) tcL[(dd * N + v) * VM_P + q] = tc;
             }
         }
@@ -2650,7 +2656,14 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 float4 tp = L.pl[q];
                 tp.w = dist2origin(cam0, qx, qy, pdepth, tp);
                 float tc = ncc_old_slow<F16>(a.self, qx, qy, v + 1, tp, &L.refw[q], VM_P, L.rmean[q], L.rvar[q]);
-                if (geom) tc = fmaf(gf, geom_cost(a, qx, qy, v + 1, tp), tc);
+                const float g = geom ? geom_cost(a, qx, qy, v + 1, tp) : 0.0f;
+                const int pd = d0 + dd - 30;
+                if (a.lr_ncc && pd >= -5 && pd <= 5) {
+                    const size_t i = (size_t)((pd + 5) * N + v) * lr_slots + (size_t)blk * VM_P + q;
+                    a.lr_ncc[i] = tc;
+                    if (geom) a.lr_geo[i] = g;
+                }
+                if (geom) tc = fmaf(gf, g, tc);
                 tcL[(dd * N + v) * VM_P + q] = tc;
             }
         }
@@ -2964,6 +2977,11 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, i
     __syncthreads();
     const bool run = T.pv && L.run[p] != 0;
     const float base = L.base[p], disp = L.disp[p], wn = L.wn[p];
+    // DepthToWeak evaluated this pixel's samples (same plane, views, base line and depths: active
+    // there = not within 6 px of the border, od != 0, a selected view; run implies the last two)
+    const bool dwc = a.lr_ncc != nullptr &&
+                     !(px < 6 || py < 6 || px >= a.W - 6 || py >= a.H - 6);
+    const size_t lr_slots = (size_t)gridDim.x * VM_P, lr_px = (size_t)xcd_remap(blockIdx.x, gridDim.x) * VM_P + p;
     float min_cost = 2.0f, best = od;  // tracked by wave 0's lane of the pixel
     for (int d0 = 0; d0 < 11; d0 += chunk) {
         const int dc = min(chunk, 11 - d0);
@@ -2975,12 +2993,18 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, i
             const bool in_range = !(pdepth < a.dmin || pdepth > a.dmax);
             float nv = 0.0f, gv = 0.0f;
             if (run && in_range && ((sv >> v) & 1u)) {
-                float4 tp = pl;
-                tp.w = dist2origin(cam0, px, py, pdepth, tp);
-                bool slow;
-                nv = ncc_old_fast<F16, VM_P>(a, px, py, v + 1, tp, rw, slow);
-                if (slow) defer |= 1ull << k;
-                if (geom) gv = gf * geom_cost(a, px, py, v + 1, tp);
+                if (dwc) {
+                    const size_t i = (size_t)((d + 5) * N + v) * lr_slots + lr_px;
+                    nv = a.lr_ncc[i];
+                    if (geom) gv = gf * a.lr_geo[i];
+                } else {
+                    float4 tp = pl;
+                    tp.w = dist2origin(cam0, px, py, pdepth, tp);
+                    bool slow;
+                    nv = ncc_old_fast<F16, VM_P>(a, px, py, v + 1, tp, rw, slow);
+                    if (slow) defer |= 1ull << k;
+                    if (geom) gv = gf * geom_cost(a, px, py, v + 1, tp);
+                }
             }
             nvL[t * VM_P + p] = nv;
             gvL[t * VM_P + p] = gv;
@@ -3249,7 +3273,7 @@ struct apd_ctx {
     std::string err;
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
-        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, wdone;
+        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, wdone, lrs;
     int n_near = 0;
     int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
     Args args{};
@@ -3258,6 +3282,7 @@ struct apd_ctx {
     int dw_tile_w = 8;             // DepthToWeak pixel tile width (64 / tile height); APD_DW_TILE_W
     int tile_w = 8;                // sweep list tile width (tile = tile_w x 256/tile_w positions); APD_TILE_W
     bool cand_pairs = true;        // Weak sweep candidates through k_weak_cand_vm; APD_NO_CAND_PAIRS=1 disables
+    bool lr_handover = true;       // LocalRefine reads DepthToWeak's samples; APD_NO_LR_HANDOVER=1 disables
     int weak_count = 0;
     int cnt[4] = {0, 0, 0, 0};     // strong black, strong red, weak black, weak red
     size_t list_cap = 0;
@@ -3429,6 +3454,7 @@ apd_ctx *apd_create(int32_t device) {
     for (auto &e : ctx->ev) (void)hipEventCreate(&e);
     ctx->sweep_vm = getenv("APD_SWEEP_LANES") == nullptr;
     ctx->cand_pairs = getenv("APD_NO_CAND_PAIRS") == nullptr;
+    ctx->lr_handover = getenv("APD_NO_LR_HANDOVER") == nullptr;
     // tile_pix needs the tile width to divide the 64-pixel tile (otherwise two workgroups share pixels)
     if (const char *e = getenv("APD_DW_TILE_W")) {
         const int t = atoi(e);
@@ -3463,7 +3489,8 @@ void apd_destroy(apd_ctx *ctx) {
     DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
-                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand, &ctx->wdone};
+                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand, &ctx->wdone,
+                      &ctx->lrs};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
@@ -3857,6 +3884,25 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
                                (const int *)list_ptr(ctx, colour), n);
     }
     if (ctx->want_curve && ctx->curve.p) a.curve = devptr<decltype(a.curve)>(ctx->curve.p);
+    a.lr_ncc = nullptr;
+    a.lr_geo = nullptr;
+    if (ctx->sweep_vm && ctx->lr_handover) {
+        // DepthToWeak hands LocalRefine the NCC-Old / geometric terms of the 11 samples they share
+        // ([11][N][tile slots] each); skipped above 16 GiB (LocalRefine then evaluates them itself)
+        const int tw = ctx->dw_tile_w, th = VM_P / tw;
+        const size_t slots = (size_t)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th)) * VM_P;
+        const size_t plane = (size_t)11 * a.N * slots;
+        const size_t bytes = plane * sizeof(float) * (a.geom ? 2 : 1);
+        if (bytes <= ((size_t)16 << 30)) {
+            if (ensure(ctx, ctx->lrs, bytes) == APD_OK) {
+                a.lr_ncc = devptr<decltype(a.lr_ncc)>(ctx->lrs.p);
+                a.lr_geo = a.geom ? devptr<decltype(a.lr_geo)>((float *)ctx->lrs.p + plane) : nullptr;
+            } else {  // not fatal: clear the allocation error
+                (void)hipGetLastError();
+                ctx->err.clear();
+            }
+        }
+    }
     {
         if (ctx->sweep_vm) {
             const int tw = ctx->dw_tile_w, th = VM_P / tw;

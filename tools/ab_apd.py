@@ -2,7 +2,8 @@
 library builds, interleaved in one process. Priors come from FIRST_INIT runs of the neighbouring
 views (first library), as in tools/time_apd_pass.py. Prints the HIP-event breakdown per build and
 whether every build's outputs are bit-identical to the first's.
-Usage: python tools/ab_apd.py libA.so[:ENV=VAL,...] libB.so [...]   (AB_W / AB_H / AB_N / AB_ROUNDS / AB_SA)"""
+Usage: python tools/ab_apd.py libA.so[:ENV=VAL,...] libB.so [...]   (AB_W / AB_H / AB_N / AB_ROUNDS / AB_SA;
+AB_FIRST=1 times a FIRST_INIT problem instead)"""
 import os, sys, statistics
 import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -34,9 +35,12 @@ def run(e, arr):
     return e.results(A.Outputs(arr.width, arr.height, len(arr.images) - 1))
 
 
-priors = [run(e0, cases.base_problem(sc, r, N)) for r in range(len(sc.images))]
-arr = cases.refine_problem(sc, priors, 0, N, state=A.REFINE_ITER, geom=True, apd=True,
-                           sa=os.environ.get("AB_SA") == "1")  # AB_SA=1: the scene's plane labels as SA masks
+if os.environ.get("AB_FIRST") == "1":
+    arr = cases.base_problem(sc, 0, N)
+else:
+    priors = [run(e0, cases.base_problem(sc, r, N)) for r in range(len(sc.images))]
+    arr = cases.refine_problem(sc, priors, 0, N, state=A.REFINE_ITER, geom=True, apd=True,
+                               sa=os.environ.get("AB_SA") == "1")  # AB_SA=1: the scene's plane labels as SA masks
 outs = {}
 res = {n: [] for n, _ in engines}
 for r in range(ROUNDS):
