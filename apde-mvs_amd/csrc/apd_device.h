@@ -55,6 +55,10 @@ struct Args {
     float ikx, iky, cxk, cyk;              // Kr^-1 pieces: 1/fx, 1/fy, cx/fx, cy/fy
     float anc_cos, anc_sin, anc_thr;       // GenAnchors per-launch constants (APD.cu:1897-1901)
     int anc_shift;
+    // GenAnchors inlier test d / (dmax - dmin) < ransac_thr as d < anc_dlim (d >= 0): the smallest d
+    // whose IEEE quotient reaches the threshold, found on the host (the quotient is monotone in d)
+    float anc_dlim;
+    int anc_dlim_ok;
     size_t qstride;                        // float4 elements per source quad image ((W+1)*(H+1))
     const APD_G float *ref;                // reference image, H*W
     const APD_G float4 *quad;              // source images 1..N in quad layout, view v at (v-1)*qstride
@@ -154,6 +158,20 @@ struct Rng {
             key0 += 0x9E3779B9u; key1 += 0xBB67AE85u;
         }
         b0 = x0; b1 = x1; b2 = x2; b3 = x3;
+    }
+    // block `blk` of this stream (draws 4*blk .. 4*blk+3), state untouched
+    __device__ __forceinline__ uint4 block(uint32_t blk) const {
+        uint32_t x0 = c0, x1 = c1, x2 = blk, x3 = RNG_TAG;
+        uint32_t key0 = k0, key1 = k1;
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            uint32_t lo0 = 0xD2511F53u * x0, hi0 = __umulhi(0xD2511F53u, x0);
+            uint32_t lo1 = 0xCD9E8D57u * x2, hi1 = __umulhi(0xCD9E8D57u, x2);
+            uint32_t n0 = hi1 ^ x1 ^ key0, n2 = hi0 ^ x3 ^ key1;
+            x0 = n0; x1 = lo1; x2 = n2; x3 = lo0;
+            key0 += 0x9E3779B9u; key1 += 0xBB67AE85u;
+        }
+        return make_uint4(x0, x1, x2, x3);
     }
     // curand()
     __device__ __forceinline__ uint32_t u32() {

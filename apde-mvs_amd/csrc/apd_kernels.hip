@@ -360,6 +360,21 @@ __device__ __forceinline__ bool point_in_triangle(int ax, int ay, int bx, int by
 }
 
 // GenAnchors (APD.cu:1857-2082): directional search for strong anchors + RANSAC plane.
+__device__ __forceinline__ bool anc_inlier(const Args &a, float d, float depth_diff) {
+    return a.anc_dlim_ok ? d < a.anc_dlim : d / depth_diff < a.ransac_thr;
+}
+// x % d for d in 1..32 without an integer division: with M = floor((2^64 - 1) / d) + 1, the low 64 bits
+// of M * x are frac(x / d) * 2^64 (to within d * 2^-32 < 1/d), whose high part times d is x mod d
+// (Lemire, Kaser, Kurz 2019 for 32-bit x and d)
+struct FastMod {
+    uint64_t M;
+    uint32_t d;
+    __device__ __forceinline__ explicit FastMod(uint32_t dd) : M(~0ull / dd + 1ull), d(dd) {}
+    __device__ __forceinline__ uint32_t mod(uint32_t x) const {
+        const uint64_t low = M * (uint64_t)x;
+        return (uint32_t)__umul64hi(low, (uint64_t)d);
+    }
+};
 __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
     const int c = blockIdx.x * BLOCK + threadIdx.x;
     if (c >= a.HW) return;
@@ -378,7 +393,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
     for (int i = 0; i < 32; ++i) sp[i] = make_short2(-1, -1);
     int odi = -1, nsp = 0;
     const int rt = a.rotate_time;
-    const unsigned shift = (unsigned)a.anc_shift;
+    const FastMod fshift((uint32_t)a.anc_shift);
     for (int odx = -1; odx <= 1; ++odx) {
         for (int ody = -1; ody <= 1; ++ody) {
             if (odx == 0 && ody == 0) continue;
@@ -390,25 +405,35 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
                 for (int radius = 2; radius <= APD_MAX_SEARCH_RADIUS; radius = min(radius * 2, radius + 25)) {
                     float tx = (float)px + dx * (float)radius, ty = (float)py + dy * (float)radius;
                     if (tx < 0 || ty < 0 || tx >= (float)W || ty >= (float)H) break;
+                    // The 4 attempts of this radius: attempt t draws 4 values, i.e. exactly Philox block
+                    // n/4 + t (n stays a multiple of 4 throughout the search), so all four are generated
+                    // and their nearest-STRONG lookups issued together, then judged in order; the stream
+                    // resumes after the first successful attempt, as if the later ones never drew.
+                    const uint32_t n0 = g.n;
+                    short2 nn[4];
+                    bool in[4];
+#pragma unroll
                     for (int t = 0; t < 4; ++t) {
-                        uint32_t sx = g.u32();
-                        uint32_t mx = g.u32();
-                        int rxs = (int)(((sx % 2u == 0) ? mx : (0u - mx)) % shift);
-                        uint32_t sy = g.u32();
-                        uint32_t my = g.u32();
-                        int rys = (int)(((sy % 2u == 0) ? my : (0u - my)) % shift);
+                        const uint4 b = g.block((n0 >> 2) + (uint32_t)t);
+                        int rxs = (int)fshift.mod((b.x % 2u == 0) ? b.y : (0u - b.y));
+                        int rys = (int)fshift.mod((b.z % 2u == 0) ? b.w : (0u - b.w));
                         float ddx = dx * 20 + (float)rxs, ddy = dy * 20 + (float)rys;
                         normalize2(ddx, ddy);
                         int ax = (int16_t)(int)((float)px + ddx * (float)radius);
                         int ay = (int16_t)(int)((float)py + ddy * (float)radius);
-                        if (ax < margin || ay < margin || ax >= W - margin || ay >= H - margin) continue;
-                        short2 nn = a.nearest[ax + ay * W];
-                        if (nn.x == -1 || nn.y == -1) continue;
-                        float tdx = (float)(nn.x - px), tdy = (float)(nn.y - py);
+                        in[t] = !(ax < margin || ay < margin || ax >= W - margin || ay >= H - margin);
+                        nn[t] = in[t] ? a.nearest[ax + ay * W] : make_short2(-1, -1);
+                    }
+                    int used = 4;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (used < 4 || !in[t] || nn[t].x == -1 || nn[t].y == -1) continue;
+                        float tdx = (float)(nn[t].x - px), tdy = (float)(nn[t].y - py);
                         normalize2(tdx, tdy);
                         float ca = tdx * dx + tdy * dy;
-                        if (ca > a.anc_thr) { sp[di] = nn; dvalid |= 1u << di; nsp++; break; }
+                        if (ca > a.anc_thr) { sp[di] = nn[t]; dvalid |= 1u << di; nsp++; used = t + 1; }
                     }
+                    g.n = n0 + 4u * (uint32_t)used;
                     if ((dvalid >> di) & 1u) break;
                 }
                 float rx = dx * a.anc_cos - dy * a.anc_sin;
@@ -439,10 +464,11 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
     bool has = false;
     float min_cost = APD_FLT_MAX;
     int max_count = 3;
+    const FastMod fm((uint32_t)vc);
     for (int it = 0; it < 50; ++it) {
-        int ia = (int)(g.u32() % (uint32_t)vc);
-        int ib = (int)(g.u32() % (uint32_t)vc);
-        int ic = (int)(g.u32() % (uint32_t)vc);
+        int ia = (int)fm.mod(g.u32());
+        int ib = (int)fm.mod(g.u32());
+        int ic = (int)fm.mod(g.u32());
         if (ia == ib || ib == ic || ia == ic) continue;
         if (!point_in_triangle(vp[ia].x, vp[ia].y, vp[ib].x, vp[ib].y, vp[ic].x, vp[ic].y, px, py)) continue;
         const float *A = v3[ia], *B = v3[ib], *C = v3[ic];
@@ -455,7 +481,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
         int tcnt = 0;
         for (int k = 0; k < vc; ++k) {
             float d = fabsf(cr.x * v3[k][0] + cr.y * v3[k][1] + cr.z * v3[k][2] + cr.w);
-            if (d / depth_diff < a.ransac_thr) tcnt++;
+            if (anc_inlier(a, d, depth_diff)) tcnt++;
         }
         if (tcnt < 6) continue;
         if (tcnt > max_count) {
@@ -471,7 +497,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
     float wgt[32];
     for (int i = 0; i < vc; ++i) {
         float d = fabsf(best.x * v3[i][0] + best.y * v3[i][1] + best.z * v3[i][2] + best.w);
-        if (d / depth_diff >= a.ransac_thr) { vp[i] = make_short2(-1, -1); wgt[i] = APD_FLT_MAX; continue; }
+        if (!anc_inlier(a, d, depth_diff)) { vp[i] = make_short2(-1, -1); wgt[i] = APD_FLT_MAX; continue; }
         if (i == ua || i == ub || i == uc) d -= 1;
         wgt[i] = d;
     }
@@ -3413,6 +3439,28 @@ static inline T devptr(const void *p) { return reinterpret_cast<T>(reinterpret_c
         }                                                                                        \
     } while (0)
 
+// The smallest non-negative float d with fl(d / D) >= t (IEEE single division, monotone in d for
+// D > 0), so that fl(d / D) < t <=> d < limit for every d >= 0 (NaN: false both ways). False when D
+// or t rules the search out; GenAnchors then divides.
+static bool inlier_limit(float D, float t, float *limit) {
+    if (!(D > 0.0f) || !std::isfinite(D) || !std::isfinite(t)) return false;
+    auto reach = [&](uint32_t bits) {
+        float d;
+        std::memcpy(&d, &bits, 4);
+        volatile float q = d / D;
+        return q >= t;
+    };
+    uint32_t lo = 0u, hi = 0x7f800000u;  // [+0, +inf]
+    if (!reach(hi)) return false;
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (reach(mid)) hi = mid;
+        else lo = mid + 1u;
+    }
+    std::memcpy(limit, &lo, 4);
+    return true;
+}
+
 static inline unsigned blocks_for(size_t n, int per_block) { return (unsigned)((n + per_block - 1) / per_block); }
 static inline unsigned group_blocks(int n_pixels, int N) {
     const int P = WAVE / N;
@@ -3647,6 +3695,7 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
         a.anc_thr = (float)cos((double)(angle / 2.0f) * 3.14159265358979323846 / 180.0f);
         const int sr = (int)(tan((double)(angle / 2.0f) * 3.14159265358979323846 / 180.0f) * 20);
         a.anc_shift = sr < 1 ? 1 : sr;
+        a.anc_dlim_ok = inlier_limit(a.dmax - a.dmin, a.ransac_thr, &a.anc_dlim) ? 1 : 0;
     }
     a.qstride = qstride;
     a.ref = devptr<decltype(a.ref)>(ctx->imgs.p);
