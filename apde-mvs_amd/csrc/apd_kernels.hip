@@ -3937,12 +3937,13 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
     a.lr_geo = nullptr;
     if (ctx->sweep_vm && ctx->lr_handover) {
         // DepthToWeak hands LocalRefine the NCC-Old / geometric terms of the 11 samples they share
-        // ([11][N][tile slots] each); skipped above 16 GiB (LocalRefine then evaluates them itself)
+        // ([11][N][tile slots] each: 21.5 GB at 6048x4032, N = 10, with geometry); skipped above
+        // 48 GiB (LocalRefine then evaluates them itself)
         const int tw = ctx->dw_tile_w, th = VM_P / tw;
         const size_t slots = (size_t)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th)) * VM_P;
         const size_t plane = (size_t)11 * a.N * slots;
         const size_t bytes = plane * sizeof(float) * (a.geom ? 2 : 1);
-        if (bytes <= ((size_t)16 << 30)) {
+        if (bytes <= ((size_t)48 << 30)) {
             if (ensure(ctx, ctx->lrs, bytes) == APD_OK) {
                 a.lr_ncc = devptr<decltype(a.lr_ncc)>(ctx->lrs.p);
                 a.lr_geo = a.geom ? devptr<decltype(a.lr_geo)>((float *)ctx->lrs.p + plane) : nullptr;
