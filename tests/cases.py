@@ -100,6 +100,7 @@ CASES = {
     "first_n6_sa0": (112, 84, 6, "first_sa0"),          # SA quadrant windows in init + Strong sweep
     "refine_iter_geom_sa0": (128, 96, 4, "geom_sa0"),   # ... and in DepthToWeak / LocalRefine
     "refine_iter_apd_geom_sa0": (96, 72, 4, "apd_geom_sa0"),
+    "refine_iter_apd_geom_rt4": (112, 84, 4, "apd_geom_rt4"),  # rotate_time 4 (rounds >= 2): 32 anchor slots
 }
 
 
@@ -124,6 +125,8 @@ def make_case(name, oracle_run):
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, sa="zero_band")
     if kind == "apd_geom_sa0":
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, sa="zero_band")
+    if kind == "apd_geom_rt4":
+        return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, rotate_time=4)
     if kind == "apd_geom":
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True)
     raise KeyError(kind)
