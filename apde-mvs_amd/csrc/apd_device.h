@@ -89,6 +89,9 @@ struct Args {
     // terms of DepthToWeak's samples p_disp = -5..5, which are LocalRefine's, [11][N][tile slots]
     APD_G float *lr_ncc;
     APD_G float *lr_geo;
+    // RandomInitialization -> first Weak sweep (null = off): each WEAK pixel's NCC-New of its initial
+    // plane per view, [N][H*W], NaN where it read an anchor's selected views
+    APD_G float *wcur;
 };
 
 // ---------------------------------------------------------------------------------------------

@@ -1440,10 +1440,12 @@ __device__ __forceinline__ void wv_build_windows(const Args &a, WvRefT<F16> &L, 
 
 // ComputeBilateralNCCNew + Softmax focal weighting (APD.cu:448-593, 431-446) for pixel slot p, source
 // view s, plane pl, with the reference side from WvLds. Called by every lane of the wave (converged);
-// `want` = the lane evaluates this task. Same operations, in the same order, as ncc_new.
+// `want` = the lane evaluates this task. Same operations, in the same order, as ncc_new. `seldep`
+// (optional) is set when the result read an anchor's selected views (a window anchor projected out
+// of the source image, APD.cu:510-520), the one input the Strong sweep changes between launches.
 template <bool F16>
 __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L, int p, int px, int py, int s, float4 pl,
-                                            bool want) {
+                                            bool want, bool *seldep = nullptr) {
     const int W = a.W, H = a.H;
     const Hom Hm = homography(a, s, pl);
     float ptx, pty;
@@ -1468,6 +1470,7 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
             if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) {
                 live = false;
                 if (k != 0) {
+                    if (seldep) *seldep = true;
                     if ((a.sel[ax + ay * W] >> (s - 1)) & 1u) {
 #pragma unroll
                         for (int t = 0; t < 9; ++t) if (t == ns) sc[t] = APD_COST_MAX;
@@ -1591,7 +1594,14 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             continue;
         }
         const float4 pl = L.hyp[h * VM_P + p1];
-        const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want);
+        float nv;
+        // iteration 0: the current plane is RandomInitialization's, whose NCC-New it kept (a.wcur)
+        // unless the value read a selected view; the task runs only if a lane lacks it
+        const float kept = (h == 8 && iter == 0 && a.wcur && want) ? a.wcur[(size_t)v * a.HW + c1] : 0.0f;
+        if (h == 8 && iter == 0 && a.wcur && !__ballot(want && __builtin_isnan(kept)))
+            nv = kept;
+        else
+            nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want);
         if (want) {
             val = nv;
             if (h == 8 && geom) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
@@ -2841,7 +2851,11 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, in
     for (int v = wave, k = 0; v < N; v += VM_WAVES, ++k) {
         float cv = 0.0f;
         float nv = 0.0f;
-        if constexpr (APD) nv = ncc_new_vm<F16>(a, *W, p, px, py, v + 1, pl, T.pv && use_new);  // all lanes
+        if constexpr (APD) {
+            bool seldep = false;
+            nv = ncc_new_vm<F16>(a, *W, p, px, py, v + 1, pl, T.pv && use_new, &seldep);  // all lanes
+            if (a.wcur && T.pv && use_new) a.wcur[(size_t)v * a.HW + c] = seldep ? __int_as_float(0x7fc00000) : nv;
+        }
         if (T.pv) {
             if (use_new) {
                 if constexpr (APD) cv = nv;
@@ -3299,7 +3313,7 @@ struct apd_ctx {
     std::string err;
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
-        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, wdone, lrs;
+        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, wdone, lrs, wcur;
     int n_near = 0;
     int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
     Args args{};
@@ -3309,6 +3323,8 @@ struct apd_ctx {
     int tile_w = 8;                // sweep list tile width (tile = tile_w x 256/tile_w positions); APD_TILE_W
     bool cand_pairs = true;        // Weak sweep candidates through k_weak_cand_vm; APD_NO_CAND_PAIRS=1 disables
     bool lr_handover = true;       // LocalRefine reads DepthToWeak's samples; APD_NO_LR_HANDOVER=1 disables
+    bool wcur_on = true;           // RandomInit keeps WEAK current-plane costs for iteration 0; APD_NO_WCUR=1 disables
+    bool wcur_fresh = false;       // they belong to the current planes (set by prepare, cleared by iteration)
     int weak_count = 0;
     int cnt[4] = {0, 0, 0, 0};     // strong black, strong red, weak black, weak red
     size_t list_cap = 0;
@@ -3503,6 +3519,7 @@ apd_ctx *apd_create(int32_t device) {
     ctx->sweep_vm = getenv("APD_SWEEP_LANES") == nullptr;
     ctx->cand_pairs = getenv("APD_NO_CAND_PAIRS") == nullptr;
     ctx->lr_handover = getenv("APD_NO_LR_HANDOVER") == nullptr;
+    ctx->wcur_on = getenv("APD_NO_WCUR") == nullptr;
     // tile_pix needs the tile width to divide the 64-pixel tile (otherwise two workgroups share pixels)
     if (const char *e = getenv("APD_DW_TILE_W")) {
         const int t = atoi(e);
@@ -3538,7 +3555,7 @@ void apd_destroy(apd_ctx *ctx) {
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
                       &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand, &ctx->wdone,
-                      &ctx->lrs};
+                      &ctx->lrs, &ctx->wcur};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
@@ -3721,6 +3738,13 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     a.fit = devptr<decltype(a.fit)>(P.use_APD ? ctx->fit.p : nullptr);
     a.near_offsets = devptr<decltype(a.near_offsets)>(P.use_APD ? ctx->near_off.p : nullptr);
     a.curve = nullptr;
+    a.lr_ncc = nullptr;
+    a.lr_geo = nullptr;
+    a.wcur = nullptr;
+    if (P.use_APD && ctx->sweep_vm && ctx->wcur_on) {  // WEAK pixels' initial NCC-New, [N][H*W]
+        if ((st = ensure(ctx, ctx->wcur, HW * N * sizeof(float)))) return st;
+        a.wcur = devptr<decltype(a.wcur)>(ctx->wcur.p);
+    }
     if ((st = ensure(ctx, ctx->dargs, sizeof(Args)))) return st;
     a.self = devptr<decltype(a.self)>(ctx->dargs.p);
     HIP_OK(ctx, hipMemcpyAsync(ctx->dargs.p, &a, sizeof(Args), hipMemcpyHostToDevice, s));
@@ -3856,6 +3880,7 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
     HIP_OK(ctx, hipMemcpyAsync(ctx->sel.p, ctx->sel2.p, (size_t)a.HW * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     if ((st = check_launch(ctx, "k_random_init"))) return st;
     (void)hipEventRecord(ctx->ev[3], s);
+    ctx->wcur_fresh = a.wcur != nullptr;
     ctx->prepared = true;
     return APD_OK;
 }
@@ -3906,15 +3931,19 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
                            (const int *)list_ptr(ctx, 2 + colour), n, (float *)ctx->wcand.p, (uint8_t *)ctx->wdone.p);
                 cand = (const float *)ctx->wcand.p;
             }
+            // RandomInitialization's kept costs are valid for the first iteration after it only
+            Args aw = a;
+            if (!(ctx->wcur_fresh && iter == 0)) aw.wcur = nullptr;
             if (ctx->sweep_vm)
                 LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N) : wv_lds_bytes<false>(a.N)), s,
-                           a, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, (const uint8_t *)ctx->wdone.p);
+                           aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, (const uint8_t *)ctx->wdone.p);
             else
                 LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
                            (const int *)list_ptr(ctx, 2 + colour), n, iter);
         }
         if ((st = check_launch(ctx, "weak sweep"))) return st;
     }
+    ctx->wcur_fresh = false;
     return APD_OK;
 }
 
