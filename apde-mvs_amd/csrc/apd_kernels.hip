@@ -134,7 +134,7 @@ __global__ __launch_bounds__(BLOCK) void k_build_pairs(const float *__restrict__
 __device__ __forceinline__ bool list_pred(const Args &a, int mode, int colour, int x, int y) {
     const uint8_t w = a.weak[y * a.W + x];
     if (mode == 2) return w == APD_WEAK;
-    if (y >= a.row_limit || ((x + y) & 1) != colour) return false;
+    if (y >= a.row_limit || (colour < 2 && ((x + y) & 1) != colour)) return false;  // colour 2: both
     return mode == 0 ? (w != APD_WEAK) : (w == APD_WEAK);
 }
 __global__ __launch_bounds__(BLOCK) void k_list_count(Args a, int mode, int colour, int *__restrict__ row_counts) {
@@ -1536,7 +1536,7 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
 template <bool F16>
 __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
                                                                 int iter, const float *__restrict__ cand,
-                                                                const uint8_t *__restrict__ cand_done) {
+                                                                const uint8_t *__restrict__ cand_done, int wc) {
     const int N = a.N, W = a.W;
     WvLdsT<F16> &L = *reinterpret_cast<WvLdsT<F16> *>(apd_dyn_lds);
     float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64], later [5][N][64]
@@ -1583,13 +1583,14 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
 
     // ---- P1: (hypothesis, view) tasks; where k_weak_cand_vm handled this group (`cand_done`), the
     // anchor candidates' costs are read, and only the current plane is evaluated here
-    const bool cand_ok = cand && cand_done[blk];
+    const int wi1 = cand ? a.amap[c1] : 0;
+    const bool cand_ok = cand && pv1 && cand_done[wi1];  // per pixel (groups of k_weak_cand_vm span both colours)
     for (int u = wave; u < 9 * N; u += WV_WAVES) {  // view-major: the waves share a source image
         const int v = u / 9, h = u - 9 * v, t = h * N + v;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
         const bool want = pv1 && (h == 8 || ((L.flags[p1] >> h) & 1u));
-        if (cand_ok && h < 8) {
-            if (want) val = cand[((size_t)v * 8 + h) * (size_t)count + first + p1];
+        if (cand && h < 8 && !__ballot(want && !cand_ok)) {  // every lane that needs it has its cost
+            if (want) val = cand[((size_t)v * 8 + h) * (size_t)wc + wi1];
             costL[t * VM_P + p1] = val;
             continue;
         }
@@ -1909,7 +1910,7 @@ __device__ __forceinline__ int pk_compact(const bool (&used)[PER], int (&ids)[PE
 
 template <bool F16>
 __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a, const int *__restrict__ list, int count,
-                                                           float *__restrict__ out, uint8_t *__restrict__ done) {
+                                                           float *__restrict__ out, uint8_t *__restrict__ done, int wc) {
     const int N = a.N, W = a.W, H = a.H;
     PkLds<F16> &L = *reinterpret_cast<PkLds<F16> *>(apd_dyn_lds);
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
@@ -1939,8 +1940,9 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
         L.plc[p1] = (uint8_t)max(slot, 0);
     }
     __syncthreads();
+    const int wi1 = a.amap[c1];  // the pixel's WEAK index: outputs are [view][candidate][WEAK index]
     if (L.ovf) {  // uniform: the Weak sweep evaluates this group's candidates itself
-        if (tid == 0) done[blk] = 0;
+        if (pv1 && wave == 0) done[wi1] = 0;
         return;
     }
     const uint32_t lc1 = L.plc[p1];
@@ -2185,7 +2187,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
     __syncthreads();
     const int nP = L.nP;
 
-    if (tid == 0) done[blk] = 1;
+    if (pv1 && wave == 0) done[wi1] = 1;
     // ---- D: per view
     for (int v = 0; v < N; ++v) {
         const int s = v + 1;
@@ -2299,7 +2301,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
                         cost = (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
                     }
                 }
-                out[((size_t)v * 8 + h) * (size_t)count + first + p1] = cost;
+                out[((size_t)v * 8 + h) * (size_t)wc + wi1] = cost;
             }
         }
         __syncthreads();
@@ -3313,7 +3315,8 @@ struct apd_ctx {
     std::string err;
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
-        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, wdone, lrs, wcur;
+        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, wdone, lrs, wcur,
+        wlist;
     int n_near = 0;
     int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
     Args args{};
@@ -3555,7 +3558,7 @@ void apd_destroy(apd_ctx *ctx) {
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
                       &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand, &ctx->wdone,
-                      &ctx->lrs, &ctx->wcur};
+                      &ctx->lrs, &ctx->wcur, &ctx->wlist};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
@@ -3844,13 +3847,18 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         HIP_OK(ctx, hipMemcpyAsync(host_tot, tot, 4 * sizeof(int), hipMemcpyDeviceToHost, s));
         HIP_OK(ctx, hipStreamSynchronize(s));
         for (int i = 0; i < 4; ++i) ctx->cnt[i] = host_tot[i];
-        if (a.use_apd && ctx->sweep_vm && ctx->cand_pairs) {
-            const size_t nmax = (size_t)std::max(ctx->cnt[2], ctx->cnt[3]);
-            if ((st = ensure(ctx, ctx->wcand, (size_t)a.N * 8 * nmax * sizeof(float)))) return st;
-            if ((st = ensure(ctx, ctx->wdone, blocks_for(nmax, VM_P)))) return st;
-        }
         for (int i = 0; i < 4; ++i) {
             if ((st = build_tile_list(ctx, modes[i][0], modes[i][1], list_ptr(ctx, i), tot + i))) return st;
+        }
+        if (a.use_apd && ctx->sweep_vm && ctx->cand_pairs && ctx->cnt[2] + ctx->cnt[3] > 0) {
+            // k_weak_cand_vm runs once per iteration over the WEAK pixels of both colours (tile
+            // order): between the two Weak launches no anchor plane or selection changes, and the
+            // denser groups share more anchor windows. Costs are kept by WEAK index.
+            const size_t wc = (size_t)std::max(ctx->weak_count, 1);
+            if ((st = ensure(ctx, ctx->wcand, (size_t)a.N * 8 * wc * sizeof(float)))) return st;
+            if ((st = ensure(ctx, ctx->wdone, wc))) return st;
+            if ((st = ensure(ctx, ctx->wlist, (size_t)(ctx->cnt[2] + ctx->cnt[3]) * sizeof(int)))) return st;
+            if ((st = build_tile_list(ctx, 1, 2, (int *)ctx->wlist.p, tot + 5))) return st;
         }
     }
     (void)hipEventRecord(ctx->ev[2], s);
@@ -3917,26 +3925,29 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
     }
     if (a.use_apd) {
         hipLaunchKernelGGL(k_ransac_fit, dim3(blocks_for((size_t)a.HW, BLOCK)), dim3(BLOCK), 0, s, a, iter);
+        const int nw = ctx->cnt[2] + ctx->cnt[3];
+        const int wc = std::max(ctx->weak_count, 1);
+        const float *cand = nullptr;
+        if (ctx->sweep_vm && ctx->cand_pairs && nw > 0) {
+            if (ctx->wcand.bytes < (size_t)a.N * 8 * (size_t)wc * sizeof(float) || ctx->wdone.bytes < (size_t)wc ||
+                ctx->wlist.bytes < (size_t)nw * sizeof(int)) {
+                ctx->err = "candidate cost buffers not sized by apd_stage_prepare";
+                return APD_ESTATE;
+            }
+            LAUNCH_TEX(k_weak_cand_vm, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK),
+                       (ctx->args.tex_f16 ? pk_lds_bytes<true>() : pk_lds_bytes<false>()), s, a,
+                       (const int *)ctx->wlist.p, nw, (float *)ctx->wcand.p, (uint8_t *)ctx->wdone.p, wc);
+            cand = (const float *)ctx->wcand.p;
+        }
         for (int colour = 0; colour < 2; ++colour) {
             const int n = ctx->cnt[2 + colour];
             if (n <= 0) continue;
-            const float *cand = nullptr;
-            if (ctx->sweep_vm && ctx->cand_pairs) {
-                if (ctx->wcand.bytes < (size_t)a.N * 8 * (size_t)n * sizeof(float) || ctx->wdone.bytes < blocks_for((size_t)n, VM_P)) {
-                    ctx->err = "candidate cost buffer not sized by apd_stage_prepare";
-                    return APD_ESTATE;
-                }
-                LAUNCH_TEX(k_weak_cand_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(PK_BLOCK),
-                           (ctx->args.tex_f16 ? pk_lds_bytes<true>() : pk_lds_bytes<false>()), s, a,
-                           (const int *)list_ptr(ctx, 2 + colour), n, (float *)ctx->wcand.p, (uint8_t *)ctx->wdone.p);
-                cand = (const float *)ctx->wcand.p;
-            }
             // RandomInitialization's kept costs are valid for the first iteration after it only
             Args aw = a;
             if (!(ctx->wcur_fresh && iter == 0)) aw.wcur = nullptr;
             if (ctx->sweep_vm)
                 LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N) : wv_lds_bytes<false>(a.N)), s,
-                           aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, (const uint8_t *)ctx->wdone.p);
+                           aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, (const uint8_t *)ctx->wdone.p, wc);
             else
                 LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
                            (const int *)list_ptr(ctx, 2 + colour), n, iter);
