@@ -1070,10 +1070,14 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
         const bool fh = h == 8 || L.nval[h * VM_P + p1];
         if (pv1 && fh) {
             const float4 pl = L.hyp[h * VM_P + p1];
-            bool slow;
-            ++issued;
-            val = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, pl, rw, slow);
-            if (slow) defer[k >> 6] |= 1ull << (k & 63);
+            if (h == 8 && a.wcur) {  // iteration 0: RandomInitialization's NCC-Old of this plane
+                val = a.wcur[(size_t)v * a.HW + c1];
+            } else {
+                bool slow;
+                ++issued;
+                val = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, pl, rw, slow);
+                if (slow) defer[k >> 6] |= 1ull << (k & 63);
+            }
             if (h == 8 && geom_imp) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
         }
         costL[t * VM_P + p1] = val;
@@ -2912,6 +2916,8 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, in
         }
         a.plane[c] = pl;
         a.cost[c] = cost_out;
+        if (a.wcur && !use_new)  // the Strong sweep's first launches re-evaluate exactly these
+            for (int k = 0; k < N; ++k) a.wcur[(size_t)k * a.HW + c] = cvL[k * VM_P + p];
         a.sel_next[c] = sv;  // launch-start snapshot semantics (oracle k_random_init)
     }
 }
@@ -3744,7 +3750,7 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     a.lr_ncc = nullptr;
     a.lr_geo = nullptr;
     a.wcur = nullptr;
-    if (P.use_APD && ctx->sweep_vm && ctx->wcur_on) {  // WEAK pixels' initial NCC-New, [N][H*W]
+    if (ctx->sweep_vm && ctx->wcur_on) {  // the initial planes' costs per view (NCC-New for WEAK pixels), [N][H*W]
         if ((st = ensure(ctx, ctx->wcur, HW * N * sizeof(float)))) return st;
         a.wcur = devptr<decltype(a.wcur)>(ctx->wcur.p);
     }
@@ -3910,6 +3916,7 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
         }
         Args ak = a;
         if (ctx->prof && ctx->evals.p) ak.evals = (APD_G unsigned long long *)ctx->evals.p;
+        if (!(ctx->wcur_fresh && iter == 0)) ak.wcur = nullptr;  // RandomInitialization's costs: iteration 0 only
         if (ctx->sweep_vm)
             LAUNCH_TEX_SA(k_sweep_strong_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), vm_lds_bytes(a.N) + sa_lds_bytes(a), s,
                        ak, (const int *)list_ptr(ctx, colour), n, iter);
