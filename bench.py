@@ -54,14 +54,19 @@ def strong_evaluations(W: int, H: int, n_src: int, colour: int, row_limit: int) 
     return int((per_px * mask).sum()) * n_src
 
 
-def latest_pmc():
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))
-    if not files:
-        return None
-    try:
-        return json.load(open(files[-1]))
-    except Exception:
-        return None
+def latest_pmc(kernel: str, W: int, n_src: int):
+    """The newest (by round/session file name) PMC summary under profiles/ for this kernel and shape.
+    Other PMC files (counter studies of other shapes or blocks) are skipped, not taken as the latest."""
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            pmc = json.load(open(f))
+        except Exception:
+            continue
+        if (isinstance(pmc, dict) and str(pmc.get("kernel", "")).startswith(kernel)
+                and pmc.get("width") == W and pmc.get("n_src") == n_src
+                and pmc.get("hbm_bytes_per_launch") is not None):
+            return pmc
+    return None
 
 
 def cpu_baseline(scene_args, n_src, threads):
@@ -205,10 +210,8 @@ def main():
     launch_ms = sweep_ms / max(launches, 1)
     achieved_tf = flop_per_launch / (launch_ms * 1e-3) / 1e12
     bytes_per_launch = (W * H / 2) * (4 * (N + 1) + 80)  # = 116 B/px at N=8
-    pmc = latest_pmc()
-    traffic = None
-    if pmc and pmc.get("kernel", "").startswith("k_sweep_strong") and pmc.get("width") == W and pmc.get("n_src") == N:
-        traffic = pmc.get("hbm_bytes_per_launch")
+    pmc = latest_pmc("k_sweep_strong", W, N)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
 
     line = None
     if rank == 0:
