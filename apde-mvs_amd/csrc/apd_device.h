@@ -21,10 +21,15 @@
 
 // Device pointers live in the global address space: without the qualifier every load through a
 // struct member is a FLAT load (no scalar path, waits on both vmcnt and lgkmcnt).
+// Per-problem tables no kernel writes (cameras, per-view homography terms) live in the constant
+// address space: loads through them are invariant, so uniform ones become scalar loads even in
+// kernels that store to global memory (the noclobber analysis cannot prove that for APD_G).
 #if defined(__HIP_DEVICE_COMPILE__)
 #define APD_G __attribute__((address_space(1)))
+#define APD_C __attribute__((address_space(4)))
 #else
 #define APD_G
+#define APD_C
 #endif
 
 namespace apd {
@@ -66,8 +71,8 @@ struct Args {
     int tex_f16;
     int force_slow;                        // test hook: route every NCC-Old window through ncc_old_slow
     const APD_G float *depth;              // [N+1][H*W] depth maps (geom / APD)
-    const APD_G SrcView *views;            // [N+1]
-    const APD_G Cam *cams;                 // [N+1]
+    const APD_C SrcView *views;            // [N+1]
+    const APD_C Cam *cams;                 // [N+1]
     APD_G float4 *plane;
     APD_G float *cost;
     APD_G uint32_t *sel;
@@ -200,27 +205,27 @@ __device__ __forceinline__ void normalize2(float &x, float &y) {
     float inv = 1.0f / sqrtf(ns);
     x *= inv; y *= inv;
 }
-__device__ __forceinline__ void get3d(const APD_G Cam &c, float px, float py, float depth, float X[3]) {
+__device__ __forceinline__ void get3d(const APD_C Cam &c, float px, float py, float depth, float X[3]) {
     X[0] = depth * (px - c.K[2]) / c.K[0];
     X[1] = depth * (py - c.K[5]) / c.K[4];
     X[2] = depth;
 }
-__device__ __forceinline__ float4 view_dir(const APD_G Cam &c, int px, int py, float depth) {
+__device__ __forceinline__ float4 view_dir(const APD_C Cam &c, int px, int py, float depth) {
     float X[3];
     get3d(c, (float)px, (float)py, depth, X);
     float norm = sqrtf(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
     return make_float4(X[0] / norm, X[1] / norm, X[2] / norm, 0.0f);
 }
-__device__ __forceinline__ float dist2origin(const APD_G Cam &c, int px, int py, float depth, float4 n) {
+__device__ __forceinline__ float dist2origin(const APD_C Cam &c, int px, int py, float depth, float4 n) {
     float X[3];
     get3d(c, (float)px, (float)py, depth, X);
     return -(n.x * X[0] + n.y * X[1] + n.z * X[2]);
 }
-__device__ __forceinline__ float depth_from_plane(const APD_G Cam &c, float4 pl, int px, int py) {
+__device__ __forceinline__ float depth_from_plane(const APD_C Cam &c, float4 pl, int px, int py) {
     return -pl.w * c.K[0] /
            (((float)px - c.K[2]) * pl.x + (c.K[0] / c.K[4]) * ((float)py - c.K[5]) * pl.y + c.K[0] * pl.z);
 }
-__device__ __forceinline__ float4 random_normal(const APD_G Cam &c, int px, int py, Rng &g, float depth) {
+__device__ __forceinline__ float4 random_normal(const APD_C Cam &c, int px, int py, Rng &g, float depth) {
     float q1 = 1.0f, q2 = 1.0f, s = 2.0f;
     while (s >= 1.0f) {
         q1 = 2.0f * g.uniform() - 1.0f;
@@ -235,7 +240,7 @@ __device__ __forceinline__ float4 random_normal(const APD_G Cam &c, int px, int 
     normalize3(n);
     return n;
 }
-__device__ __forceinline__ float4 perturbed_normal(const APD_G Cam &c, int px, int py, float4 n, Rng &g, float pert) {
+__device__ __forceinline__ float4 perturbed_normal(const APD_C Cam &c, int px, int py, float4 n, Rng &g, float pert) {
     float4 vd = view_dir(c, px, py, 1.0f);
     float a1 = (g.uniform() - 0.5f) * pert;
     float a2 = (g.uniform() - 0.5f) * pert;
@@ -257,15 +262,15 @@ __device__ __forceinline__ float4 perturbed_normal(const APD_G Cam &c, int px, i
     normalize3(p);
     return p;
 }
-__device__ __forceinline__ float4 to_world(const APD_G Cam &c, float4 p) {
+__device__ __forceinline__ float4 to_world(const APD_C Cam &c, float4 p) {
     return make_float4(c.R[0] * p.x + c.R[3] * p.y + c.R[6] * p.z, c.R[1] * p.x + c.R[4] * p.y + c.R[7] * p.z,
                        c.R[2] * p.x + c.R[5] * p.y + c.R[8] * p.z, p.w);
 }
-__device__ __forceinline__ float4 to_ref(const APD_G Cam &c, float4 p) {
+__device__ __forceinline__ float4 to_ref(const APD_C Cam &c, float4 p) {
     return make_float4(c.R[0] * p.x + c.R[1] * p.y + c.R[2] * p.z, c.R[3] * p.x + c.R[4] * p.y + c.R[5] * p.z,
                        c.R[6] * p.x + c.R[7] * p.y + c.R[8] * p.z, p.w);
 }
-__device__ __forceinline__ void world_point(const APD_G Cam &c, float x, float y, float depth, float P[3]) {
+__device__ __forceinline__ void world_point(const APD_C Cam &c, float x, float y, float depth, float P[3]) {
     float X0 = depth * (x - c.K[2]) / c.K[0];
     float X1 = depth * (y - c.K[5]) / c.K[4];
     float X2 = depth;
@@ -274,7 +279,7 @@ __device__ __forceinline__ void world_point(const APD_G Cam &c, float x, float y
     float t2 = c.R[2] * X0 + c.R[5] * X1 + c.R[8] * X2;
     P[0] = t0 + c.c[0]; P[1] = t1 + c.c[1]; P[2] = t2 + c.c[2];
 }
-__device__ __forceinline__ void project_cam(const float P[3], const APD_G Cam &c, float &px, float &py, float &d) {
+__device__ __forceinline__ void project_cam(const float P[3], const APD_C Cam &c, float &px, float &py, float &d) {
     float t0 = c.R[0] * P[0] + c.R[1] * P[1] + c.R[2] * P[2] + c.t[0];
     float t1 = c.R[3] * P[0] + c.R[4] * P[1] + c.R[5] * P[2] + c.t[1];
     float t2 = c.R[6] * P[0] + c.R[7] * P[1] + c.R[8] * P[2] + c.t[2];
@@ -302,7 +307,7 @@ __device__ __forceinline__ Hom homography(const AT &a, int s, float4 pl) {
     float m2 = fmaf(-pl.y, a.cyk, fmaf(-pl.x, a.cxk, pl.z));
     float iw = 1.0f / pl.w;
     m0 *= iw; m1 *= iw; m2 *= iw;
-    const APD_G SrcView &V = a.views[s];
+    const APD_C SrcView &V = a.views[s];
     Hom H;
     H.h[0] = fmaf(-V.b[0], m0, V.A[0]); H.h[1] = fmaf(-V.b[0], m1, V.A[1]); H.h[2] = fmaf(-V.b[0], m2, V.A[2]);
     H.h[3] = fmaf(-V.b[1], m0, V.A[3]); H.h[4] = fmaf(-V.b[1], m1, V.A[4]); H.h[5] = fmaf(-V.b[1], m2, V.A[5]);
@@ -990,8 +995,8 @@ __device__ __noinline__ float ncc_new(const APD_G Args *ap, int px, int py, int 
 
 // ComputeGeomConsistencyCost (APD.cu:865-902)
 __device__ __forceinline__ float geom_cost(const Args &a, int px, int py, int s, float4 pl) {
-    const APD_G Cam &rc = a.cams[0];
-    const APD_G Cam &sc = a.cams[s];
+    const APD_C Cam &rc = a.cams[0];
+    const APD_C Cam &sc = a.cams[s];
     float depth = depth_from_plane(rc, pl, px, py);
     float P[3];
     world_point(rc, (float)px, (float)py, depth, P);

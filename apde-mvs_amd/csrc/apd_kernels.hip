@@ -383,7 +383,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
     const int py = c / W, px = c - py * W;
     const int margin = 6;
     const float depth_diff = a.dmax - a.dmin;
-    const APD_G Cam &cam = a.cams[0];
+    const APD_C Cam &cam = a.cams[0];
     APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
     Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_ANCHORS);
     for (int i = 0; i < 9; ++i) anc[i] = make_short2(-1, -1);
@@ -526,7 +526,7 @@ __global__ __launch_bounds__(BLOCK) void k_ransac_fit(Args a, int iter) {
     if (a.weak[c] != APD_WEAK) { a.fit[c] = a.plane[c]; return; }
     const int W = a.W;
     const int py = c / W, px = c - py * W;
-    const APD_G Cam &cam = a.cams[0];
+    const APD_C Cam &cam = a.cams[0];
     const APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
     int sx[8], sy[8], cnt = 0;
     float s3[8][3], X[3];
@@ -588,7 +588,7 @@ __global__ __launch_bounds__(BLOCK) void k_random_init(Args a) {
     const Group G = make_group(N, a.HW, wave);
     const int c = G.li;
     const int py = c / a.W, px = c - py * a.W;
-    const APD_G Cam &cam = a.cams[0];
+    const APD_C Cam &cam = a.cams[0];
     float4 pl;
     if (a.state == APD_FIRST_INIT) {
         Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_INIT);
@@ -695,7 +695,7 @@ struct Cands {
     float drand, dpert;
 };
 __device__ __forceinline__ Cands refine_candidates(const Args &a, int px, int py, Rng &g, float4 cur, float depth) {
-    const APD_G Cam &cam = a.cams[0];
+    const APD_C Cam &cam = a.cams[0];
     Cands C;
     C.drand = g.uniform() * (a.dmax - a.dmin) + a.dmin;
     C.nrand = random_normal(cam, px, py, g, depth);
@@ -729,7 +729,7 @@ __global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a,
     const int c = list[G.li];
     const int py = c / W, px = c - py * W;
     const int s = G.v + 1;
-    const APD_G Cam &cam0 = a.cams[0];
+    const APD_C Cam &cam0 = a.cams[0];
     const APD_G float *__restrict__ cost = a.cost;
 
     // adaptive checkerboard neighbour selection (APD.cu:1127-1316); identical in every lane
@@ -1026,7 +1026,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     const int np = min(VM_P, count - first);
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
-    const APD_G Cam &cam0 = a.cams[0];
+    const APD_C Cam &cam0 = a.cams[0];
     const bool geom_imp = a.geom && a.impetus;
     const float gf = a.gf;
 
@@ -1550,7 +1550,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     const int np = min(VM_P, count - first);
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
-    const APD_G Cam &cam0 = a.cams[0];
+    const APD_C Cam &cam0 = a.cams[0];
     const bool geom = a.geom != 0;
     const float gf = a.gf;
     const int p1 = lane;
@@ -2324,7 +2324,7 @@ __global__ __launch_bounds__(BLOCK) void k_sweep_weak(Args a, const int *__restr
     const int c = list[G.li];
     const int py = c / W, px = c - py * W;
     const int s = G.v + 1;
-    const APD_G Cam &cam0 = a.cams[0];
+    const APD_C Cam &cam0 = a.cams[0];
     const APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
     const bool geom = a.geom != 0;
     const float gf = a.gf;
@@ -2573,7 +2573,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
     SaWin *saw = reinterpret_cast<SaWin *>(vslot + N * VM_P);         // [64] when a.sa_any
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
-    const APD_G Cam &cam0 = a.cams[0];
+    const APD_C Cam &cam0 = a.cams[0];
     const int p = lane;
     // the workgroup's pixels: a tw x (64/tw) tile (XCD-aware tile order); pixels outside the image idle
     const int th = VM_P / tw, tiles_x = (W + tw - 1) / tw;
@@ -2604,7 +2604,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
         float base = 0.0f, wn = 0.0f;
         int valid = 0;
         for (int k = 0; k < N; ++k) {
-            const APD_G Cam &sc = a.cams[k + 1];
+            const APD_C Cam &sc = a.cams[k + 1];
             const float d0 = cam0.c[0] - sc.c[0], d1 = cam0.c[1] - sc.c[1], d2 = cam0.c[2] - sc.c[2];
             const float dk = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
             if ((sv >> k) & 1u) { wn += (float)wts[k * VM_P + p]; base += dk; valid++; }
@@ -2642,11 +2642,13 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
         // ---- P1: (depth, view) tasks
         uint64_t defer = 0;
         {
-            int v = 0, vb = 0, nv = L.vcnt[0], tv = (dc * nv + 63) >> 6;
+            // the per-view counts are read through readfirstlane: v stays wave-uniform (SGPR), so the
+            // view's homography constants, cameras and texel base come through scalar loads
+            int v = 0, vb = 0, nv = __builtin_amdgcn_readfirstlane(L.vcnt[0]), tv = (dc * nv + 63) >> 6;
             for (int j = wave, k = 0;; j += VM_WAVES, ++k) {
                 while (v < N && j >= vb + tv) {
                     vb += tv;
-                    if (++v < N) { nv = L.vcnt[v]; tv = (dc * nv + 63) >> 6; }
+                    if (++v < N) { nv = __builtin_amdgcn_readfirstlane(L.vcnt[v]); tv = (dc * nv + 63) >> 6; }
                 }
                 if (v >= N) break;
                 const int t = (j - vb) * 64 + lane;
@@ -2687,8 +2689,8 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
             const int k = __builtin_ctzll(defer);
             defer &= defer - 1;
             const int j = wave + k * VM_WAVES;
-            int v = 0, vb = 0, nv = L.vcnt[0], tv = (dc * nv + 63) >> 6;
-            while (j >= vb + tv) { vb += tv; ++v; nv = L.vcnt[v]; tv = (dc * nv + 63) >> 6; }
+            int v = 0, vb = 0, nv = __builtin_amdgcn_readfirstlane(L.vcnt[0]), tv = (dc * nv + 63) >> 6;
+            while (j >= vb + tv) { vb += tv; ++v; nv = __builtin_amdgcn_readfirstlane(L.vcnt[v]); tv = (dc * nv + 63) >> 6; }
             const int t = (j - vb) * 64 + lane;
             if (t < dc * nv) {
                 const int r = t / dc, dd = t - r * dc;
@@ -2809,7 +2811,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, in
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (WAVE - 1);
     const TilePix T = tile_pix(a, tw, lane);
     const int p = lane, px = T.px, py = T.py, c = T.c;
-    const APD_G Cam &cam = a.cams[0];
+    const APD_C Cam &cam = a.cams[0];
     if (T.pv) {
         if (wave == 0) {
             float4 pl;
@@ -2950,7 +2952,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, i
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (WAVE - 1);
     const TilePix T = tile_pix(a, tw, lane);
     const int p = lane, px = T.px, py = T.py, c = T.c;
-    const APD_G Cam &cam0 = a.cams[0];
+    const APD_C Cam &cam0 = a.cams[0];
     const bool geom = a.geom != 0;
     const float gf = a.gf;
     if (T.pv) {
@@ -3003,7 +3005,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, i
         float cost_now = 0.0f, base = 0.0f, wn = 0.0f;
         int valid = 0;
         for (int k = 0; k < N; ++k) {
-            const APD_G Cam &sc = a.cams[k + 1];
+            const APD_C Cam &sc = a.cams[k + 1];
             const float d0 = cam0.c[0] - sc.c[0], d1 = cam0.c[1] - sc.c[1], d2 = cam0.c[2] - sc.c[2];
             const float dk = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
             if ((sv >> k) & 1u) {
@@ -3097,7 +3099,7 @@ __global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
     const int c = G.li;
     const int py = c / W, px = c - py * W;
     const int s = G.v + 1;
-    const APD_G Cam &cam0 = a.cams[0];
+    const APD_C Cam &cam0 = a.cams[0];
     float *pc = lds_slot(G, P, 61, 0);
     const bool border = px < 6 || py < 6 || px >= W - 6 || py >= H - 6;
     const float4 pl = to_ref(cam0, a.plane[c]);
@@ -3107,7 +3109,7 @@ __global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
     const int wv = a.vw[(size_t)G.v * a.HW + c];
     float mydist;
     {
-        const APD_G Cam &sc = a.cams[s];
+        const APD_C Cam &sc = a.cams[s];
         float d0 = cam0.c[0] - sc.c[0], d1 = cam0.c[1] - sc.c[1], d2 = cam0.c[2] - sc.c[2];
         mydist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
     }
@@ -3190,7 +3192,7 @@ __global__ __launch_bounds__(BLOCK) void k_confidence(Args a) {
     const int W = a.W;
     const int py = c / W, px = c - py * W;
     a.conf[c] = 0;
-    const APD_G Cam &rc = a.cams[0];
+    const APD_C Cam &rc = a.cams[0];
     const uint32_t sv = a.sel[c];
     const float rd = a.plane[c].w;
     if (rd <= 0.0f) { a.weak[c] = APD_UNKNOWN; return; }
@@ -3200,7 +3202,7 @@ __global__ __launch_bounds__(BLOCK) void k_confidence(Args a) {
     for (int i = 0; i < a.N; ++i) {
         if (!((sv >> i) & 1u)) continue;
         const int s = i + 1;
-        const APD_G Cam &sc = a.cams[s];
+        const APD_C Cam &sc = a.cams[s];
         float sx, sy, sd;
         project_cam(P, sc, sx, sy, sd);
         const float src_depth = a.depth[(size_t)s * a.HW + trunc_clamp(sy, a.H) * W + trunc_clamp(sx, W)];
@@ -3228,7 +3230,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_refine(Args a) {
     const int c = G.li;
     const int py = c / W, px = c - py * W;
     const int s = G.v + 1;
-    const APD_G Cam &cam0 = a.cams[0];
+    const APD_C Cam &cam0 = a.cams[0];
     const float4 pl = to_ref(cam0, a.plane[c]);
     const float od = pl.w;
     const uint32_t sv = a.sel[c];
@@ -3240,7 +3242,7 @@ __global__ __launch_bounds__(BLOCK) void k_local_refine(Args a) {
     build_refwin(a, px, py, lds_slot(G, WAVE / N, 36, 0), G.v, N, rw);
     float mydist, tc0 = 0.0f;
     {
-        const APD_G Cam &sc = a.cams[s];
+        const APD_C Cam &sc = a.cams[s];
         float d0 = cam0.c[0] - sc.c[0], d1 = cam0.c[1] - sc.c[1], d2 = cam0.c[2] - sc.c[2];
         mydist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
     }
