@@ -300,19 +300,29 @@ __device__ __forceinline__ int trunc_clamp(float x, int n) {
 // ---------------------------------------------------------------------------------------------
 struct Hom { float h[9]; };
 
+// The view-independent part of the homography, n^T Kr^-1 / w (a kernel that evaluates one plane
+// in several views may compute it once), and the per-view part H = A - b m.
 template <class AT>
-__device__ __forceinline__ Hom homography(const AT &a, int s, float4 pl) {
+__device__ __forceinline__ float3 plane_terms(const AT &a, float4 pl) {
     float m0 = pl.x * a.ikx;
     float m1 = pl.y * a.iky;
     float m2 = fmaf(-pl.y, a.cyk, fmaf(-pl.x, a.cxk, pl.z));
     float iw = 1.0f / pl.w;
     m0 *= iw; m1 *= iw; m2 *= iw;
+    return make_float3(m0, m1, m2);
+}
+template <class AT>
+__device__ __forceinline__ Hom homography_terms(const AT &a, int s, float3 m) {
     const APD_C SrcView &V = a.views[s];
     Hom H;
-    H.h[0] = fmaf(-V.b[0], m0, V.A[0]); H.h[1] = fmaf(-V.b[0], m1, V.A[1]); H.h[2] = fmaf(-V.b[0], m2, V.A[2]);
-    H.h[3] = fmaf(-V.b[1], m0, V.A[3]); H.h[4] = fmaf(-V.b[1], m1, V.A[4]); H.h[5] = fmaf(-V.b[1], m2, V.A[5]);
-    H.h[6] = fmaf(-V.b[2], m0, V.A[6]); H.h[7] = fmaf(-V.b[2], m1, V.A[7]); H.h[8] = fmaf(-V.b[2], m2, V.A[8]);
+    H.h[0] = fmaf(-V.b[0], m.x, V.A[0]); H.h[1] = fmaf(-V.b[0], m.y, V.A[1]); H.h[2] = fmaf(-V.b[0], m.z, V.A[2]);
+    H.h[3] = fmaf(-V.b[1], m.x, V.A[3]); H.h[4] = fmaf(-V.b[1], m.y, V.A[4]); H.h[5] = fmaf(-V.b[1], m.z, V.A[5]);
+    H.h[6] = fmaf(-V.b[2], m.x, V.A[6]); H.h[7] = fmaf(-V.b[2], m.y, V.A[7]); H.h[8] = fmaf(-V.b[2], m.z, V.A[8]);
     return H;
+}
+template <class AT>
+__device__ __forceinline__ Hom homography(const AT &a, int s, float4 pl) {
+    return homography_terms(a, s, plane_terms(a, pl));
 }
 __device__ __forceinline__ void project(const Hom &H, float x, float y, float &ox, float &oy) {
     float X = fmaf(H.h[1], y, fmaf(H.h[0], x, H.h[2]));
@@ -842,11 +852,11 @@ __device__ __noinline__ float ncc_old_slow(const APD_G Args *ap, int px, int py,
 // hit at the projected centre, or a Z the Newton reciprocal is not proven for); the returned value
 // is then meaningless (the taps ran on a dummy homography that keeps every address in bounds).
 // RS = LDS stride of the reference window (1: per-pixel contiguous; 64: [k][pixel] layout).
+// (ncc_old_fast_h: the same with the window's homography given, e.g. from precomputed plane_terms)
 template <bool F16, int RS = 1>
-__device__ __forceinline__ float ncc_old_fast(const Args &a, int px, int py, int s, float4 pl, const RefWin &rw,
-                                              bool &slow) {
+__device__ __forceinline__ float ncc_old_fast_h(const Args &a, int px, int py, int s, Hom Hm, const RefWin &rw,
+                                                bool &slow) {
     const int W = a.W, H = a.H;
-    Hom Hm = homography(a, s, pl);
     float ptx, pty;
     project(Hm, (float)px, (float)py, ptx, pty);
     slow = false;
@@ -884,6 +894,11 @@ __device__ __forceinline__ float ncc_old_fast(const Args &a, int px, int py, int
     }
     ncc_old_taps<FastTex<F16, (RS > 1)>, RS>(T, Hm, px, py, rw, ss, sss, srs);
     return ncc_old_finish(ss, sss, srs, rw.mean, rw.var);
+}
+template <bool F16, int RS = 1>
+__device__ __forceinline__ float ncc_old_fast(const Args &a, int px, int py, int s, float4 pl, const RefWin &rw,
+                                              bool &slow) {
+    return ncc_old_fast_h<F16, RS>(a, px, py, s, homography(a, s, pl), rw, slow);
 }
 
 template <bool F16, int RS = 1>

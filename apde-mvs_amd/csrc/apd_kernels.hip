@@ -2544,8 +2544,8 @@ __global__ __launch_bounds__(BLOCK) void k_filter(Args a, const int *__restrict_
 // and the peak analysis. Waves skip every task none of their pixels selected (selected_views is
 // spatially coherent), which the lanes = views layout could not.
 // ---------------------------------------------------------------------------------------------
-#ifndef DW_CHUNK_BYTES
-#define DW_CHUNK_BYTES 16384  // 8 disparities per chunk at N = 8: 44 KiB per workgroup, 3 per CU (16: 2 per CU, 7 % slower)
+#ifndef DW_LDS_BUDGET
+#define DW_LDS_BUDGET 53248  // bytes per workgroup: 3 per CU (8 disparities per chunk at N = 8; 2 per CU with 16 was 7 % slower)
 #endif
 struct DwLds {
     float refw[36 * VM_P];
@@ -2554,14 +2554,21 @@ struct DwLds {
     float base[VM_P], disp[VM_P], wn[VM_P];
     float rmean[VM_P], rvar[VM_P];  // reference-window moments (RefWin)
     uint32_t sel[VM_P];
-    int active[VM_P];
+    uint8_t active[VM_P];
     int pxy[VM_P];              // px | py << 16
     int vcnt[32];               // active pixels that selected view v
 };
-static inline int dw_chunk(int N) { return std::max(1, std::min(61, DW_CHUNK_BYTES / (N * VM_P * (int)sizeof(float)))); }
-// + cost table [chunk][N][64] fp32, view weights [N][64] u8, per-view pixel slots [N][64] u8
-static inline size_t dw_lds_bytes(int N) {
-    return sizeof(DwLds) + (size_t)dw_chunk(N) * N * VM_P * sizeof(float) + (size_t)2 * N * VM_P;
+// + cost table [chunk][N][64] fp32, view weights [N][64] u8, per-view pixel slots [N][64] u8, the
+// per-(disparity, pixel) plane terms of the chunk [3][chunk][64] fp32 (+ [chunk][64] plane w with
+// geometric consistency) and evaluation flags [chunk][64] u8; the chunk is the largest that keeps
+// the workgroup within DW_LDS_BUDGET
+static inline size_t dw_per_disp(int N, bool geom) { return (size_t)N * VM_P * sizeof(float) + (size_t)VM_P * (13 + (geom ? 4 : 0)); }
+static inline int dw_chunk(int N, bool geom, size_t extra) {
+    const long fixed = (long)(sizeof(DwLds) + (size_t)2 * N * VM_P + extra);
+    return std::max(1, std::min(61, (int)((DW_LDS_BUDGET - fixed) / (long)dw_per_disp(N, geom))));
+}
+static inline size_t dw_lds_bytes(int N, bool geom, int chunk) {
+    return sizeof(DwLds) + (size_t)2 * N * VM_P + (size_t)chunk * dw_per_disp(N, geom);
 }
 template <bool F16, bool SA>
 __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, int chunk, int tw) {
@@ -2570,7 +2577,11 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
     float *tcL = reinterpret_cast<float *>(&L + 1);                 // [chunk][N][64]
     uint8_t *wts = reinterpret_cast<uint8_t *>(tcL + chunk * N * VM_P);  // [N][64]
     uint8_t *vslot = wts + N * VM_P;                                 // [N][64] pixel slots per view
-    SaWin *saw = reinterpret_cast<SaWin *>(vslot + N * VM_P);         // [64] when a.sa_any
+    const bool geom = a.geom != 0;
+    float *ptm = reinterpret_cast<float *>(vslot + N * VM_P);         // [3][chunk][64] plane terms
+    float *ptw = ptm + 3 * chunk * VM_P;                              // [chunk][64] plane w (geom only)
+    uint8_t *pok = reinterpret_cast<uint8_t *>(ptw + (geom ? chunk * VM_P : 0));  // [chunk][64] evaluated
+    SaWin *saw = reinterpret_cast<SaWin *>(pok + chunk * VM_P);       // [64] when a.sa_any
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
     const APD_C Cam &cam0 = a.cams[0];
@@ -2624,7 +2635,6 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
     const float base = L.base[p], disp = L.disp[p], wn = L.wn[p];
     const uint32_t sv = L.sel[p];
     const float4 pl = L.pl[p];
-    const bool geom = a.geom != 0;
     const float gf = a.gf;
     // Compacted (disparity, pixel) pairs: per view, only the active pixels that selected it (the
     // others' costs are never read), packed 64 to a wave-task, disparity-major, dealt round-robin over
@@ -2637,8 +2647,29 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
         if (lane == 0) L.vcnt[v] = __popcll(m);
     }
     __syncthreads();
-    for (int d0 = 0; d0 < 61; d0 += chunk) {
-        const int dc = min(chunk, 61 - d0);
+    // The peak analysis reads the costs of disparities 1..59 only (and disparity 0 when no peak is found
+    // and weak_peak_radius >= 30): disparities 0 and 60 are evaluated only for the curve export.
+    const bool ends = a.curve != nullptr || a.peak_radius >= 30;
+    const int dlo = ends ? 0 : 1, dhi = ends ? 61 : 60;
+    for (int d0 = dlo; d0 < dhi; d0 += chunk) {
+        const int dc = min(chunk, dhi - d0);
+        // ---- P0': the view-independent terms of each (disparity, pixel) plane, once instead of once per
+        // selected view: depth range test, plane w (dist2origin), homography terms n^T Kr^-1 / w
+        for (int e = tid; e < dc * VM_P; e += VM_BLOCK) {
+            const int q = e & (VM_P - 1), dd = e >> 6;
+            const float pdepth = cam0.K[0] * L.base[q] / (L.disp[q] + (float)(d0 + dd - 30));
+            const bool ok = L.active[q] != 0 && !(pdepth < a.dmin || pdepth > a.dmax);
+            pok[e] = ok;
+            if (ok) {
+                const int xy = L.pxy[q];
+                float4 tp = L.pl[q];
+                tp.w = dist2origin(cam0, xy & 0xFFFF, xy >> 16, pdepth, tp);
+                const float3 m = plane_terms(a, tp);
+                ptm[e] = m.x; ptm[chunk * VM_P + e] = m.y; ptm[2 * chunk * VM_P + e] = m.z;
+                if (geom) ptw[e] = tp.w;
+            }
+        }
+        __syncthreads();
         // ---- P1: (depth, view) tasks
         uint64_t defer = 0;
         {
@@ -2663,18 +2694,22 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 }
                 const int xy = L.pxy[q];
                 const int qx = xy & 0xFFFF, qy = xy >> 16;
-                const float pdepth = cam0.K[0] * L.base[q] / (L.disp[q] + (float)(d0 + dd - 30));
-                const bool eval = has && !(pdepth < a.dmin || pdepth > a.dmax);
+                const int e = dd * VM_P + q;
+                const bool eval = has && pok[e];
                 const RefWin rwq{&L.refw[q], L.rmean[q], L.rvar[q], SA ? &saw[q] : nullptr};
-                float4 tp = L.pl[q];
                 float tc = 0.0f;
                 bool slow = false;
                 if (eval) {
-                    tp.w = dist2origin(cam0, qx, qy, pdepth, tp);
-                    tc = ncc_old_fast<F16, VM_P>(a, qx, qy, v + 1, tp, rwq, slow);
+                    const float3 m = make_float3(ptm[e], ptm[chunk * VM_P + e], ptm[2 * chunk * VM_P + e]);
+                    tc = ncc_old_fast_h<F16, VM_P>(a, qx, qy, v + 1, homography_terms(a, v + 1, m), rwq, slow);
                     if (slow) defer |= 1ull << k;
                 }
-                const float g = (eval && geom) ? geom_cost(a, qx, qy, v + 1, tp) : 0.0f;
+                float g = 0.0f;
+                if (eval && geom) {
+                    float4 tp = L.pl[q];
+                    tp.w = ptw[e];
+                    g = geom_cost(a, qx, qy, v + 1, tp);
+                }
                 const int pd = d0 + dd - 30;
                 if (a.lr_ncc && eval && !slow && pd >= -5 && pd <= 5) {
                     const size_t i = (size_t)((pd + 5) * N + v) * lr_slots + (size_t)blk * VM_P + q;
@@ -2698,7 +2733,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 const int qx = xy & 0xFFFF, qy = xy >> 16;
                 const float pdepth = cam0.K[0] * L.base[q] / (L.disp[q] + (float)(d0 + dd - 30));
                 float4 tp = L.pl[q];
-                tp.w = dist2origin(cam0, qx, qy, pdepth, tp);
+                tp.w = dist2origin(cam0, qx, qy, pdepth, tp);  // (the same w as P0', recomputed off the hot path)
                 float tc = ncc_old_slow<F16>(a.self, qx, qy, v + 1, tp, &L.refw[q], VM_P, L.rmean[q], L.rvar[q]);
                 const float g = geom ? geom_cost(a, qx, qy, v + 1, tp) : 0.0f;
                 const int pd = d0 + dd - 30;
@@ -4006,7 +4041,8 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
         if (ctx->sweep_vm) {
             const int tw = ctx->dw_tile_w, th = VM_P / tw;
             const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
-            LAUNCH_TEX_SA(k_depth_to_weak_vm, dim3(nb), dim3(VM_BLOCK), dw_lds_bytes(a.N) + sa_lds_bytes(a), s, a, dw_chunk(a.N), tw);
+            const int dwc = dw_chunk(a.N, a.geom != 0, sa_lds_bytes(a));
+            LAUNCH_TEX_SA(k_depth_to_weak_vm, dim3(nb), dim3(VM_BLOCK), dw_lds_bytes(a.N, a.geom != 0, dwc) + sa_lds_bytes(a), s, a, dwc, tw);
         } else {
             const size_t lds = group_lds_bytes(a.N, 61 + 36);
             LAUNCH_TEX(k_depth_to_weak, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), lds, s, a);
