@@ -689,6 +689,40 @@ __device__ __forceinline__ int view_selection(const float ca[8], float prior, in
     return w;
 }
 
+// The same with the pixel's 15 draws precomputed (u[k * us] = the k-th uniform() of its stream).
+__device__ __forceinline__ int view_selection_u(const float ca[8], float prior, int iter, const float *u, int us,
+                                                const Group &G, int N) {
+    const float thr = (float)(0.8 * (double)d_expf((float)(iter * iter) / (-90.0f)));
+    float count = 0.0f, tmpw = 0.0f;
+    int cf = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float c = ca[j];
+        if (c < thr) { tmpw += d_expf(c * c / (-0.18f)); count += 1.0f; }
+        if (c > 1.2f) cf++;
+    }
+    float sp = 0.0f;
+    if (count > 2 && cf < 3) sp = tmpw / count;
+    else if (cf < 3) sp = d_expf(thr * thr / (-0.32f));
+    sp = sp * prior;
+    float sum = 0.0f;
+    for (int k = 0; k < N; ++k) sum += __shfl(sp, G.base + k);
+    const float inv = 1.0f / sum;
+    float cum = 0.0f, mycdf = 0.0f;
+    for (int k = 0; k < N; ++k) {
+        cum = fmaf(__shfl(sp, G.base + k), inv, cum);
+        if (k == G.v) mycdf = cum;
+    }
+    int w = 0;
+    for (int smp = 0; smp < 15; ++smp) {
+        const float uu = u[smp * us] - APD_FLT_EPSILON;
+        const uint32_t m = group_bits(mycdf > uu, G);
+        if (m != 0u && (__ffs(m) - 1) == G.v) w++;
+    }
+    return w;
+}
+#define VS_DRAWS 15  // uniform() draws of view_selection
+
 // PlaneHypothesisRefinement{Strong,Weak} candidate generation (APD.cu:961-980 / 1054-1067)
 struct Cands {
     float4 nrand, npert;
@@ -956,6 +990,8 @@ struct VmLds {  // static part; the cost table [9][N][64] and the weights [N][64
     uint8_t nval[8 * VM_P];      // [d][p]: neighbour d exists (adaptive-checkerboard scan hit)
     float4 pnow[VM_P];
     float st[4 * VM_P];          // depth_now, cost_now, cost_init, weight_norm
+    float vsu[VS_DRAWS * VM_P];  // [k][p]: the view selection's 15 uniform() draws of the pixel's stream
+    uint32_t tsel[VM_P];         // views with a sampled weight > 0
 };
 #define VM_CAND(L) ((L).hyp)
 // per-pixel SaWin table appended to the view-major kernels' dynamic LDS when the problem has SA masks
@@ -1047,6 +1083,11 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
                 L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
             }
             if (SA && wave == VM_WAVES - 1) saw[p] = sa_window(a, px, py);
+            if (wave == 1 % VM_WAVES) {  // the view selection's draws, once per pixel (not per view lane)
+                Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c, ord_strong(iter));
+#pragma unroll
+                for (int k = 0; k < VS_DRAWS; ++k) L.vsu[k * VM_P + p] = rg.uniform();
+            }
         }
     }
     __syncthreads();
@@ -1094,7 +1135,8 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     }
     __syncthreads();
 
-    // ---- P2: lane = (pixel, view) groups; rounds of VM_WAVES * (64/N) pixels
+    // ---- P2a: lane = (pixel, view) groups, rounds of VM_WAVES * (64/N) pixels: joint view selection
+    // (the in-order CDF over the pixel's N lanes and its 15 draws) -> view weights and selection bits
     const int Gp = WAVE / N;
     const int ppr = VM_WAVES * Gp;
     for (int r0 = 0; r0 < np; r0 += ppr) {
@@ -1109,11 +1151,9 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
         G.valid = lane_ok && pr < np;
         const int p = min(pr, np - 1);
         const int c = list[first + p];
-        const int py = c / W, px = c - py * W;
         float ca[8];
 #pragma unroll
         for (int h = 0; h < 8; ++h) ca[h] = costL[(h * N + v) * VM_P + p];
-        const float cv_now = costL[(8 * N + v) * VM_P + p];
         // view selection priors from the 4 direct neighbours (APD.cu:1323-1337)
         float prior = 0.0f;
         {
@@ -1122,21 +1162,31 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
             for (int i = 0; i < 4; ++i)
                 if (L.nval[(2 * i) * VM_P + p]) prior += ((a.sel[nb[i]] >> v) & 1u) ? 0.9f : 0.1f;
         }
-        Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c, ord_strong(iter));
-        const int w = view_selection(ca, prior, iter, rg, G, N);
+        const int w = view_selection_u(ca, prior, iter, &L.vsu[p], VM_P, G, N);
         const uint32_t tsel = group_bits(w > 0, G);
+        if (G.valid) {
+            wts[v * VM_P + p] = (uint8_t)w;
+            if (G.v == 0) L.tsel[p] = tsel;
+        }
+    }
+    __syncthreads();
+
+    // ---- P2b: lane = pixel (wave 0): weighted hypothesis costs in view order, argmin, refinement
+    // candidates (the pixel's stream resumes after the view selection's 15 draws)
+    if (wave == 0 && pv1) {
+        const int p = p1, c = c1, px = px1, py = py1;
         float fc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         float wn = 0.0f, cost_now = 0.0f;
         for (int k = 0; k < N; ++k) {
-            const int wk = __shfl(w, G.base + k);
+            const int wk = wts[k * VM_P + p];
             const float fwk = (float)wk;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const float ck = __shfl(ca[j], G.base + k);
+                const float ck = costL[(j * N + k) * VM_P + p];
                 if (wk > 0) fc[j] = fmaf(fwk, ck, fc[j]);
             }
             if (wk > 0) wn += fwk;
-            cost_now = fmaf(fwk, __shfl(cv_now, G.base + k), cost_now);
+            cost_now = fmaf(fwk, costL[(8 * N + k) * VM_P + p], cost_now);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) fc[j] /= wn;
@@ -1160,29 +1210,27 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
                 const float db = depth_from_plane(cam0, cand, px, py);
                 if (db >= a.dmin && db <= a.dmax && fcm < cost_now) {
                     depth_now = db; pnow = cand; cost_now = fcm;
-                    if (G.valid && G.v == 0) a.sel[c] = tsel;
+                    a.sel[c] = L.tsel[p];
                 }
             }
         }
         // PlaneHypothesisRefinementStrong candidates (APD.cu:950-980)
+        Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c, ord_strong(iter));
+        rg.n = VS_DRAWS;
+        rg.refill();
         const Cands C = refine_candidates(a, px, py, rg, pnow, depth_now);
-        if (G.valid) {
-            wts[v * VM_P + p] = (uint8_t)w;
-            if (G.v == 0) {
 #pragma unroll 1
-                for (int k = 0; k < 5; ++k) {
-                    float dk;
-                    float4 t = candidate(C, k, pnow, depth_now, dk);
-                    t.w = dist2origin(cam0, px, py, dk, t);
-                    VM_CAND(L)[k * VM_P + p] = t;
-                }
-                L.pnow[p] = pnow;
-                L.st[0 * VM_P + p] = depth_now;
-                L.st[1 * VM_P + p] = cost_now;
-                L.st[2 * VM_P + p] = cost_init;
-                L.st[3 * VM_P + p] = wn;
-            }
+        for (int k = 0; k < 5; ++k) {
+            float dk;
+            float4 t = candidate(C, k, pnow, depth_now, dk);
+            t.w = dist2origin(cam0, px, py, dk, t);
+            VM_CAND(L)[k * VM_P + p] = t;
         }
+        L.pnow[p] = pnow;
+        L.st[0 * VM_P + p] = depth_now;
+        L.st[1 * VM_P + p] = cost_now;
+        L.st[2 * VM_P + p] = cost_init;
+        L.st[3 * VM_P + p] = wn;
     }
     __syncthreads();
 
