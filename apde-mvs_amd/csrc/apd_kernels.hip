@@ -960,13 +960,16 @@ __global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a,
 // runs the pixel's work in phases separated by workgroup barriers, each phase with the lane shape
 // that suits it:
 //   P0  lane = (pixel, direction): adaptive-checkerboard scan of one of the 8 directions; the 9
-//       hypothesis planes, their validity and the 6x6 reference window go to LDS.
+//       hypothesis planes, their validity, the 6x6 reference window and the pixel's 15 view-selection
+//       draws go to LDS.
 //   P1  lane = pixel, wave = (hypothesis, view) task: every gather instruction of a wave samples ONE
 //       source image around 64 neighbouring pixels (compact footprint, L1 reuse across window
 //       columns and across the wave's successive tasks); costs -> LDS [h][v][pixel].
-//   P2  lane = (pixel, view) groups, as in k_sweep_strong: joint view selection with the in-order
-//       CDF and 15 draws, weighted hypothesis costs, argmin, refinement candidates (RNG order
-//       unchanged); candidates, weights and the running state -> LDS.
+//   P2a lane = (pixel, view) groups, as in k_sweep_strong: joint view selection with the in-order
+//       CDF and the 15 draws -> view weights.
+//   P2b lane = pixel (one wave, 64 pixels per instruction instead of 64/N): weighted hypothesis
+//       costs, argmin, refinement candidates (the stream resumed after the 15 draws); candidates
+//       and the running state -> LDS.
 //   P3  lane = pixel, wave = (candidate, view) task: refinement NCC (+ geometric) -> LDS.
 //   P4  lane = pixel: in-order weighted candidate costs, acceptance, writes.
 // ---------------------------------------------------------------------------------------------
@@ -982,7 +985,7 @@ __global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a,
 #ifndef APD_VM_LDS_PAD
 #define APD_VM_LDS_PAD 0  // experiments: extra LDS bytes per workgroup (fewer workgroups per CU)
 #endif
-// 39.9 KB at N = 8: four workgroups fit a CU's 160 KB of LDS.
+// 44 KB at N = 8: three workgroups fit a CU's 160 KB of LDS (the VGPR budget allows three).
 struct VmLds {  // static part; the cost table [9][N][64] and the weights [N][64] (uint8) follow
     float refw[36 * VM_P];       // [k][p]
     float4 hyp[9 * VM_P];        // [h][p]: 8 propagated + current; P2 overwrites [0..4] with the
