@@ -1049,6 +1049,61 @@ __device__ __forceinline__ int scan_direction(const APD_G float *__restrict__ co
     return best;
 }
 
+// Both directions d0 = wave, d1 = wave + 4 of a P0 lane (same near/far kind): every candidate cost is
+// loaded first (out-of-range candidates read the pixel's own cost and are ignored), then the scans
+// run in scan_direction's order -- one memory round trip instead of one per candidate.
+__device__ __forceinline__ void scan_directions2(const APD_G float *__restrict__ cost, int d0, int c, int px, int py,
+                                                 int W, int H, int q[2]) {
+    const bool far = d0 & 1;
+    constexpr int NC = 11;  // far: 11 strip candidates; near: the first + 3 x 2 V-shape candidates
+    float v[2][NC];
+    int t[2][NC];
+    bool ok[2][NC];
+    int du[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int dir = (d0 + 4 * r) >> 1;
+        const int sx = dir == 2 ? -1 : (dir == 3 ? 1 : 0);
+        const int sy = dir == 0 ? -1 : (dir == 1 ? 1 : 0);
+        du[r] = dir == 0 ? py : (dir == 1 ? H - 1 - py : (dir == 2 ? px : W - 1 - px));
+        const int step = sy * W + sx;
+        if (far) {
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+                ok[r][i] = du[r] > 2 + 2 * i;
+                t[r][i] = c + (3 + 2 * i) * step;
+            }
+        } else {
+            const bool vert = dir < 2;
+            const int vstep = vert ? 1 : W;
+            const int dneg = vert ? px : py, dpos = vert ? W - 1 - px : H - 1 - py;
+            ok[r][0] = du[r] > 0;
+            t[r][0] = c + step;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                ok[r][1 + 2 * i] = du[r] > 1 + i && dneg > i;
+                t[r][1 + 2 * i] = c + (i + 2) * step - (i + 1) * vstep;
+                ok[r][2 + 2 * i] = du[r] > 1 + i && dpos > i;
+                t[r][2 + 2 * i] = c + (i + 2) * step + (i + 1) * vstep;
+            }
+#pragma unroll
+            for (int i = 7; i < NC; ++i) { ok[r][i] = false; t[r][i] = c; }
+        }
+#pragma unroll
+        for (int i = 0; i < NC; ++i) v[r][i] = cost[ok[r][i] ? t[r][i] : c];
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        if (!ok[r][0]) { q[r] = -1; continue; }
+        int best = t[r][0];
+        float cmin = v[r][0];
+#pragma unroll
+        for (int i = 1; i < NC; ++i)
+            if (ok[r][i] && v[r][i] < cmin) { cmin = v[r][i]; best = t[r][i]; }
+        q[r] = best;
+    }
+}
+
 template <bool F16, bool SA>
 #ifndef VM_MINW
 #define VM_MINW 3  // waves per SIMD -> VGPR budget 512 / VM_MINW
@@ -1075,16 +1130,29 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
         if (p < np) {
             const int c = list[first + p];
             const int py = c / W, px = c - py * W;
-            for (int d = wave; d < 8; d += VM_WAVES) {
-                const int q = scan_direction(a.cost, d, c, px, py, W, H);
-                L.nval[d * VM_P + p] = q >= 0;
-                if (q >= 0) L.hyp[d * VM_P + p] = a.plane[q];
+            static_assert(VM_WAVES == 4, "P0 deals the 8 directions as d = wave, wave + 4");
+            int q[2];
+            scan_directions2(a.cost, wave, c, px, py, W, H, q);
+            // all loads first (the two picked planes, the own plane, the reference taps), then the LDS writes
+            float4 hp[3];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) hp[r] = a.plane[q[r] >= 0 ? q[r] : c];
+            hp[2] = a.plane[c];
+            float rv[36 / VM_WAVES];
+#pragma unroll
+            for (int kk = 0; kk < 36 / VM_WAVES; ++kk) {
+                const int k = wave + VM_WAVES * kk, i = k / 6, j = k - 6 * (k / 6);
+                rv[kk] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
             }
-            if (wave == 0) L.hyp[8 * VM_P + p] = a.plane[c];
-            for (int k = wave; k < 36; k += VM_WAVES) {
-                const int i = k / 6, j = k - 6 * (k / 6);
-                L.refw[k * VM_P + p] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int d = wave + 4 * r;
+                L.nval[d * VM_P + p] = q[r] >= 0;
+                if (q[r] >= 0) L.hyp[d * VM_P + p] = hp[r];
             }
+            if (wave == 0) L.hyp[8 * VM_P + p] = hp[2];
+#pragma unroll
+            for (int kk = 0; kk < 36 / VM_WAVES; ++kk) L.refw[(wave + VM_WAVES * kk) * VM_P + p] = rv[kk];
             if (SA && wave == VM_WAVES - 1) saw[p] = sa_window(a, px, py);
             if (wave == 1 % VM_WAVES) {  // the view selection's draws, once per pixel (not per view lane)
                 Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c, ord_strong(iter));
