@@ -1524,40 +1524,63 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const typename std
 }
 
 // NCC-New reference side of pixel slot p (APD.cu:448-575): the 9 windows' reference taps, SA tap
-// masks and moments; wave w builds windows w, w + nwaves, ... (tap order = the reference's).
+// masks and moments; wave w builds windows w, w + nwaves, ... (tap order = the reference's). Each
+// window's taps (and SA labels) are all loaded before the in-order moment sums, so a window costs one
+// memory round trip instead of one per tap.
+template <bool F16, int N1, int INC>
+__device__ __forceinline__ void wv_build_window(const Args &a, WvRefT<F16> &L, int p1, int k, int ax, int ay,
+                                                bool use_sa, int cid) {
+    constexpr int NT = N1 * N1;
+    const int tap0 = (k == 0) ? 0 : 36 + 9 * (k - 1);
+    // branch-free loads (clamped addresses; sa_at_dev's out-of-image -1 never equals a label cid > 0)
+    float r[NT];
+    bool in[NT];
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) {
+        const int i = tk / N1, j = tk - N1 * (tk / N1);
+        const int rx = ax - 5 + INC * i, ry = ay - 5 + INC * j;
+        r[tk] = tex_ref(a, rx, ry);
+        in[tk] = true;
+    }
+    if (a.sa_any) {
+#pragma unroll
+        for (int tk = 0; tk < NT; ++tk) {
+            const int i = tk / N1, j = tk - N1 * (tk / N1);
+            const long idx = (long)(ay - 5 + INC * j) * a.W + (ax - 5 + INC * i);
+            const bool inb = idx >= 0 && idx < a.HW;
+            const int lab = a.sa[inb ? idx : 0];
+            in[tk] = !use_sa || (inb && lab == cid);
+        }
+    }
+    float sr = 0.0f, srr = 0.0f, ws = 0.0f;
+    uint64_t mask = 0;
+#pragma unroll
+    for (int tk = 0; tk < NT; ++tk) {
+        if (!in[tk]) {
+            L.rref[(tap0 + tk) * VM_P + p1] = 0.0f;
+            continue;
+        }
+        L.rref[(tap0 + tk) * VM_P + p1] = r[tk];
+        mask |= 1ull << tk;
+        sr += r[tk];
+        srr = fmaf(r[tk], r[tk], srr);
+        ws += 1.0f;
+    }
+    L.wsr[k * VM_P + p1] = sr;
+    L.wsrr[k * VM_P + p1] = srr;
+    L.wsum[k * VM_P + p1] = (uint8_t)ws;
+    if (k == 0) L.tmask0[p1] = mask;
+    else L.tmask[(k - 1) * VM_P + p1] = (uint16_t)mask;
+}
 template <bool F16>
 __device__ __forceinline__ void wv_build_windows(const Args &a, WvRefT<F16> &L, int p, const APD_G short2 *anc, int cid,
                                                  int wave, int nwaves) {
     const bool use_sa = cid != 0;
-    const int p1 = p;
     for (int k = wave; k < 9; k += nwaves) {
         const short2 ap = anc[k];
         if (ap.x == -1 || ap.y == -1) continue;
-        const int ax = ap.x, ay = ap.y;
-        const int n1 = (k == 0) ? 6 : 3, inc = (k == 0) ? 2 : 5;
-        const int tap0 = (k == 0) ? 0 : 36 + 9 * (k - 1);
-        float sr = 0.0f, srr = 0.0f, ws = 0.0f;
-        uint64_t mask = 0;
-        for (int i = 0; i < n1; ++i)
-            for (int j = 0; j < n1; ++j) {
-                const int rx = ax - 5 + inc * i, ry = ay - 5 + inc * j;
-                const int tk = i * n1 + j;
-                if (use_sa && sa_at_dev(a, rx, ry) != cid) {
-                    L.rref[(tap0 + tk) * VM_P + p1] = 0.0f;
-                    continue;
-                }
-                const float r = tex_ref(a, rx, ry);
-                L.rref[(tap0 + tk) * VM_P + p1] = r;
-                mask |= 1ull << tk;
-                sr += r;
-                srr = fmaf(r, r, srr);
-                ws += 1.0f;
-            }
-        L.wsr[k * VM_P + p1] = sr;
-        L.wsrr[k * VM_P + p1] = srr;
-        L.wsum[k * VM_P + p1] = (uint8_t)ws;
-        if (k == 0) L.tmask0[p1] = mask;
-        else L.tmask[(k - 1) * VM_P + p1] = (uint16_t)mask;
+        if (k == 0) wv_build_window<F16, 6, 2>(a, L, p, k, ap.x, ap.y, use_sa, cid);
+        else wv_build_window<F16, 3, 5>(a, L, p, k, ap.x, ap.y, use_sa, cid);
     }
 }
 
@@ -1683,22 +1706,37 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         const int cid = a.sa_any ? a.sa[c1] : 0;
         const bool use_sa = cid != 0;
         if (wave == 0) {
+            // loads in three rounds (anchors; their labels and states; the STRONG anchors' planes)
             uint32_t hflag = 0, awin = 0;
+            // (branch-free: absent anchors read the pixel's own entries, which are ignored)
+            short2 ap[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) ap[k] = anc[k];
+            int lab[9], qk[9];
+            uint8_t st[9];
+#pragma unroll
             for (int k = 0; k < 9; ++k) {
-                const short2 ap = anc[k];
-                const bool ok = !(ap.x == -1 || ap.y == -1);
-                L.anc[k * VM_P + p1] = ok ? ((int)(uint16_t)ap.x | ((int)ap.y << 16)) : -1;
-                if (ok && !(use_sa && sa_at_dev(a, ap.x, ap.y) != cid)) awin |= 1u << k;
-                if (k >= 1) {
-                    const int q = ok ? ap.x + ap.y * W : -1;
-                    if (ok && a.weak[q] == APD_STRONG) {
-                        hflag |= 1u << (k - 1);
-                        L.hyp[(k - 1) * VM_P + p1] = a.plane[q];
-                    }
+                const bool ok = !(ap[k].x == -1 || ap[k].y == -1);
+                qk[k] = ok ? ap[k].x + ap[k].y * W : c1;  // anchors are in-image pixels
+                lab[k] = a.sa_any ? (int)a.sa[qk[k]] : cid;
+                st[k] = a.weak[qk[k]];
+            }
+            float4 hp[9];
+#pragma unroll
+            for (int k = 1; k < 9; ++k) hp[k] = a.plane[st[k] == APD_STRONG ? qk[k] : c1];
+            const float4 cur = a.plane[c1];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const bool ok = !(ap[k].x == -1 || ap[k].y == -1);
+                L.anc[k * VM_P + p1] = ok ? ((int)(uint16_t)ap[k].x | ((int)ap[k].y << 16)) : -1;
+                if (ok && !(use_sa && lab[k] != cid)) awin |= 1u << k;
+                if (k >= 1 && ok && st[k] == APD_STRONG) {  // (st of an absent anchor is the pixel's own: WEAK)
+                    hflag |= 1u << (k - 1);
+                    L.hyp[(k - 1) * VM_P + p1] = hp[k];
                 }
             }
             L.flags[p1] = hflag | (awin << 16);
-            L.hyp[8 * VM_P + p1] = a.plane[c1];
+            L.hyp[8 * VM_P + p1] = cur;
         }
         wv_build_windows<F16>(a, L, p1, anc, cid, wave, WV_WAVES);
     }
