@@ -2810,6 +2810,9 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
     const int dlo = ends ? 0 : 1, dhi = ends ? 61 : 60;
     for (int d0 = dlo; d0 < dhi; d0 += chunk) {
         const int dc = min(chunk, dhi - d0);
+        // t / dc for the task decode as a multiply-high: with m = ceil(2^32 / dc), umulhi(t, m) == t / dc
+        // for every t < 2^32 / dc (here t < 61 * 64); dc == 1 (m = 2^32) is taken apart
+        const uint32_t mdc = dc > 1 ? 0xFFFFFFFFu / (uint32_t)dc + 1u : 0u;
         // ---- P0': the view-independent terms of each (disparity, pixel) plane, once instead of once per
         // selected view: depth range test, plane w (dist2origin), homography terms n^T Kr^-1 / w
         for (int e = tid; e < dc * VM_P; e += VM_BLOCK) {
@@ -2845,7 +2848,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 if (has) {
                     // pixel-major: a wave-task's 64 lanes are ~64/dc neighbouring pixels x their dc
                     // disparities, so one gather instruction spans a short stretch of epipolar lines
-                    const int r = t / dc;
+                    const int r = dc > 1 ? (int)__umulhi((uint32_t)t, mdc) : t;
                     dd = t - r * dc;
                     q = vslot[v * VM_P + r];
                 }
@@ -2885,7 +2888,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
             while (j >= vb + tv) { vb += tv; ++v; nv = __builtin_amdgcn_readfirstlane(L.vcnt[v]); tv = (dc * nv + 63) >> 6; }
             const int t = (j - vb) * 64 + lane;
             if (t < dc * nv) {
-                const int r = t / dc, dd = t - r * dc;
+                const int r = dc > 1 ? (int)__umulhi((uint32_t)t, mdc) : t, dd = t - r * dc;
                 const int q = vslot[v * VM_P + r], xy = L.pxy[q];
                 const int qx = xy & 0xFFFF, qy = xy >> 16;
                 const float pdepth = cam0.K[0] * L.base[q] / (L.disp[q] + (float)(d0 + dd - 30));
