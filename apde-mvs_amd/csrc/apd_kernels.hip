@@ -544,10 +544,11 @@ __global__ __launch_bounds__(BLOCK) void k_ransac_fit(Args a, int iter) {
     float min_cost = APD_FLT_MAX;
     float4 best = make_float4(0, 0, 0, 0);
     bool has = false;
+    const FastMod fm((uint32_t)cnt);  // x % cnt without a per-draw integer division (cnt <= 8)
     for (int it = 0; it < 50; ++it) {
-        int ia = (int)(g.u32() % (uint32_t)cnt);
-        int ib = (int)(g.u32() % (uint32_t)cnt);
-        int ic = (int)(g.u32() % (uint32_t)cnt);
+        int ia = (int)fm.mod(g.u32());
+        int ib = (int)fm.mod(g.u32());
+        int ic = (int)fm.mod(g.u32());
         if (ia == ib || ib == ic || ia == ic) continue;
         if (!point_in_triangle(sx[ia], sy[ia], sx[ib], sy[ib], sx[ic], sy[ic], px, py)) continue;
         const float *A = s3[ia], *B = s3[ib], *C = s3[ic];
