@@ -22,6 +22,10 @@ ANCHOR_NUM = 9
 FIRST_INIT, REFINE_INIT, REFINE_ITER = 0, 1, 2
 WEAK, STRONG, UNKNOWN = 0, 1, 2
 
+# apd_profile_kernel kinds and apd_profile_counters slots (include/apd_hip.h)
+PROF_STRONG_SWEEP, PROF_RANSAC_FIT, PROF_WEAK_CAND, PROF_WEAK_SWEEP = 0, 1, 2, 3
+PROF_COUNTERS = 4  # [NCC-Old (Strong sweep), NCC-New (Weak sweep), geometric terms (Weak sweep), reserved]
+
 STATUS = {0: "APD_OK", -1: "APD_EINVAL", -2: "APD_ENOMEM", -3: "APD_EDEVICE", -4: "APD_ETOOMANYVIEWS",
           -5: "APD_ESTATE"}
 
@@ -178,7 +182,7 @@ class Outputs:
 EXPORTS = ["apd_abi_version", "apd_device_count", "apd_create", "apd_destroy", "apd_last_error",
            "apd_set_problem", "apd_run_patchmatch", "apd_stage_prepare", "apd_stage_iteration",
            "apd_stage_finish", "apd_synchronize", "apd_get_results", "apd_get_timing", "apd_profile_reset",
-           "apd_profile_query", "apd_profile_evaluations", "apd_epilogue", "apd_fusion_create", "apd_fusion_destroy",
+           "apd_profile_query", "apd_profile_kernel", "apd_profile_counters", "apd_profile_evaluations", "apd_epilogue", "apd_fusion_create", "apd_fusion_destroy",
            "apd_fusion_last_error", "apd_fusion_set_views", "apd_fusion_weak_filter", "apd_fusion_consistency",
            "apd_fusion_tat_levels"]
 
@@ -217,6 +221,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.apd_profile_query.restype = C.c_int32
     lib.apd_profile_query.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                       C.POINTER(C.c_int64)]
+    lib.apd_profile_kernel.restype = C.c_int32
+    lib.apd_profile_kernel.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                                       C.POINTER(C.c_int64)]
+    lib.apd_profile_counters.restype = C.c_int32
+    lib.apd_profile_counters.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]
     lib.apd_fusion_create.restype = C.c_void_p
     lib.apd_fusion_create.argtypes = [C.c_int32]
     lib.apd_fusion_destroy.argtypes = [C.c_void_p]
@@ -350,6 +359,18 @@ class Engine:
         ms, n, px = C.c_double(), C.c_int64(), C.c_int64()
         self._check(self.lib.apd_profile_query(self.ctx, C.byref(ms), C.byref(n), C.byref(px)), "apd_profile_query")
         return ms.value, n.value, px.value
+
+    def profile_kernel(self, kind: int):
+        """(total ms, launches, pixels) of the profiled launches of one APD_PROF_* kind."""
+        ms, n, px = C.c_double(), C.c_int64(), C.c_int64()
+        self._check(self.lib.apd_profile_kernel(self.ctx, kind, C.byref(ms), C.byref(n), C.byref(px)),
+                    "apd_profile_kernel")
+        return ms.value, n.value, px.value
+
+    def profile_counters(self):
+        c = (C.c_int64 * PROF_COUNTERS)()
+        self._check(self.lib.apd_profile_counters(self.ctx, c, PROF_COUNTERS), "apd_profile_counters")
+        return list(c)
 
     def profile_evaluations(self) -> int:
         n = C.c_int64()

@@ -89,7 +89,7 @@ struct Args {
     APD_G float *curve;                    // optional H*W*61
     const APD_G short2 *near_offsets;      // 201*201 offsets sorted by (d^2, x, y)
     const APD_G struct Args *self;         // this struct in device memory, for out-of-line callees
-    APD_G unsigned long long *evals;       // profiling only (else null): NCC-Old evaluations issued
+    APD_G unsigned long long *evals;       // profiling only (else null): the APD_PROF_COUNTERS device counters (apd_hip.h)
     // DepthToWeak -> LocalRefine hand-over (view-major kernels; null = off): the NCC-Old and geometric
     // terms of DepthToWeak's samples p_disp = -5..5, which are LocalRefine's, [11][N][tile slots]
     APD_G float *lr_ncc;

@@ -1931,6 +1931,26 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     }
     __syncthreads();
 
+    if (a.evals && wave == 0) {
+        // profiling: the NCC-New evaluations and geometric terms CheckerboardPropagationWeak issues
+        // for this pixel (APD.cu:1471-1482, 1577-1589, 1026-1094) whose values are used: the valid
+        // anchor candidates x N views, the current plane x N, and -- when the fit plane exists -- the
+        // fit plane and the 5 refinement candidates x the views with weight > 0. Counted whether the
+        // values came from k_weak_cand_vm, RandomInitialization's kept costs or this kernel.
+        uint32_t nn = 0, ng = 0;
+        if (pv1) {
+            int nsel = 0;
+            for (int v = 0; v < N; ++v) nsel += wts[v * VM_P + p1] > 0;
+            const int nh = __builtin_popcount(L.flags[p1] & 0xFFu);
+            const int nr = refine ? 6 * nsel : 0;
+            nn = (uint32_t)((nh + 1) * N + nr);
+            ng = geom ? (uint32_t)(nh * nsel + N + nr) : 0u;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) { nn += __shfl_xor(nn, o); ng += __shfl_xor(ng, o); }
+        if (lane == 0) { atomicAdd(a.evals + 1, (unsigned long long)nn); atomicAdd(a.evals + 2, (unsigned long long)ng); }
+    }
+
     // ---- P6: acceptance, writes
     if (pv1) {
         for (int v = wave; v < N; v += WV_WAVES) a.vw[(size_t)v * a.HW + c1] = (uint8_t)wts[v * VM_P + p1];
@@ -3533,6 +3553,7 @@ struct apd_ctx {
     bool wcur_on = true;           // RandomInit keeps WEAK current-plane costs for iteration 0; APD_NO_WCUR=1 disables
     bool wcur_fresh = false;       // they belong to the current planes (set by prepare, cleared by iteration)
     int weak_count = 0;
+    size_t lrs_need = 0;           // bytes of the LocalRefine hand-over this problem uses (0: none)
     int cnt[4] = {0, 0, 0, 0};     // strong black, strong red, weak black, weak red
     size_t list_cap = 0;
     bool want_curve = false;
@@ -3540,10 +3561,14 @@ struct apd_ctx {
     // timing
     hipEvent_t ev[16] = {};
     apd_timing timing{};
-    // profiling of the dominant kernel
+    // profiling of the loop-body kernels (HIP events around each launch on the ctx stream)
+    struct ProfEv {
+        hipEvent_t e0, e1;
+        int kind;    // APD_PROF_STRONG_SWEEP, APD_PROF_RANSAC_FIT, APD_PROF_WEAK_CAND, APD_PROF_WEAK_SWEEP
+        int64_t px;  // pixels the launch covered
+    };
     bool prof = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_ev;
-    int64_t prof_pixels = 0;
+    std::vector<ProfEv> prof_ev;
 };
 
 #define HIP_OK(ctx, call)                                                                          \
@@ -3766,7 +3791,7 @@ void apd_destroy(apd_ctx *ctx) {
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
-    for (auto &pe : ctx->prof_ev) { (void)hipEventDestroy(pe.first); (void)hipEventDestroy(pe.second); }
+    for (auto &pe : ctx->prof_ev) { (void)hipEventDestroy(pe.e0); (void)hipEventDestroy(pe.e1); }
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -3972,6 +3997,32 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
         if ((st = ensure(ctx, ctx->curve, HW * 61 * sizeof(float)))) return st;
         HIP_OK(ctx, hipMemsetAsync(ctx->curve.p, 0, HW * 61 * sizeof(float), s));
     }
+    // DepthToWeak -> LocalRefine hand-over ([11][N][tile slots] fp32 NCC-Old, and as much again for
+    // the geometric terms: 21.5 GB at 6048x4032, N = 10, with geometry). Sized here, after every
+    // buffer the path needs, so that no allocation sits inside the timed stages: held at exactly this
+    // problem's size (a larger buffer from an earlier problem is released, so a scan's geometric
+    // pass does not keep it through the next round's init pass), and only when it fits in the
+    // device's free memory with 4 GiB to spare -- else LocalRefine evaluates the samples itself.
+    ctx->lrs_need = 0;
+    if (ctx->sweep_vm && ctx->lr_handover) {
+        const int tw = ctx->dw_tile_w, th = VM_P / tw;
+        const size_t slots = (size_t)(((W + tw - 1) / tw) * ((H + th - 1) / th)) * VM_P;
+        const size_t need = (size_t)11 * N * slots * sizeof(float) * (P.geom_consistency ? 2 : 1);
+        if (ctx->lrs.p && ctx->lrs.bytes != need) {
+            (void)hipFree(ctx->lrs.p);
+            ctx->lrs.p = nullptr;
+            ctx->lrs.bytes = 0;
+        }
+        size_t free_b = 0, total_b = 0;
+        const size_t spare = (size_t)4 << 30;
+        if (!ctx->lrs.p && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > spare && need <= free_b - spare) {
+            if (ensure(ctx, ctx->lrs, need) != APD_OK) {  // not fatal: clear the allocation error
+                (void)hipGetLastError();
+                ctx->err.clear();
+            }
+        }
+        if (ctx->lrs.p) ctx->lrs_need = need;
+    }
     ctx->params = P;
     ctx->loaded = true;
     return APD_OK;
@@ -4097,23 +4148,36 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
     return APD_OK;
 }
 
+// profiling brackets around one launch (no-ops unless apd_profile_reset(ctx, 1))
+static hipEvent_t prof_begin(apd_ctx *ctx) {
+    hipEvent_t e0 = nullptr;
+    if (ctx->prof) {
+        (void)hipEventCreate(&e0);
+        (void)hipEventRecord(e0, ctx->stream);
+    }
+    return e0;
+}
+static void prof_end(apd_ctx *ctx, hipEvent_t e0, int kind, int64_t px) {
+    if (!ctx->prof) return;
+    hipEvent_t e1 = nullptr;
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e1, ctx->stream);
+    ctx->prof_ev.push_back({e0, e1, kind, px});
+}
+
 int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
     if (!ctx || !ctx->prepared) return APD_ESTATE;
     (void)hipSetDevice(ctx->device);
     Args &a = ctx->args;
     hipStream_t s = ctx->stream;
     int st;
+    APD_G unsigned long long *evals = (ctx->prof && ctx->evals.p) ? (APD_G unsigned long long *)ctx->evals.p : nullptr;
     for (int colour = 0; colour < 2; ++colour) {
         const int n = ctx->cnt[colour];
         if (n <= 0) continue;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (ctx->prof) {
-            (void)hipEventCreate(&e0);
-            (void)hipEventCreate(&e1);
-            (void)hipEventRecord(e0, s);
-        }
+        hipEvent_t e0 = prof_begin(ctx);
         Args ak = a;
-        if (ctx->prof && ctx->evals.p) ak.evals = (APD_G unsigned long long *)ctx->evals.p;
+        ak.evals = evals;
         if (!(ctx->wcur_fresh && iter == 0)) ak.wcur = nullptr;  // RandomInitialization's costs: iteration 0 only
         if (ctx->sweep_vm)
             LAUNCH_TEX_SA(k_sweep_strong_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), vm_lds_bytes(a.N) + sa_lds_bytes(a), s,
@@ -4121,15 +4185,13 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
         else
             LAUNCH_TEX(k_sweep_strong, dim3(group_blocks(n, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a,
                        (const int *)list_ptr(ctx, colour), n, iter);
-        if (ctx->prof) {
-            (void)hipEventRecord(e1, s);
-            ctx->prof_ev.emplace_back(e0, e1);
-            ctx->prof_pixels += n;
-        }
+        prof_end(ctx, e0, APD_PROF_STRONG_SWEEP, n);
         if ((st = check_launch(ctx, "k_sweep_strong"))) return st;
     }
     if (a.use_apd) {
+        hipEvent_t e0 = prof_begin(ctx);
         hipLaunchKernelGGL(k_ransac_fit, dim3(blocks_for((size_t)a.HW, BLOCK)), dim3(BLOCK), 0, s, a, iter);
+        prof_end(ctx, e0, APD_PROF_RANSAC_FIT, a.HW);
         const int nw = ctx->cnt[2] + ctx->cnt[3];
         const int wc = std::max(ctx->weak_count, 1);
         const float *cand = nullptr;
@@ -4139,9 +4201,11 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
                 ctx->err = "candidate cost buffers not sized by apd_stage_prepare";
                 return APD_ESTATE;
             }
+            e0 = prof_begin(ctx);
             LAUNCH_TEX(k_weak_cand_vm, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK),
                        (ctx->args.tex_f16 ? pk_lds_bytes<true>() : pk_lds_bytes<false>()), s, a,
                        (const int *)ctx->wlist.p, nw, (float *)ctx->wcand.p, (uint8_t *)ctx->wdone.p, wc);
+            prof_end(ctx, e0, APD_PROF_WEAK_CAND, nw);
             cand = (const float *)ctx->wcand.p;
         }
         for (int colour = 0; colour < 2; ++colour) {
@@ -4149,13 +4213,16 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             if (n <= 0) continue;
             // RandomInitialization's kept costs are valid for the first iteration after it only
             Args aw = a;
+            aw.evals = evals;
             if (!(ctx->wcur_fresh && iter == 0)) aw.wcur = nullptr;
+            e0 = prof_begin(ctx);
             if (ctx->sweep_vm)
                 LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N) : wv_lds_bytes<false>(a.N)), s,
                            aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, (const uint8_t *)ctx->wdone.p, wc);
             else
                 LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
                            (const int *)list_ptr(ctx, 2 + colour), n, iter);
+            prof_end(ctx, e0, APD_PROF_WEAK_SWEEP, n);
         }
         if ((st = check_launch(ctx, "weak sweep"))) return st;
     }
@@ -4180,23 +4247,12 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
     if (ctx->want_curve && ctx->curve.p) a.curve = devptr<decltype(a.curve)>(ctx->curve.p);
     a.lr_ncc = nullptr;
     a.lr_geo = nullptr;
-    if (ctx->sweep_vm && ctx->lr_handover) {
+    if (ctx->sweep_vm && ctx->lr_handover && ctx->lrs_need > 0 && ctx->lrs.p && ctx->lrs.bytes >= ctx->lrs_need) {
         // DepthToWeak hands LocalRefine the NCC-Old / geometric terms of the 11 samples they share
-        // ([11][N][tile slots] each: 21.5 GB at 6048x4032, N = 10, with geometry); skipped above
-        // 48 GiB (LocalRefine then evaluates them itself)
-        const int tw = ctx->dw_tile_w, th = VM_P / tw;
-        const size_t slots = (size_t)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th)) * VM_P;
-        const size_t plane = (size_t)11 * a.N * slots;
-        const size_t bytes = plane * sizeof(float) * (a.geom ? 2 : 1);
-        if (bytes <= ((size_t)48 << 30)) {
-            if (ensure(ctx, ctx->lrs, bytes) == APD_OK) {
-                a.lr_ncc = devptr<decltype(a.lr_ncc)>(ctx->lrs.p);
-                a.lr_geo = a.geom ? devptr<decltype(a.lr_geo)>((float *)ctx->lrs.p + plane) : nullptr;
-            } else {  // not fatal: clear the allocation error
-                (void)hipGetLastError();
-                ctx->err.clear();
-            }
-        }
+        // (buffer sized by apd_set_problem; without it LocalRefine evaluates them itself)
+        const size_t plane = ctx->lrs_need / (sizeof(float) * (a.geom ? 2 : 1));
+        a.lr_ncc = devptr<decltype(a.lr_ncc)>(ctx->lrs.p);
+        a.lr_geo = a.geom ? devptr<decltype(a.lr_geo)>((float *)ctx->lrs.p + plane) : nullptr;
     }
     {
         if (ctx->sweep_vm) {
@@ -4291,42 +4347,54 @@ int32_t apd_profile_reset(apd_ctx *ctx, int32_t enable) {
     if (!ctx) return APD_EINVAL;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    for (auto &pe : ctx->prof_ev) { (void)hipEventDestroy(pe.first); (void)hipEventDestroy(pe.second); }
+    for (auto &pe : ctx->prof_ev) { (void)hipEventDestroy(pe.e0); (void)hipEventDestroy(pe.e1); }
     ctx->prof_ev.clear();
-    ctx->prof_pixels = 0;
     ctx->prof = enable != 0;
     if (ctx->prof) {
-        int st = ensure(ctx, ctx->evals, sizeof(unsigned long long));
+        int st = ensure(ctx, ctx->evals, APD_PROF_COUNTERS * sizeof(unsigned long long));
         if (st) return st;
-        HIP_OK(ctx, hipMemsetAsync(ctx->evals.p, 0, sizeof(unsigned long long), ctx->stream));
+        HIP_OK(ctx, hipMemsetAsync(ctx->evals.p, 0, APD_PROF_COUNTERS * sizeof(unsigned long long), ctx->stream));
     }
+    return APD_OK;
+}
+
+int32_t apd_profile_counters(apd_ctx *ctx, int64_t *counts, int32_t n) {
+    if (!ctx || !counts || n < 0) return APD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+    unsigned long long c[APD_PROF_COUNTERS] = {};
+    if (ctx->evals.p) HIP_OK(ctx, hipMemcpy(c, ctx->evals.p, sizeof(c), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) counts[i] = i < APD_PROF_COUNTERS ? (int64_t)c[i] : 0;
     return APD_OK;
 }
 
 int32_t apd_profile_evaluations(apd_ctx *ctx, int64_t *ncc_evaluations) {
-    if (!ctx || !ncc_evaluations) return APD_EINVAL;
-    (void)hipSetDevice(ctx->device);
-    HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
-    unsigned long long n = 0;
-    if (ctx->evals.p) HIP_OK(ctx, hipMemcpy(&n, ctx->evals.p, sizeof(n), hipMemcpyDeviceToHost));
-    *ncc_evaluations = (int64_t)n;
-    return APD_OK;
+    if (!ncc_evaluations) return APD_EINVAL;
+    return apd_profile_counters(ctx, ncc_evaluations, 1);
 }
 
-int32_t apd_profile_query(apd_ctx *ctx, double *sweep_ms_total, int64_t *sweep_launches, int64_t *sweep_pixels) {
+int32_t apd_profile_kernel(apd_ctx *ctx, int32_t kind, double *ms_total, int64_t *launches, int64_t *pixels) {
     if (!ctx) return APD_EINVAL;
     (void)hipSetDevice(ctx->device);
     HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
     double tot = 0.0;
+    int64_t nl = 0, px = 0;
     for (auto &pe : ctx->prof_ev) {
+        if (pe.kind != kind) continue;
         float ms = 0.0f;
-        (void)hipEventElapsedTime(&ms, pe.first, pe.second);
+        (void)hipEventElapsedTime(&ms, pe.e0, pe.e1);
         tot += ms;
+        ++nl;
+        px += pe.px;
     }
-    if (sweep_ms_total) *sweep_ms_total = tot;
-    if (sweep_launches) *sweep_launches = (int64_t)ctx->prof_ev.size();
-    if (sweep_pixels) *sweep_pixels = ctx->prof_pixels;
+    if (ms_total) *ms_total = tot;
+    if (launches) *launches = nl;
+    if (pixels) *pixels = px;
     return APD_OK;
+}
+
+int32_t apd_profile_query(apd_ctx *ctx, double *sweep_ms_total, int64_t *sweep_launches, int64_t *sweep_pixels) {
+    return apd_profile_kernel(ctx, APD_PROF_STRONG_SWEEP, sweep_ms_total, sweep_launches, sweep_pixels);
 }
 
 int32_t apd_epilogue(int32_t width, int32_t height, const float *planes, float depth_min, float depth_max,

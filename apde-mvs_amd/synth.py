@@ -10,6 +10,7 @@ tools/colmap2mvsnet.py:494-514 writes and APD.cpp:85-135 / main.cpp:44-102 read.
 from __future__ import annotations
 
 import os
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -58,24 +59,34 @@ class _Texture:
 
     SIZE = 512
 
-    def __init__(self, rng, base_freq=6.0, flat_patches=()):
+    def __init__(self, rng, base_freq=6.0, flat_patches=(), detail=None):
         n = self.SIZE
-        white = rng.normal(size=(n, n))
-        fy = np.fft.fftfreq(n)[:, None]
-        fx = np.fft.fftfreq(n)[None, :]
-        band = np.exp(-((np.hypot(fx, fy) * n / 24.0) ** 2))  # keep ~24 cycles per tile
-        tex = np.real(np.fft.ifft2(np.fft.fft2(white) * band))
-        self.tex = (tex / tex.std()).astype(np.float32)
+        self.tex = self._noise(rng, n, 24.0)  # keep ~24 cycles per tile
         self.k = base_freq * n / 24.0 / (2 * np.pi) * 2.0  # texels per world unit
         self.flat = list(flat_patches)  # (u0, v0, u1, v1, value)
         self.mean = rng.uniform(90, 160)
         self.scale = rng.uniform(28, 40)
+        # optional fine detail (texture-rich scenes): (rng, texels per world unit, amplitude), from a
+        # generator of its own so the coarse texture is the same with and without it
+        self.detail = None
+        if detail is not None:
+            drng, dk, damp = detail
+            self.detail = (self._noise(drng, self.DETAIL_SIZE, self.DETAIL_SIZE / 8.0), dk, damp)
 
-    def __call__(self, u, v):
-        """Returns (value, flat_mask): flat_mask marks the textureless patches."""
-        n = self.SIZE
-        x = u * self.k
-        y = v * self.k
+    DETAIL_SIZE = 1024
+
+    @staticmethod
+    def _noise(rng, n, cycles):
+        white = rng.normal(size=(n, n))
+        fy = np.fft.fftfreq(n)[:, None]
+        fx = np.fft.fftfreq(n)[None, :]
+        band = np.exp(-((np.hypot(fx, fy) * n / cycles) ** 2))
+        tex = np.real(np.fft.ifft2(np.fft.fft2(white) * band))
+        return (tex / tex.std()).astype(np.float32)
+
+    @staticmethod
+    def _bilinear(T, x, y):
+        n = T.shape[0]
         x0 = np.floor(x)
         y0 = np.floor(y)
         ax = x - x0
@@ -84,10 +95,16 @@ class _Texture:
         y0 = y0.astype(np.int64) % n
         x1 = (x0 + 1) % n
         y1 = (y0 + 1) % n
-        T = self.tex
         top = T[y0, x0] * (1 - ax) + T[y0, x1] * ax
         bot = T[y1, x0] * (1 - ax) + T[y1, x1] * ax
-        val = self.mean + self.scale * (top * (1 - ay) + bot * ay)
+        return top * (1 - ay) + bot * ay
+
+    def __call__(self, u, v):
+        """Returns (value, flat_mask): flat_mask marks the textureless patches."""
+        val = self.mean + self.scale * self._bilinear(self.tex, u * self.k, v * self.k)
+        if self.detail is not None:
+            T, dk, damp = self.detail
+            val = val + damp * self.scale * self._bilinear(T, u * dk, v * dk)
         flat = np.zeros(val.shape, bool)
         for (u0, v0, u1, v1, value) in self.flat:
             m = (u >= u0) & (u <= u1) & (v >= v0) & (v <= v1)
@@ -119,28 +136,54 @@ class _Quad:
 
         with np.errstate(divide="ignore", invalid="ignore"):
             t = ((self.o - C) @ self.n) / lin(self.n)
-        rel0 = C - self.o
-        b0 = rel0 @ self.eu + t * lin(self.eu)
-        b1 = rel0 @ self.ev + t * lin(self.ev)
-        s = self.Ginv[0, 0] * b0 + self.Ginv[0, 1] * b1
-        r = self.Ginv[1, 0] * b0 + self.Ginv[1, 1] * b1
-        ok = (t > 1e-6) & (s >= 0) & (s <= 1) & (r >= 0) & (r <= 1) & np.isfinite(t)
+            rel0 = C - self.o
+            b0 = rel0 @ self.eu + t * lin(self.eu)
+            b1 = rel0 @ self.ev + t * lin(self.ev)
+            s = self.Ginv[0, 0] * b0 + self.Ginv[0, 1] * b1
+            r = self.Ginv[1, 0] * b0 + self.Ginv[1, 1] * b1
+            ok = (t > 1e-6) & (s >= 0) & (s <= 1) & (r >= 0) & (r <= 1) & np.isfinite(t)
         return np.where(ok, t, np.inf), s * np.linalg.norm(self.eu), r * np.linalg.norm(self.ev)
 
 
-def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=True, depth=6.0) -> Scene:
+TEXTURES = ("smooth", "rich")
+
+
+def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=True, depth=6.0,
+               workers: int = 0, texture: str = "smooth", detail_period_px: float = 5.0) -> Scene:
+    """texture="smooth": band-limited textures fixed in world units, so they get smoother per pixel
+    as the resolution grows (90-94 % of the pixels end WEAK at 3024x2016 and 6048x4032).
+    texture="rich": the same scene plus a fine detail octave of `detail_period_px` pixels at the
+    reference view, and three more textureless patches: a resolution-independent, texture-rich
+    variant whose WEAK fraction is set by the textureless area."""
+    if texture not in TEXTURES:
+        raise ValueError(f"texture must be one of {TEXTURES}")
     rng = np.random.default_rng(seed)
+    rich = texture == "rich"
+    drng = np.random.default_rng(seed + 1) if rich else None
     f = 0.8 * width
     K = np.array([[f, 0.0, width / 2.0], [0.0, f, height / 2.0], [0.0, 0.0, 1.0]])
+
+    def detail():
+        if not rich:
+            return None
+        period_world = detail_period_px * depth / f  # world size of the detail period at the wall
+        return (drng, (_Texture.DETAIL_SIZE / (_Texture.DETAIL_SIZE / 8.0)) / period_world, 0.8)
+
     # scene geometry in world coords (ref camera at origin looking along +z)
     half_w = depth * (width / 2.0) / f * 1.6
     half_h = depth * (height / 2.0) / f * 1.6
     quads = []
     flat = [(0.68 * half_w, 0.25 * half_h, 1.2 * half_w, 1.1 * half_h, 128.0)] if weak_patches else []
+    floor_flat = []
+    if rich and weak_patches:
+        flat += [(1.45 * half_w, 0.1 * half_h, 2.0 * half_w, 1.5 * half_h, 112.0),
+                 (0.05 * half_w, 1.25 * half_h, 0.9 * half_w, 1.9 * half_h, 150.0)]
+        floor_flat = [(0.2 * half_w, 0.0, 1.1 * half_w, 0.35 * depth, 96.0)]
     quads.append(_Quad([-half_w, -half_h, depth], [2 * half_w, 0, 0.35 * depth], [0, 2 * half_h, 0],
-                       _Texture(rng, base_freq=4.0, flat_patches=flat)))  # slanted back wall
+                       _Texture(rng, base_freq=4.0, flat_patches=flat, detail=detail())))  # slanted back wall
     quads.append(_Quad([-half_w, 0.55 * half_h, 0.45 * depth], [2 * half_w, 0, 0],
-                       [0, 0.45 * half_h, 0.9 * depth], _Texture(rng, base_freq=5.0)))  # floor
+                       [0, 0.45 * half_h, 0.9 * depth],
+                       _Texture(rng, base_freq=5.0, flat_patches=floor_flat, detail=detail())))  # floor
     for b in range(3):
         cx = rng.uniform(-0.6, 0.6) * half_w
         cy = rng.uniform(-0.5, 0.3) * half_h
@@ -150,7 +193,7 @@ def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=Tru
         eu = np.array([np.cos(ang), 0, np.sin(ang)]) * sz
         ev = np.array([0, 1.0, rng.uniform(-0.3, 0.3)]) * sz
         bflat = [(0.1 * sz, 0.1 * sz, 0.7 * sz, 0.7 * sz, rng.uniform(60, 200))] if (weak_patches and b == 0) else []
-        quads.append(_Quad([cx, cy, cz], eu, ev, _Texture(rng, base_freq=7.0, flat_patches=bflat)))
+        quads.append(_Quad([cx, cy, cz], eu, ev, _Texture(rng, base_freq=7.0, flat_patches=bflat, detail=detail())))
 
     # cameras: ref at origin, sources on an arc around the scene centre
     target = np.array([0.0, 0.0, 0.8 * depth])
@@ -165,8 +208,8 @@ def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=Tru
     xs = np.arange(width, dtype=np.float64)
     ys = np.arange(height, dtype=np.float64)
     Kinv = np.linalg.inv(K)
-    images, depths, labels = [], [], []
-    for cam in cams:
+
+    def render(cam, noise):
         M = cam.R.T @ Kinv  # world-frame ray of pixel (x, y) with camera-frame z = 1
         C = cam.center
         best_t = np.full((height, width), np.inf)
@@ -186,16 +229,27 @@ def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=Tru
                 tv, tf = q.tex(hits[qi][0][m], hits[qi][1][m])
                 val[m] = tv
                 flat[m] = tf
+        del hits
         lab = (best_q + 1).astype(np.uint8)
         hit = np.isfinite(best_t)
         # textureless patches: constant albedo + per-view sensor noise (uncorrelated across views, so
         # NCC cannot lock on and DepthToWeak classifies them WEAK, APD.cu:2220-2249)
-        val = np.where(flat, val + rng.normal(0.0, 2.0, size=val.shape), val)
+        val = np.where(flat, val + noise, val)
         img = np.where(hit, val, 30.0)
         img = np.clip(np.round(img), 0, 255).astype(np.float32)
-        images.append(img)
-        depths.append(np.where(hit, best_t, 0.0).astype(np.float32))  # ray z = 1 in camera frame
-        labels.append(lab)
+        return img, np.where(hit, best_t, 0.0).astype(np.float32), lab  # ray z = 1 in camera frame
+
+    # The views render in parallel (numpy releases the GIL in its array loops); the only random draws
+    # after the cameras are each view's sensor noise, drawn here in view order, so the scene does not
+    # depend on the number of workers.
+    workers = max(1, min(len(cams), workers if workers else min(8, os.cpu_count() or 1)))
+    with ThreadPoolExecutor(workers) as pool:
+        futs = [pool.submit(render, cam, rng.normal(0.0, 2.0, size=(height, width))) for cam in cams]
+        rendered = [f.result() for f in futs]
+    images = [r[0] for r in rendered]
+    depths = [r[1] for r in rendered]
+    labels = [r[2] for r in rendered]
+    del rendered
     valid = np.concatenate([d[d > 0] for d in depths])
     dmin = float(np.percentile(valid, 1) * 0.75)
     dmax = float(np.percentile(valid, 99) * 1.25)

@@ -1,24 +1,39 @@
-"""Benchmark: Mpix/s per PatchMatch iteration on the BASELINE.json configs[1] workload.
+"""Benchmark: Mpix/s per PatchMatch iteration on the north-star workload, BASELINE.json configs[2].
 
-Workload (BASELINE.md §3 "C2"): a synthetic ETH3D-office-shaped scan at half resolution, 3024x2016,
-one reference view + 8 source views, FIRST_INIT pass (geometric consistency off, APD off). A "step" is
-one iteration of the sweep loop body (APD.cu:2699-2708: Black + Red Strong checkerboard kernels) over
-the whole reference view; the view is uploaded and initialised (RandomInitialization) before the timed
-region, so inputs are resident in HBM. value = W*H*steps summed over ranks / max-over-ranks time.
+Workload ("C3"): a synthetic ETH3D-office-shaped scan at full resolution,
+6048x4032, one reference view + 10 source views, the final round's geometric pass of main.cpp
+(main.cpp:333-365 with i = 3: REFINE_ITER, deformable PatchMatch (APD) with focal-weighted anchors,
+geometric consistency, impetus, rotate_time 4, ransac_threshold 0.00625). Its priors (depths,
+normals, pixel states, confidence of every view) come from FIRST_INIT runs of the scan's views at the
+same resolution. A "step" is one iteration of the loop body APD.cu:2699-2708 over the whole
+reference view: Strong sweep black + red, RANSACToGetFitPlane, and the Weak sweep black + red
+(k_weak_cand_vm + k_sweep_weak_vm). Steps are iterations 0, 1, 2 of FRESH runs (the
+median over a fresh run's iterations): before every block of (up to) 3 steps the problem is
+re-uploaded and re-initialised (apd_set_problem + apd_stage_prepare, outside the timed region), so
+no step repeats an iteration on an already-converged view. Each block is bracketed by a barrier and
+a device synchronisation, and the blocks' times are summed; inputs are resident in HBM throughout.
+value = W*H*steps summed over ranks / max-over-ranks time.
 
-Multi-GPU (weak scaling): one process per GPU (torch.distributed.run), each rank runs its own reference
-view of the scan (the scan's views are independent in a FIRST_INIT pass); the only collectives are the
-timing barrier and a max-reduction of the elapsed time (no data-path collective).
+Multi-GPU (weak scaling): one process per GPU (torch.distributed.run); each rank runs its own
+reference view (rank mod #views) with its own priors. Within a pass the reference views are
+independent given the previous pass's depth maps, so the only collectives are the
+timing barriers and a max-reduction of the elapsed time (no data-path collective).
 
-Besides the headline line the JSON carries:
-  roofline      dominant kernel (k_sweep_strong): algorithmic FP32 flops per launch (SURVEY.md §8d:
-                1446 flop per NCC-Old evaluation x evaluations actually issued) / its mean launch time
-                from HIP events on the engine stream, against the FP32 peak; HBM bytes from the latest
-                rocprofv3 PMC summary under profiles/ when present.
-  cpu_baseline  the C oracle (oracle/liboracle.so, OpenMP) on a bounded sample: the same scene rendered
-                at 756x504 (same cameras/texture statistics, same N), one sweep iteration.
-  apd_pass      (rank 0) the same metric for an APD + geometric-consistency pass (main.cpp rounds >= 1)
-                on the same view, priors from FIRST_INIT runs of every view of the scene.
+Besides the headline the JSON line carries:
+  roofline      the dominant kernels of the step, the Weak sweep (k_weak_cand_vm + 2 x k_sweep_weak_vm
+                per iteration, 95 % of it at C3): algorithmic FP32 flops = NCC-New evaluations x 4038 +
+                geometric terms x 80, both counted on the device for the evaluations
+                CheckerboardPropagationWeak uses (apd_profile_counters), / their summed launch time from
+                HIP events on the engine stream, against the FP32 vector peak; HBM bytes per launch from
+                the newest rocprofv3 PMC summary of k_sweep_weak_vm at this shape under profiles/.
+  cpu_baseline  the C oracle (oracle/liboracle.so) on a bounded sample of the same workload: the
+                same scene rendered at 756x504 with N = 10, one APD iteration of the same pass, at
+                --cpu-threads cores; plus the same at 1 core on 378x252 (cpu_baseline_1core).
+  end_to_end    one full RunPatchMatch of the headline problem (main.cpp:157-161 bracket).
+  c2_first_init configs[1] (3024x2016, N = 8, FIRST_INIT, Strong sweep only): the round-1/2 headline,
+                same fresh-run timing, with the Strong sweep's NCC-Old roofline.
+  rich_texture  the headline pass on the texture-rich variant of the scene (synth texture="rich":
+                fine detail + more textureless patches, WEAK fraction 30-50 % instead of ~94 %).
 """
 from __future__ import annotations
 
@@ -26,8 +41,10 @@ import argparse
 import glob
 import json
 import os
+import statistics
 import sys
 import time
+from types import SimpleNamespace
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(REPO, "apde-mvs_amd"), os.path.join(REPO, "tests")]
@@ -35,23 +52,17 @@ sys.path[:0] = [os.path.join(REPO, "apde-mvs_amd"), os.path.join(REPO, "tests")]
 import numpy as np  # noqa: E402
 
 METRIC = "Mpix/s per PatchMatch iteration (ref view, N src) at 1/2/4/8 GPU; depth L1 vs ref"
-FLOP_PER_NCC_OLD = 36 * 36 + 150  # 36 samples x 36 flop + homography/finalise
-PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) peak
+FLOP_PER_NCC_OLD = 36 * 36 + 150   # 36 samples x 36 flop + homography/finalise
+FLOP_PER_NCC_NEW = 108 * 36 + 150  # <= 108 samples (6x6 centre + 8 anchors x 3x3)
+FLOP_PER_GEOM = 80                 # one geometric-consistency term
+PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak (packed FP32)
 PEAK_HBM_GBS = 8000.0
+FINAL_ROUND = 3  # C3 has 4 rounds (6048 -> 756 halvings, main.cpp:129-146); the headline is round 3
 
 
-def strong_evaluations(W: int, H: int, n_src: int, colour: int, row_limit: int) -> int:
-    """Upper bound on the NCC-Old evaluations of one Strong sweep launch over a colour: per pixel
-    (valid adaptive-checkerboard neighbours + current + 5 refinement candidates) x N views. The
-    refinement NCCs of views with sampled weight 0 are skipped by the kernel, so the device count
-    (apd_profile_evaluations) is lower; roofline.achieved uses the device count."""
-    ys = np.arange(row_limit)[:, None]
-    xs = np.arange(W)[None, :]
-    mask = ((xs + ys) & 1) == colour
-    flags = ((ys > 2).astype(int) + (ys < H - 3) + (xs > 2) + (xs < W - 3) + (ys > 0) + (ys < H - 1)
-             + (xs > 0) + (xs < W - 1))
-    per_px = flags + 6
-    return int((per_px * mask).sum()) * n_src
+def workload_name(W, H, N, apd):
+    known = {(6048, 4032, 10, True): "C3", (3024, 2016, 8, False): "C2"}
+    return known.get((W, H, N, apd), "custom")
 
 
 def latest_pmc(kernel: str, W: int, n_src: int):
@@ -65,56 +76,225 @@ def latest_pmc(kernel: str, W: int, n_src: int):
         if (isinstance(pmc, dict) and str(pmc.get("kernel", "")).startswith(kernel)
                 and pmc.get("width") == W and pmc.get("n_src") == n_src
                 and pmc.get("hbm_bytes_per_launch") is not None):
+            pmc["_file"] = os.path.relpath(f, REPO)
             return pmc
     return None
 
 
-def cpu_baseline(scene_args, n_src, threads):
-    import oracle_lib
+def make_scene(W, H, N, world, texture):
     import synth
-    import apd_abi as A
+    return synth.make_scene(W, H, max(N, world), seed=20251114, texture=texture)
 
-    w, h = 756, 504
-    sc = synth.make_scene(w, h, n_src, **scene_args)
-    arr = A.scene_problem(sc, 0, [j for j, _ in sc.pairs[0]][:n_src])
-    lib = oracle_lib.load()
+
+def first_init_priors(eng, sc, ids, N):
+    """FIRST_INIT runs (round 0's data flow) of the views in `ids`: per view the planes, pixel states
+    and confidence the next pass reads as priors (main.cpp:306-331)."""
+    import apd_abi as A
+    W, H = sc.width, sc.height
+    priors = {}
+    for r in ids:
+        arr = A.scene_problem(sc, r, [j for j, _ in sc.pairs[r]][:N], seed=0x5EED ^ r)
+        eng.set_problem(arr)
+        eng.run()
+        out = SimpleNamespace(planes=np.zeros((H, W, 4), np.float32), weak_info=np.zeros((H, W), np.uint8),
+                              confidence=np.zeros((H, W), np.uint8))
+        s = A.ApdOutputs()
+        s.planes = A._ptr(out.planes, A.C.c_float)
+        s.weak_info = A._ptr(out.weak_info, A.C.c_uint8)
+        s.confidence = A._ptr(out.confidence, A.C.c_uint8)
+        eng._check(eng.lib.apd_get_results(eng.ctx, A.C.byref(s)), "apd_get_results")
+        priors[r] = out
+    return priors
+
+
+def final_round_problem(sc, priors, ref, N):
+    """The REFINE_ITER + APD + geometric pass of main.cpp's last round (main.cpp:336-352, i = 3, j = 0)."""
+    import apd_abi as A
+    import cases
+    arr = cases.refine_problem(sc, priors, ref, N, state=A.REFINE_ITER, geom=True, apd=True)
+    arr.params.rotate_time = min(2 ** FINAL_ROUND, 4)
+    arr.params.ransac_threshold = 0.01 - FINAL_ROUND * 0.00125
+    arr.params.weak_peak_radius = max(4 - 2 * 0, 2)
+    arr.params.use_impetus = 1
+    return arr
+
+
+def timed_fresh_iterations(eng, arr, steps, warmup, barrier):
+    """Warm-up, then `steps` loop-body iterations taken in blocks of one fresh run's iterations
+    0..max_iterations-1; each block re-uploads and re-initialises the problem untimed, and is timed
+    between a barrier + device synchronisation on both sides. Returns (summed seconds, per-step ms)."""
+    iters = max(1, arr.params.max_iterations)
+    done = 0
+    while done < warmup:
+        eng.set_problem(arr)
+        eng.prepare()
+        n = min(iters, warmup - done)
+        for i in range(n):
+            eng.iteration(i)
+        done += n
+    eng.synchronize()
+    eng.profile_reset(True)
+    elapsed, step_ms, done = 0.0, [], 0
+    while done < steps:
+        eng.set_problem(arr)
+        eng.prepare()
+        eng.synchronize()
+        barrier()
+        t_block = time.perf_counter()
+        t_prev = t_block
+        n = min(iters, steps - done)
+        for i in range(n):
+            eng.iteration(i)
+            eng.synchronize()  # per-step times for the median (a few us against >=25 ms steps)
+            t = time.perf_counter()
+            step_ms.append((t - t_prev) * 1e3)
+            t_prev = t
+        elapsed += t_prev - t_block
+        barrier()
+        done += n
+    return elapsed, step_ms
+
+
+def kernel_stats(eng, kind):
+    ms, n, px = eng.profile_kernel(kind)
+    return {"ms_total": ms, "launches": n, "avg_ms": round(ms / n, 4) if n else None, "pixels": px}
+
+
+def weak_roofline(eng, steps, W, N):
+    """Roofline of the Weak sweep (k_weak_cand_vm + k_sweep_weak_vm) over the timed steps."""
+    import apd_abi as A
+    cnt = eng.profile_counters()
+    cand = kernel_stats(eng, A.PROF_WEAK_CAND)
+    sweep = kernel_stats(eng, A.PROF_WEAK_SWEEP)
+    strong = kernel_stats(eng, A.PROF_STRONG_SWEEP)
+    ransac = kernel_stats(eng, A.PROF_RANSAC_FIT)
+    ms = cand["ms_total"] + sweep["ms_total"]
+    flop = cnt[1] * FLOP_PER_NCC_NEW + cnt[2] * FLOP_PER_GEOM
+    achieved = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+    pmc = latest_pmc("k_sweep_weak_vm", W, N)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    return {
+        "bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+        "kernel": "k_sweep_weak_vm (+ k_weak_cand_vm): CheckerboardPropagationWeak, APD.cu:1442-1615",
+        "note": "VALU-FP32 gather/stencil kernels (no matrix work, SURVEY.md §8d); one Weak sweep "
+                "iteration = 1 k_weak_cand_vm + 2 k_sweep_weak_vm launches; flops = device-counted "
+                "NCC-New x 4038 + geometric terms x 80, over their summed HIP-event time; traffic = "
+                "HBM bytes per k_sweep_weak_vm launch (PMC, profiles/)",
+        "ms_per_iteration": round(ms / max(steps, 1), 3),
+        "flop_per_iteration": flop / max(steps, 1),
+        "ncc_new_per_iteration": round(cnt[1] / max(steps, 1)),
+        "geom_terms_per_iteration": round(cnt[2] / max(steps, 1)),
+        "launch_avg_ms": {"k_weak_cand_vm": cand["avg_ms"], "k_sweep_weak_vm": sweep["avg_ms"],
+                          "k_sweep_strong_vm": strong["avg_ms"], "k_ransac_fit": ransac["avg_ms"]},
+        "launches": {"k_weak_cand_vm": cand["launches"], "k_sweep_weak_vm": sweep["launches"],
+                     "k_sweep_strong_vm": strong["launches"], "k_ransac_fit": ransac["launches"]},
+        "pmc_file": pmc.get("_file") if pmc else None,
+    }
+
+
+def strong_roofline(eng, W, N):
+    """Roofline of the Strong sweep (k_sweep_strong_vm) over the profiled launches."""
+    import apd_abi as A
+    st = kernel_stats(eng, A.PROF_STRONG_SWEEP)
+    evals = eng.profile_counters()[0]
+    n = max(st["launches"], 1)
+    launch_ms = st["ms_total"] / n
+    flop = evals / n * FLOP_PER_NCC_OLD
+    achieved = flop / (launch_ms * 1e-3) / 1e12 if launch_ms > 0 else 0.0
+    pmc = latest_pmc("k_sweep_strong", W, N)
+    return {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+            "kernel": "k_sweep_strong_vm: CheckerboardPropagationStrong, APD.cu:1098-1440",
+            "launch_ms": round(launch_ms, 4), "launches": st["launches"], "flop_per_launch": flop,
+            "ncc_evals_per_launch": round(evals / n)}
+
+
+def gt_accuracy(sc, ref, eng, W, H, N):
+    import apd_abi as A
+    out = eng.results(A.Outputs(W, H, N))
+    gt = sc.gt_depth[ref]
+    d = out.planes[..., 3]
+    m = (gt > 0) & (out.weak_info != A.UNKNOWN)
+    rel = np.abs(d[m] - gt[m]) / gt[m]
+    return {"gt_median_rel_depth_err": round(float(np.median(rel)), 5),
+            "gt_frac_within_1pct": round(float((rel < 0.01).mean()), 4),
+            "weak_frac_out": round(float((out.weak_info == A.WEAK).mean()), 4)}
+
+
+def end_to_end(eng, arr, sc, ref, W, H, N):
+    """One full RunPatchMatch (the main.cpp:157-161 bracket), after an untimed one (first-use
+    allocations and code loading out of the way)."""
+    eng.set_problem(arr)
+    eng.run()
+    eng.set_problem(arr)
+    t1 = time.perf_counter()
+    eng.run()
+    t2 = time.perf_counter()
+    tm = eng.timing()
+    iters = tm.iterations
+    r = {"run_patchmatch_ms": round(tm.total_ms, 3), "host_wall_ms": round((t2 - t1) * 1e3, 3),
+         "mpix_s_end_to_end": round(W * H * iters / (tm.total_ms * 1e-3) / 1e6, 3),
+         "anchors_ms": round(tm.anchors_ms, 3), "init_ms": round(tm.init_ms, 3), "sweep_ms": round(tm.sweep_ms, 3),
+         "post_ms": round(tm.post_ms, 3), "iter_ms": [round(x, 3) for x in list(tm.iter_ms)[:iters]]}
+    r.update(gt_accuracy(sc, ref, eng, W, H, N))
+    return r
+
+
+def apd_pass_once(eng, sc, ref, N, label):
+    """Priors + one fresh timed pass (3 iterations) + end to end, for a secondary scene variant."""
+    W, H = sc.width, sc.height
+    ids = [ref] + [j for j, _ in sc.pairs[ref]][:N]
+    priors = first_init_priors(eng, sc, ids, N)
+    arr = final_round_problem(sc, priors, ref, N)
+    el, step_ms = timed_fresh_iterations(eng, arr, arr.params.max_iterations, 1, lambda: None)
+    roof = weak_roofline(eng, len(step_ms), W, N)
+    eng.profile_reset(False)
+    e2e = end_to_end(eng, arr, sc, ref, W, H, N)
+    return {"workload": label, "mpix_s_iter": round(W * H * len(step_ms) / el / 1e6, 3),
+            "iter_ms": [round(x, 2) for x in step_ms], "weak_frac": round(float((arr.weak_info == 0).mean()), 4),
+            "roofline_frac": roof["frac"], "roofline_achieved": roof["achieved"], "end_to_end": e2e}
+
+
+def c2_first_init(eng, steps, warmup):
+    """configs[1]: 3024x2016, N = 8, FIRST_INIT (geom off, APD off): Strong sweep B + R per step."""
+    import apd_abi as A
+    W, H, N = 3024, 2016, 8
+    sc = make_scene(W, H, N, 1, "smooth")
+    arr = A.scene_problem(sc, 0, [j for j, _ in sc.pairs[0]][:N], seed=0x5EED)
+    el, step_ms = timed_fresh_iterations(eng, arr, steps, warmup, lambda: None)
+    roof = strong_roofline(eng, W, N)
+    eng.profile_reset(False)
+    e2e = end_to_end(eng, arr, sc, 0, W, H, N)
+    return {"workload": "C2: ETH3D-office-shaped scan, half-res 3024x2016, 1 ref + 8 src views, FIRST_INIT "
+                        "(geom off, APD off), Strong sweep B + R per step, fresh runs",
+            "value": round(W * H * len(step_ms) / el / 1e6, 3), "unit": "Mpix/s", "steps": len(step_ms),
+            "ms_per_step": round(el / len(step_ms) * 1e3, 4),
+            "iter_ms_median": round(statistics.median(step_ms), 3), "roofline": roof, "end_to_end": e2e}
+
+
+def cpu_baseline(eng, texture, N, w, h, threads):
+    """The C oracle on one APD iteration of the headline pass, on the same scene rendered at w x h
+    (priors from FIRST_INIT runs on the device, which are bit-identical to the oracle's)."""
     import ctypes as C
+    import oracle_lib
+    sc = make_scene(w, h, N, 1, texture)
+    ids = [0] + [j for j, _ in sc.pairs[0]][:N]
+    priors = first_init_priors(eng, sc, ids, N)
+    arr = final_round_problem(sc, priors, 0, N)
+    lib = oracle_lib.load()
     pb = arr.build()
     times = (C.c_double * 3)()
     st = lib.oracle_time_iterations(C.byref(pb), 1, threads, times)
     if st != 0:
         return None
     t_iter = times[1]
-    return {"value": round(w * h / t_iter / 1e6, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
-            "sample": f"oracle (C restatement, OpenMP) on the same synthetic scene rendered at {w}x{h}, N={n_src}, "
-                      f"FIRST_INIT, one sweep iteration (t_iter={t_iter:.2f}s; prepare {times[0]:.2f}s untimed)"}
-
-
-def apd_pass(eng, sc, ref, N):
-    """One REFINE_ITER problem with APD (deformable NCC, focal weights, anchors) and geometric
-    consistency on -- what main.cpp runs in rounds >= 1 -- on the same scene, priors from FIRST_INIT
-    runs of every view (the data flow of round 0). Per-iteration Mpix/s as the headline metric
-    (loop body = Strong B+R, RANSAC fit, candidate costs, Weak B+R), median over the 3 iterations."""
-    import apd_abi as A
-    import cases
-    import statistics
-    W, H = sc.width, sc.height
-    priors = []
-    for r in range(len(sc.images)):
-        arr = A.scene_problem(sc, r, [j for j, _ in sc.pairs[r]][:N], seed=0x5EED ^ r)
-        eng.set_problem(arr)
-        eng.run()
-        priors.append(eng.results(A.Outputs(W, H, N)))
-    arr = cases.refine_problem(sc, priors, ref, N, state=A.REFINE_ITER, geom=True, apd=True)
-    eng.set_problem(arr)
-    eng.run()
-    tm = eng.timing()
-    iters = list(tm.iter_ms)[: tm.iterations]
-    return {"mpix_s_iter": round(W * H / (statistics.median(iters) * 1e-3) / 1e6, 3),
-            "iter_ms": [round(x, 2) for x in iters], "run_patchmatch_ms": round(tm.total_ms, 2),
-            "mpix_s_end_to_end": round(W * H * tm.iterations / (tm.total_ms * 1e-3) / 1e6, 3),
-            "anchors_ms": round(tm.anchors_ms, 2), "init_ms": round(tm.init_ms, 2), "sweep_ms": round(tm.sweep_ms, 2),
-            "post_ms": round(tm.post_ms, 2), "weak_frac": round(float((arr.weak_info == A.WEAK).mean()), 4)}
+    return {"value": round(w * h / t_iter / 1e6, 5), "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (C restatement{', OpenMP' if threads > 1 else ', 1 thread'}) on the headline "
+                      f"pass (REFINE_ITER, APD + focal + geom + impetus, final-round params) of the same "
+                      f"synthetic scan rendered at {w}x{h}, N={N}, one loop-body iteration "
+                      f"(t_iter={t_iter:.2f}s; anchors/RandomInit {times[0]:.2f}s untimed)"}
 
 
 def main():
@@ -122,15 +302,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--width", type=int, default=3024)
-    ap.add_argument("--height", type=int, default=2016)
-    ap.add_argument("--n-src", type=int, default=8)
+    ap.add_argument("--width", type=int, default=6048)
+    ap.add_argument("--height", type=int, default=4032)
+    ap.add_argument("--n-src", type=int, default=10)
+    ap.add_argument("--texture", default="smooth", choices=["smooth", "rich"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--end-to-end", type=int, default=1, help="also time one full RunPatchMatch (0/1)")
-    ap.add_argument("--apd-pass", type=int, default=1,
-                    help="also time one APD + geometric-consistency pass (REFINE_ITER, rounds >= 1) (0/1)")
+    ap.add_argument("--c2", type=int, default=1, help="also measure configs[1] (C2 FIRST_INIT) (0/1)")
+    ap.add_argument("--rich", type=int, default=1, help="also measure the texture-rich scene variant (0/1)")
     args = ap.parse_args()
+    t_start_all = time.time()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -147,30 +329,6 @@ def main():
         tdist.init_process_group(backend=backend)
         dist = (torch, tdist, backend)
 
-    import apd_abi as A
-    import synth
-
-    W, H, N = args.width, args.height, args.n_src
-    scene_args = dict(seed=20251114)
-    t0 = time.time()
-    sc = synth.make_scene(W, H, max(N, world), **scene_args)
-    t_scene = time.time() - t0
-    n_views = len(sc.images)
-    ref = rank % n_views
-    srcs = [j for j, _ in sc.pairs[ref]][:N]
-    arr = A.scene_problem(sc, ref, srcs, seed=0x5EED ^ ref)
-
-    lib = A.load_library()
-    device = local_rank % max(1, lib.apd_device_count())
-    eng = A.Engine(device, lib)
-    eng.set_problem(arr)
-    eng.prepare()
-    eng.synchronize()
-    iters = arr.params.max_iterations
-    for s in range(args.warmup):
-        eng.iteration(s % iters)
-    eng.synchronize()
-
     def barrier():
         if dist:
             torch, tdist, backend = dist
@@ -178,18 +336,29 @@ def main():
             if torch.cuda.is_available():
                 torch.cuda.synchronize()
 
-    eng.profile_reset(True)
-    barrier()
-    eng.synchronize()
-    t_start = time.perf_counter()
-    for s in range(args.steps):
-        eng.iteration(s % iters)
-    eng.synchronize()
-    t_end = time.perf_counter()
-    barrier()
-    elapsed = t_end - t_start
-    sweep_ms, launches, sweep_px = eng.profile_query()
-    ncc_evals = eng.profile_evaluations()
+    import apd_abi as A
+
+    W, H, N = args.width, args.height, args.n_src
+    t0 = time.time()
+    sc = make_scene(W, H, N, world, args.texture)
+    t_scene = time.time() - t0
+    n_views = len(sc.images)
+    ref = rank % n_views
+    ids = [ref] + [j for j, _ in sc.pairs[ref]][:N]
+
+    lib = A.load_library()
+    device = local_rank % max(1, lib.apd_device_count())
+    eng = A.Engine(device, lib)
+    t0 = time.time()
+    priors = first_init_priors(eng, sc, ids, N)
+    t_priors = time.time() - t0
+    arr = final_round_problem(sc, priors, ref, N)
+    del priors
+    weak_frac = float((arr.weak_info == A.WEAK).mean())
+
+    elapsed, step_ms = timed_fresh_iterations(eng, arr, args.steps, args.warmup, barrier)
+    roof = weak_roofline(eng, args.steps, W, N)
+    roof_strong_apd = strong_roofline(eng, W, N)
     eng.profile_reset(False)
     if dist:
         torch, tdist, backend = dist
@@ -201,41 +370,23 @@ def main():
     n_gpus = world if dist else 1
     value = n_gpus * W * H * args.steps / elapsed / 1e6
 
-    # dominant kernel roofline (k_sweep_strong): flops of the NCC-Old evaluations the launches actually
-    # issued (counted on the device), per launch; the static upper bound is kept beside it
-    hh = H // 2
-    row_limit = min(H, 32 * ((hh + 15) // 16))
-    evals_bound = strong_evaluations(W, H, N, 0, row_limit) + strong_evaluations(W, H, N, 1, row_limit)
-    flop_per_launch = ncc_evals / max(launches, 1) * FLOP_PER_NCC_OLD
-    launch_ms = sweep_ms / max(launches, 1)
-    achieved_tf = flop_per_launch / (launch_ms * 1e-3) / 1e12
-    bytes_per_launch = (W * H / 2) * (4 * (N + 1) + 80)  # = 116 B/px at N=8
-    pmc = latest_pmc("k_sweep_strong", W, N)
-    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-
     line = None
     if rank == 0:
-        e2e = None
-        if args.end_to_end:
-            eng.set_problem(arr)
-            t1 = time.perf_counter()
-            eng.run()
-            t2 = time.perf_counter()
-            tm = eng.timing()
-            out = eng.results(A.Outputs(W, H, N))
-            gt = sc.gt_depth[ref]
-            d = out.planes[..., 3]
-            m = (gt > 0) & (out.weak_info != A.UNKNOWN)
-            rel = np.abs(d[m] - gt[m]) / gt[m]
-            e2e = {"run_patchmatch_ms": round(tm.total_ms, 3), "host_wall_ms": round((t2 - t1) * 1e3, 3),
-                   "mpix_s_end_to_end": round(W * H * iters / (tm.total_ms * 1e-3) / 1e6, 3),
-                   "init_ms": round(tm.init_ms, 3), "sweep_ms": round(tm.sweep_ms, 3),
-                   "post_ms": round(tm.post_ms, 3),
-                   "iter_ms": [round(x, 3) for x in list(tm.iter_ms)[:iters]],
-                   "gt_median_rel_depth_err": round(float(np.median(rel)), 5),
-                   "gt_frac_within_1pct": round(float((rel < 0.01).mean()), 4)}
-        apd = apd_pass(eng, sc, ref, N) if args.apd_pass else None
-        cpu = None if args.no_cpu_baseline else cpu_baseline(scene_args, N, args.cpu_threads)
+        e2e = end_to_end(eng, arr, sc, ref, W, H, N) if args.end_to_end else None
+        del arr, sc
+        single = n_gpus == 1
+        c2 = c2_first_init(eng, 6, 2) if (args.c2 and single) else None
+        rich = None
+        if args.rich and single and args.texture != "rich":
+            rsc = make_scene(W, H, N, 1, "rich")
+            rich = apd_pass_once(eng, rsc, 0, N, f"{workload_name(W, H, N, True)} pass on the texture-rich "
+                                                  f"scene variant (synth texture='rich')")
+            del rsc
+        cpu = cpu1 = None
+        if not args.no_cpu_baseline and single:
+            cpu = cpu_baseline(eng, args.texture, N, 756, 504, args.cpu_threads)
+            cpu1 = cpu_baseline(eng, args.texture, N, 378, 252, 1)
+        name = workload_name(W, H, N, True)
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -248,26 +399,28 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded piecewise-planar scan, apde-mvs_amd/synth.py; no ETH3D data offline)",
-            "config": {"workload": "C2: ETH3D-office-shaped scan, half-res 3024x2016, 1 ref + 8 src views, "
-                                   "FIRST_INIT sweep iteration (geom off, APD off), one ref view per GPU",
-                       "width": W, "height": H, "n_src": N, "global_batch": n_gpus, "parallelism": f"views{n_gpus}"},
-            "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4),
-                         "traffic": traffic,
-                         "kernel": "k_sweep_strong",
-                         "note": "VALU-FP32 gather/stencil kernel (no matrix work): priced against the FP32 "
-                                 "peak, which on gfx950 is the same 157.3 TF for VALU and f32 MFMA",
-                         "launch_ms": round(launch_ms, 4), "launches": launches,
-                         "flop_per_launch": flop_per_launch,
-                         "ncc_evals_per_launch": round(ncc_evals / max(launches, 1)),
-                         "ncc_evals_bound_per_launch": evals_bound // 2,
-                         "hbm_algorithmic_gbs": round(bytes_per_launch / (launch_ms * 1e-3) / 1e9, 2),
-                         "hbm_peak_gbs": PEAK_HBM_GBS},
+            "data": f"synthetic (seeded piecewise-planar scan, apde-mvs_amd/synth.py, texture={args.texture}; "
+                    f"no ETH3D data offline)",
+            "config": {"workload": f"{name}: ETH3D-office-shaped scan, full-res {W}x{H}, 1 ref + {N} src views, "
+                                   f"final-round REFINE_ITER pass (deformable PM + focal-weighted anchors + geom "
+                                   f"consistency + impetus, rotate_time {arr_rt()}, priors from FIRST_INIT runs); "
+                                   f"step = loop body APD.cu:2699-2708 (Strong B+R, RANSAC fit, Weak B+R) of "
+                                   f"fresh runs; one ref view per GPU",
+                       "width": W, "height": H, "n_src": N, "texture": args.texture,
+                       "weak_frac": round(weak_frac, 4), "global_batch": n_gpus,
+                       "parallelism": f"views{n_gpus}"},
+            "iter_ms_median": round(statistics.median(step_ms), 3),
+            "iter_ms": [round(x, 2) for x in step_ms],
+            "roofline": roof,
+            "roofline_strong_sweep": roof_strong_apd,
             "cpu_baseline": cpu,
+            "cpu_baseline_1core": cpu1,
             "end_to_end": e2e,
-            "apd_pass": apd,
+            "c2_first_init": c2,
+            "rich_texture": rich,
             "scene_gen_s": round(t_scene, 2),
+            "priors_s": round(t_priors, 2),
+            "bench_wall_s": round(time.time() - t_start_all, 1),
         }
     eng.close()
     if dist:
@@ -276,6 +429,10 @@ def main():
         tdist.destroy_process_group()
     if line is not None:
         print(json.dumps(line), flush=True)
+
+
+def arr_rt():
+    return min(2 ** FINAL_ROUND, 4)
 
 
 if __name__ == "__main__":

@@ -189,15 +189,32 @@ int32_t apd_get_results(apd_ctx *ctx, const apd_outputs *out);
 /* Device timing of the last apd_run_patchmatch. */
 int32_t apd_get_timing(apd_ctx *ctx, apd_timing *timing);
 
-/* Average duration (ms) of the dominant kernel (the Strong checkerboard sweep) over the launches
-   since the last reset, measured with HIP events on the ctx stream; and the algorithmic NCC
-   sample count those launches processed. Used by bench.py for roofline.achieved. */
+/* Profiling of the loop-body kernels (APD.cu:2699-2708), used by bench.py for roofline.achieved.
+   apd_profile_reset(ctx, 1) clears and enables it: every later launch of the kinds below is
+   bracketed by HIP events on the ctx stream, and the device counters below are accumulated.
+   apd_profile_kernel: total duration (ms), launch count and pixels covered by the launches of one
+   kind since the reset. apd_profile_query == apd_profile_kernel(APD_PROF_STRONG_SWEEP). */
+#define APD_PROF_STRONG_SWEEP 0 /* k_sweep_strong_vm (CheckerboardPropagationStrong, APD.cu:1098-1440) */
+#define APD_PROF_RANSAC_FIT 1   /* k_ransac_fit (RANSACToGetFitPlane, APD.cu:2486-2598)             */
+#define APD_PROF_WEAK_CAND 2    /* k_weak_cand_vm (anchor-candidate NCC-New of the Weak sweep)       */
+#define APD_PROF_WEAK_SWEEP 3   /* k_sweep_weak_vm (CheckerboardPropagationWeak, APD.cu:1442-1615)   */
 int32_t apd_profile_reset(apd_ctx *ctx, int32_t enable);
+int32_t apd_profile_kernel(apd_ctx *ctx, int32_t kind, double *ms_total, int64_t *launches,
+                           int64_t *pixels);
 int32_t apd_profile_query(apd_ctx *ctx, double *sweep_ms_total, int64_t *sweep_launches,
                           int64_t *sweep_pixels);
-/* NCC-Old evaluations the profiled Strong sweep launches actually issued (counted on the device:
-   valid propagation candidates + current plane + refinement candidates of views with weight > 0),
-   so bench.py prices roofline.achieved on work done, not on an upper bound. */
+/* Device counters since the reset, so bench.py prices roofline.achieved on work done, not on an
+   upper bound. counts[0..n-1] (n <= APD_PROF_COUNTERS; extra entries are zeroed):
+   [0] NCC-Old evaluations the Strong sweep launches issued (valid propagation candidates + current
+       plane + refinement candidates of views with weight > 0);
+   [1] NCC-New evaluations of the Weak sweep whose values CheckerboardPropagationWeak uses: valid
+       anchor candidates x N + current plane x N + (fit plane + 5 refinement candidates) x views
+       with weight > 0 when the fit plane exists -- however the engine obtained them (shared anchor
+       windows in k_weak_cand_vm, RandomInitialization's kept costs, or the sweep itself);
+   [2] geometric-consistency terms of the same Weak sweep (APD.cu:1561, 1583, 1037, 1079).
+   apd_profile_evaluations(ctx, &n) == apd_profile_counters(ctx, &n, 1). */
+#define APD_PROF_COUNTERS 4
+int32_t apd_profile_counters(apd_ctx *ctx, int64_t *counts, int32_t n);
 int32_t apd_profile_evaluations(apd_ctx *ctx, int64_t *ncc_evaluations);
 
 /* Host epilogue of ProcessProblem (main.cpp:168-178): depth = plane.w clipped to

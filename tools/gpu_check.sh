@@ -14,6 +14,6 @@ fi
 if [ "$WHAT" = bench ] || [ "$WHAT" = all ]; then
   timeout -k 10 600 python3 -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
   cd /tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --end-to-end 0 --steps 20 > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof_bench.err"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --end-to-end 0 --c2 0 --rich 0 --steps 6 --warmup 1 > "$GRAFT_REPO_ROOT/$OUT/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof_bench.err"
 fi
 echo ok
