@@ -153,7 +153,7 @@ def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=Tru
     """texture="smooth": band-limited textures fixed in world units, so they get smoother per pixel
     as the resolution grows (90-94 % of the pixels end WEAK at 3024x2016 and 6048x4032).
     texture="rich": the same scene plus a fine detail octave of `detail_period_px` pixels at the
-    reference view, and three more textureless patches: a resolution-independent, texture-rich
+    reference view, and two more textureless patches: a resolution-independent, texture-rich
     variant whose WEAK fraction is set by the textureless area."""
     if texture not in TEXTURES:
         raise ValueError(f"texture must be one of {TEXTURES}")
@@ -176,8 +176,7 @@ def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=Tru
     flat = [(0.68 * half_w, 0.25 * half_h, 1.2 * half_w, 1.1 * half_h, 128.0)] if weak_patches else []
     floor_flat = []
     if rich and weak_patches:
-        flat += [(1.45 * half_w, 0.1 * half_h, 2.0 * half_w, 1.5 * half_h, 112.0),
-                 (0.05 * half_w, 1.25 * half_h, 0.9 * half_w, 1.9 * half_h, 150.0)]
+        flat += [(1.45 * half_w, 0.1 * half_h, 2.0 * half_w, 1.5 * half_h, 112.0)]
         floor_flat = [(0.2 * half_w, 0.0, 1.1 * half_w, 0.35 * depth, 96.0)]
     quads.append(_Quad([-half_w, -half_h, depth], [2 * half_w, 0, 0.35 * depth], [0, 2 * half_h, 0],
                        _Texture(rng, base_freq=4.0, flat_patches=flat, detail=detail())))  # slanted back wall

@@ -14,9 +14,15 @@
  *
  * Semantic contract shared bit-for-bit with the HIP kernels (written twice, independently):
  *  - fp32 everywhere the reference uses fp32; double exactly where the reference promotes to double
- *    (0.8 x expf, 0.25 x and 0.75 x, cost - 0.1). Both sides compile with -ffp-contract=off; fused multiply-adds
- *    appear only as explicit fmaf() at the accumulation sites nvcc --fmad=true contracts in the
- *    reference (NCC moments, weighted view sums, CDF).
+ *    (0.8 x expf, 0.25 x and 0.75 x, cost - 0.1). Both sides compile with -ffp-contract=off; fused
+ *    multiply-adds appear only as explicit fmaf() at a FIXED set of sites: the NCC moments and
+ *    variances, the weighted view sums, the CDF, the homography projection. nvcc --fmad=true (the
+ *    reference's default) may contract every other a*b+c as well -- e.g. the anchor position
+ *    point.x + direction.x * radius (APD.cu:1925), restated here as a separate multiply and add --
+ *    and which sites it contracts is the compiler's choice, not the source's. This contract is
+ *    therefore one fixed, documented rounding of the reference's arithmetic: the HIP kernels equal
+ *    it bit for bit, and agreement with a real CUDA build of the reference can only be statistical
+ *    (within rounding), never bitwise.
  *  - Division and sqrt are IEEE correctly rounded. rsqrtf(x) is restated as 1.0f/sqrtf(x).
  *    exp/sin/cos are the deterministic polynomials o_expf/o_sinf/o_cosf below.
  *  - Homography: H = A - b*(n^T Kr^-1)/w with A = Ks*R_rel*Kr^-1, b = Ks*t_rel precomputed per source
@@ -1191,6 +1197,31 @@ static void k_filter(octx *o, int px, int py) {
     o->plane[c].w = (n % 2 == 0) ? (f[m - 1] + f[m]) / 2 : f[m];
 }
 
+/* DepthToWeak's classification of a 61-sample cost curve (disparities -30..30), APD.cu:2200-2249:
+   local minima ("peaks") at samples 2..58; WEAK unless the lowest one lies within weak_peak_radius of
+   the centre and costs <= 0.5; then a single peak is STRONG iff it costs <= 0.15, several are STRONG
+   iff the other peaks' cost spread sqrt(sum (c_i - c_min)^2) / (count - 1) exceeds 0.2. */
+static int o_classify_curve(const float *pc, int weak_peak_radius) {
+    int is_peak[61] = {0};
+    int count = 0, min_peak = 0;
+    float min_cost = 2.0f;
+    for (int i = 2; i < 59; ++i) {
+        if (pc[i - 1] > pc[i] && pc[i + 1] > pc[i]) {
+            is_peak[i] = 1; count++;
+            if (pc[i] < min_cost) { min_peak = i; min_cost = pc[i]; }
+        }
+    }
+    if (abs(min_peak - 30) > weak_peak_radius || pc[min_peak] > 0.5f) return WEAK;
+    if (count == 1) return (pc[min_peak] <= 0.15f) ? STRONG : WEAK;
+    float var = 0.0f;
+    for (int i = 2; i < 59; ++i) {
+        if (is_peak[i] && i != min_peak) { float d = pc[i] - min_cost; var = fmaf(d, d, var); }
+    }
+    var = sqrtf(var);
+    var /= (float)(count - 1);
+    return (var > 0.2f) ? STRONG : WEAK;
+}
+
 /* DepthToWeak, APD.cu:2103-2250 */
 static void k_depth_to_weak(octx *o, int px, int py) {
     const int W = o->W, H = o->H, c = px + py * W, N = o->N;
@@ -1233,24 +1264,7 @@ static void k_depth_to_weak(octx *o, int px, int py) {
         pc[pd + 30] = CV_MIN(2.0f, p);
     }
     if (o->curve) memcpy(&o->curve[(size_t)c * 61], pc, sizeof(pc));
-    int is_peak[61] = {0};
-    int count = 0, min_peak = 0;
-    float min_cost = 2.0f;
-    for (int i = 2; i < 59; ++i) {
-        if (pc[i - 1] > pc[i] && pc[i + 1] > pc[i]) {
-            is_peak[i] = 1; count++;
-            if (pc[i] < min_cost) { min_peak = i; min_cost = pc[i]; }
-        }
-    }
-    if (abs(min_peak - 30) > o->P.weak_peak_radius || pc[min_peak] > 0.5f) { o->weak[c] = WEAK; return; }
-    if (count == 1) { o->weak[c] = (pc[min_peak] <= 0.15f) ? STRONG : WEAK; return; }
-    float var = 0.0f;
-    for (int i = 2; i < 59; ++i) {
-        if (is_peak[i] && i != min_peak) { float d = pc[i] - min_cost; var = fmaf(d, d, var); }
-    }
-    var = sqrtf(var);
-    var /= (float)(count - 1);
-    o->weak[c] = (var > 0.2f) ? STRONG : WEAK;
+    o->weak[c] = (uint8_t)o_classify_curve(pc, o->P.weak_peak_radius);
 }
 
 /* ConfidenceCompute, APD.cu:2282-2344 */
@@ -1538,3 +1552,84 @@ float oracle_expf(float x) { return o_expf(x); }
 float oracle_sinf(float x) { return o_sinf(x); }
 float oracle_cosf(float x) { return o_cosf(x); }
 void oracle_philox(uint32_t *c4, uint32_t k0, uint32_t k1) { o_philox(c4, k0, k1); }
+
+/* DepthToWeak's curve classification alone (APD.cu:2200-2249). */
+int oracle_classify_curve(const float *pc61, int weak_peak_radius) { return o_classify_curve(pc61, weak_peak_radius); }
+
+/* ComputeBilateralNCCNew (APD.cu:448-593) of one (pixel, source, plane) with caller-given anchors
+   (9 x (x, y), anchor 0 first) and selected-view bitmasks (H*W); the problem must have use_APD set
+   and the pixel WEAK in its weak_info. Returns -1 on a bad context. */
+float oracle_ncc_new(const apd_problem *pb, int px, int py, int src, const float *plane4, const int16_t *anchors9,
+                     const uint32_t *sel) {
+    octx *o = (octx *)malloc(sizeof(octx));
+    float r = -1.0f;
+    if (kat_ctx(o, pb) == APD_OK && o->amap[px + py * o->W] >= 0) {
+        memcpy(&o->anchors[2 * (o->amap[px + py * o->W] * ANCHOR_NUM)], anchors9, ANCHOR_NUM * 2 * sizeof(int16_t));
+        if (sel) memcpy(o->sel, sel, (size_t)o->HW * sizeof(uint32_t));
+        f4 p = {plane4[0], plane4[1], plane4[2], plane4[3]};
+        r = o_ncc_new(o, px, py, src, p);
+    }
+    ctx_free(o); free(o);
+    return r;
+}
+
+/* One stage of the post-processing / anchor preparation over the whole image on caller state, for
+   the known-answer tests (tests/test_oracle_kat_apd.py). In/out arrays are H*W (planes: 4 floats per
+   pixel, (world normal, depth) for stages 0/1 as after GetDepthandNormal):
+     stage 0  CheckerboardFilterStrong, black then red non-WEAK pixels (APD.cu:1711-1855): planes
+              (in/out), costs (in), weak (in);
+     stage 1  ConfidenceCompute (APD.cu:2282-2344): planes (in), sel (in), pb->depths (in), conf
+              (out), weak (in/out: UNKNOWN where depth <= 0);
+     stage 2  FindNearestStrongPoint (APD.cu:2434-2484): weak, conf (in) -> nearest (out, x, y);
+     stage 3  FindNearestStrongPoint + GenAnchors (APD.cu:1857-2082) + NeigbourUpdate
+              (APD.cu:2084-2100): planes (in, as during the sweep), weak (in/out), conf (in) ->
+              anchors (out, weak_count x 9 x (x, y), row-major WEAK order of the input), reliable (out).
+   Returns APD_OK or a negative status. */
+int oracle_kat_stage(const apd_problem *pb, int stage, const uint32_t *sel, const float *costs, float *planes,
+                     uint8_t *weak, uint8_t *conf, int16_t *nearest, int16_t *anchors, uint8_t *reliable) {
+    octx *o = (octx *)malloc(sizeof(octx));
+    if (!o) return APD_ENOMEM;
+    int st = kat_ctx(o, pb);
+    if (st != APD_OK) { ctx_free(o); free(o); return st; }
+    const size_t HW = (size_t)o->HW;
+    if (planes) memcpy(o->plane, planes, HW * sizeof(f4));
+    if (costs) memcpy(o->cost, costs, HW * sizeof(float));
+    if (sel) memcpy(o->sel, sel, HW * sizeof(uint32_t));
+    if (weak) memcpy(o->weak, weak, HW);
+    if (conf) memcpy(o->conf, conf, HW);
+    switch (stage) {
+    case 0:
+        FOR_COLOUR(o, 0, if (o->weak[py * o->W + px] != WEAK) k_filter(o, px, py));
+        FOR_COLOUR(o, 1, if (o->weak[py * o->W + px] != WEAK) k_filter(o, px, py));
+        break;
+    case 1:
+        FOR_ALL(o, k_confidence(o, px, py));
+        break;
+    case 2:
+        FOR_ALL(o, k_find_nearest(o, px, py));
+        break;
+    case 3: {
+        FOR_ALL(o, k_find_nearest(o, px, py));
+        anchor_consts K = make_anchor_consts(o->P.rotate_time);
+        FOR_ALL(o, k_gen_anchors(o, px, py, K));
+        FOR_ALL(o, {
+            int c = py * o->W + px;
+            if (o->weak[c] == WEAK && o->reliable[c] != 1) o->weak[c] = UNKNOWN;
+        });
+        break;
+    }
+    default:
+        st = APD_EINVAL;
+    }
+    if (st == APD_OK) {
+        if (planes) memcpy(planes, o->plane, HW * sizeof(f4));
+        if (weak) memcpy(weak, o->weak, HW);
+        if (conf) memcpy(conf, o->conf, HW);
+        if (nearest) memcpy(nearest, o->nearest, HW * 2 * sizeof(int16_t));
+        if (anchors && o->weak_count > 0) memcpy(anchors, o->anchors, (size_t)o->weak_count * ANCHOR_NUM * 2 * sizeof(int16_t));
+        if (reliable) memcpy(reliable, o->reliable, HW);
+    }
+    ctx_free(o);
+    free(o);
+    return st;
+}

@@ -16,8 +16,8 @@ import synth
 
 
 @functools.lru_cache(maxsize=None)
-def scene(w=160, h=120, n_src=4, seed=20251114, weak=True):
-    return synth.make_scene(w, h, n_src, seed=seed, weak_patches=weak)
+def scene(w=160, h=120, n_src=4, seed=20251114, weak=True, texture="smooth"):
+    return synth.make_scene(w, h, n_src, seed=seed, weak_patches=weak, texture=texture)
 
 
 def base_problem(sc, ref=0, n_src=None, **params):
@@ -101,13 +101,20 @@ CASES = {
     "refine_iter_geom_sa0": (128, 96, 4, "geom_sa0"),   # ... and in DepthToWeak / LocalRefine
     "refine_iter_apd_geom_sa0": (96, 72, 4, "apd_geom_sa0"),
     "refine_iter_apd_geom_rt4": (112, 84, 4, "apd_geom_rt4"),  # rotate_time 4 (rounds >= 2): 32 anchor slots
+    # TaT_a / TaT_i datasets: geom_factor 0.05 (main.cpp:293-299), N = 10 as config C4, final round
+    "refine_iter_tat_n10_apd_geom": (120, 66, 10, "apd_geom_tat"),
+    "refine_init_tat_n10_geom": (120, 66, 10, "geom_tat_init"),
+    # texture-rich scene variant (synth texture="rich"): fine detail, 30-50 % WEAK
+    "first_n6_rich": (128, 96, 6, "first_rich"),
+    "refine_iter_apd_geom_rich": (128, 96, 6, "apd_geom_rich"),
 }
 
 
 def make_case(name, oracle_run):
     w, h, n, kind = CASES[name]
-    sc = scene(w, h, max(n, 4))
-    if kind == "first":
+    rich = kind.endswith("_rich")
+    sc = scene(w, h, max(n, 4), texture="rich" if rich else "smooth")
+    if kind in ("first", "first_rich"):
         return base_problem(sc, 0, n)
     if kind == "first_sa0":
         arr = base_problem(sc, 0, n)
@@ -127,8 +134,13 @@ def make_case(name, oracle_run):
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, sa="zero_band")
     if kind == "apd_geom_rt4":
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, rotate_time=4)
-    if kind == "apd_geom":
+    if kind in ("apd_geom", "apd_geom_rich"):
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True)
+    if kind == "apd_geom_tat":  # main.cpp round 3, geometric pass j = 1 of a TaT scan
+        return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, geom_factor=0.05,
+                              rotate_time=4, ransac_threshold=0.01 - 3 * 0.00125, weak_peak_radius=2)
+    if kind == "geom_tat_init":  # REFINE_INIT with geometric consistency (the `apd` binary's 2-round path)
+        return refine_problem(sc, priors, 0, n, state=A.REFINE_INIT, geom=True, geom_factor=0.05)
     raise KeyError(kind)
 
 

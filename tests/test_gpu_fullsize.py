@@ -121,3 +121,131 @@ def test_fullsize_apd_pass_properties(engine, engine_tw16, full_scene):
     assert_same(a, run(engine, arr), "repeat APD run")
     assert_same(a, run(engine_tw16, arr), "16-wide list tiles (APD)")
     assert_same(a, run(engine, arr, f32=True), "fp32 quad texels (APD)")
+
+
+# ---- configs C4 and C3 at their real shapes (BASELINE.json configs[3] / configs[2])
+
+def slim_priors(eng, sc, n, ids):
+    """FIRST_INIT outputs of the views in `ids` (planes, pixel states, confidence only: at 6048x4032
+    a full Outputs per view would hold ~0.9 GB)."""
+    out = [None] * len(sc.images)
+    for r in ids:
+        eng.set_problem(cases.base_problem(sc, r, n))
+        eng.run()
+        o = A.Outputs.__new__(A.Outputs)
+        o.planes = np.zeros((sc.height, sc.width, 4), np.float32)
+        o.weak_info = np.zeros((sc.height, sc.width), np.uint8)
+        o.confidence = np.zeros((sc.height, sc.width), np.uint8)
+        s = A.ApdOutputs()
+        s.planes = A._ptr(o.planes, A.C.c_float)
+        s.weak_info = A._ptr(o.weak_info, A.C.c_uint8)
+        s.confidence = A._ptr(o.confidence, A.C.c_uint8)
+        eng._check(eng.lib.apd_get_results(eng.ctx, A.C.byref(s)), "apd_get_results")
+        out[r] = o
+    return out
+
+
+SLIM = ("planes", "costs", "weak_info", "confidence", "selected_views")
+
+
+def run_slim(eng, arr):
+    eng.set_problem(arr)
+    eng.run()
+    o = A.Outputs.__new__(A.Outputs)
+    o.planes = np.zeros((arr.height, arr.width, 4), np.float32)
+    o.costs = np.zeros((arr.height, arr.width), np.float32)
+    o.weak_info = np.zeros((arr.height, arr.width), np.uint8)
+    o.confidence = np.zeros((arr.height, arr.width), np.uint8)
+    o.selected_views = np.zeros((arr.height, arr.width), np.uint32)
+    o.weak_count = np.zeros(1, np.int32)
+    s = A.ApdOutputs()
+    for f, t in (("planes", A.C.c_float), ("costs", A.C.c_float), ("weak_info", A.C.c_uint8),
+                 ("confidence", A.C.c_uint8), ("selected_views", A.C.c_uint32), ("weak_count", A.C.c_int32)):
+        setattr(s, f, A._ptr(getattr(o, f), t))
+    eng._check(eng.lib.apd_get_results(eng.ctx, A.C.byref(s)), "apd_get_results")
+    return o
+
+
+def assert_same_slim(a, b, what):
+    d = cases.compare(a, b, SLIM)
+    assert not any(d.values()), f"{what}: differing elements {d}"
+
+
+def gt_floor(sc, out, ref=0, median=2e-3, within=0.6):
+    gt = sc.gt_depth[ref]
+    d = out.planes[..., 3]
+    m = (gt > 0) & (out.weak_info != A.UNKNOWN)
+    rel = np.abs(d[m] - gt[m]) / gt[m]
+    assert m.mean() > 0.5
+    assert float(np.median(rel)) < median, float(np.median(rel))
+    assert float((rel < 0.01).mean()) > within, float((rel < 0.01).mean())
+
+
+def tat_final_pass(sc, priors, n):
+    """main.cpp's last geometric pass of a TaT scan (geom_factor 0.05, main.cpp:293-299)."""
+    return cases.refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, geom_factor=0.05,
+                                rotate_time=4, ransac_threshold=0.01 - 2 * 0.00125, weak_peak_radius=4)
+
+
+def test_c4_quarter_tat_bit_exact(engine):
+    """C4's scene at a quarter of its size (480x264, N = 10, TaT geom_factor 0.05), final-round APD +
+    geom pass, bit-exact against the oracle."""
+    sc = synth.make_scene(480, 264, 10, seed=20251114)
+    priors = slim_priors(engine, sc, 10, range(len(sc.images)))
+    arr = tat_final_pass(sc, priors, 10)
+    assert (arr.weak_info == A.WEAK).any()
+    ref = oracle_lib.run(oracle_lib.load(), arr, 16)
+    got = run(engine, arr)
+    assert_same(ref, got, "480x264 N=10 TaT APD + geom")
+
+
+def test_c4_fullsize_tat_properties(engine, engine_tw16):
+    """Config C4 (T&T Family shape, 1920x1056, N = 10, TaT geom_factor 0.05): the FIRST_INIT pass and
+    the final-round APD + geometric pass; repeat-run identity, list-tile independence, fp32 texels,
+    ground-truth floors."""
+    sc = synth.make_scene(1920, 1056, 10, seed=20251114)
+    first = cases.base_problem(sc, 0, 10)
+    f = run_slim(engine, first)
+    assert_same_slim(f, run_slim(engine_tw16, first), "C4 FIRST_INIT, 16-wide list tiles")
+    gt_floor(sc, f)
+    priors = slim_priors(engine, sc, 10, range(len(sc.images)))
+    arr = tat_final_pass(sc, priors, 10)
+    a = run_slim(engine, arr)
+    assert int(a.weak_count[0]) > 0
+    assert_same_slim(a, run_slim(engine, arr), "C4 repeat APD run")
+    assert_same_slim(a, run_slim(engine_tw16, arr), "C4 16-wide list tiles (APD)")
+    os.environ["APD_TEX_F32"] = "1"
+    try:
+        b = run_slim(engine, arr)
+    finally:
+        os.environ.pop("APD_TEX_F32", None)
+    assert_same_slim(a, b, "C4 fp32 quad texels (APD)")
+    assert np.isfinite(a.planes[..., 3]).all()
+    gt_floor(sc, a)
+
+
+def test_c3_fullsize_apd_properties(engine, engine_tw16):
+    """Config C3 at its real shape (6048x4032, N = 10), the final-round APD + focal + geometric
+    REFINE_ITER pass (the bench's headline problem): repeat-run identity, list-tile independence,
+    the DepthToWeak -> LocalRefine hand-over (21.5 GB, > 2^31 elements) == LocalRefine evaluating
+    every sample itself (APD_NO_LR_HANDOVER=1), finite depths, ground-truth floors."""
+    sc = synth.make_scene(6048, 4032, 10, seed=20251114)
+    priors = slim_priors(engine, sc, 10, range(len(sc.images)))
+    arr = cases.refine_problem(sc, priors, 0, 10, state=A.REFINE_ITER, geom=True, apd=True, rotate_time=4,
+                               ransac_threshold=0.01 - 3 * 0.00125, weak_peak_radius=4)
+    del priors
+    a = run_slim(engine, arr)
+    assert int(a.weak_count[0]) > 0
+    assert_same_slim(a, run_slim(engine, arr), "C3 repeat run")
+    assert_same_slim(a, run_slim(engine_tw16, arr), "C3 16-wide list tiles")
+    os.environ["APD_NO_LR_HANDOVER"] = "1"
+    try:
+        eng = A.Engine(0, engine.lib)
+    finally:
+        os.environ.pop("APD_NO_LR_HANDOVER", None)
+    try:
+        assert_same_slim(a, run_slim(eng, arr), "C3 LocalRefine without the hand-over")
+    finally:
+        eng.close()
+    assert np.isfinite(a.planes[..., 3]).all()
+    gt_floor(sc, a)
