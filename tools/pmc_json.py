@@ -1,23 +1,35 @@
-"""Write profiles/<name>.json from a tools/pmc_profile.sh directory: per-launch mean counters of the
-Strong sweep kernel and the HBM traffic estimate bench.py reports as roofline.traffic.
-    python tools/pmc_json.py gpurun_out/pmcNN profiles/r1_pmc_sweep_strong.json [kernel_stats.csv]
+"""Write profiles/<name>.json from a tools/pmc_profile.sh / tools/pmc_c3.sh directory: per-launch mean
+counters of one kernel and the HBM traffic estimate bench.py reports as roofline.traffic.
+    python tools/pmc_json.py <pmc dir> <out.json> [--kernel k_sweep_strong] [--width 3024 --height 2016
+                             --n-src 8] [--stats kernel_stats.csv] [--source "..."]
 HBM bytes per launch = 2 x FETCH_SIZE (gfx950 reports half of wide reads, MI355X_MICROARCH.md §HBM)
 + WRITE_SIZE, both in KiB from rocprofv3; the per-width calibration of narrow gathers is open."""
-import csv, glob, json, os, sys, collections
-src, dst = sys.argv[1], sys.argv[2]
+import argparse, csv, glob, json, os, collections
+ap = argparse.ArgumentParser()
+ap.add_argument("src")
+ap.add_argument("dst")
+ap.add_argument("--kernel", default="k_sweep_strong")
+ap.add_argument("--width", type=int, default=3024)
+ap.add_argument("--height", type=int, default=2016)
+ap.add_argument("--n-src", type=int, default=8)
+ap.add_argument("--stats")
+ap.add_argument("--source", default="rocprofv3 --pmc, one pass per counter group (tools/pmc_profile.sh), "
+                                    "bench.py --steps 2 --warmup 1")
+a = ap.parse_args()
 d = collections.defaultdict(list)
 name = None
-for f in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True):
+for f in glob.glob(os.path.join(a.src, "**", "*counter_collection.csv"), recursive=True):
     per = collections.defaultdict(float)
     for r in csv.DictReader(open(f)):
-        if "k_sweep_strong" not in r["Kernel_Name"]:
+        if a.kernel not in r["Kernel_Name"]:
             continue
         name = r["Kernel_Name"]
         per[(r["Counter_Name"], r["Dispatch_Id"])] += float(r["Counter_Value"])
     for (k, _), v in per.items():
         d[k].append(v)
 m = {k: sum(v) / len(v) for k, v in d.items()}
-out = {"kernel": "k_sweep_strong", "kernel_symbol": name, "width": 3024, "height": 2016, "n_src": 8,
+out = {"kernel": a.kernel, "kernel_symbol": name, "width": a.width, "height": a.height, "n_src": a.n_src,
+       "launches_sampled": max((len(v) for v in d.values()), default=0),
        "counters_per_launch": {k: round(v, 1) for k, v in sorted(m.items())}}
 if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
     out["fetch_bytes_raw"] = m["FETCH_SIZE"] * 1024
@@ -26,15 +38,21 @@ if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
     out["correction"] = "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes); narrow-gather widths uncalibrated"
 if "SQ_WAVE_CYCLES" in m:
     w = m["SQ_WAVE_CYCLES"]
-    out["derived"] = {"wait_frac": m["SQ_WAIT_ANY"] / w, "issue_stall_frac": m["SQ_WAIT_INST_ANY"] / w,
-                      "active_frac": m["SQ_ACTIVE_INST_ANY"] / w,
-                      "valu_per_wave": m["SQ_INSTS_VALU"] / m["SQ_WAVES"],
+    g = lambda k: m.get(k)
+    out["derived"] = {"wait_frac": g("SQ_WAIT_ANY") / w if g("SQ_WAIT_ANY") else None,
+                      "issue_stall_frac": g("SQ_WAIT_INST_ANY") / w if g("SQ_WAIT_INST_ANY") else None,
+                      "active_frac": g("SQ_ACTIVE_INST_ANY") / w if g("SQ_ACTIVE_INST_ANY") else None,
+                      "valu_per_wave": m["SQ_INSTS_VALU"] / m["SQ_WAVES"] if "SQ_INSTS_VALU" in m else None,
+                      "valu_per_gather": m["SQ_INSTS_VALU"] / m["SQ_INSTS_VMEM_RD"] if "SQ_INSTS_VMEM_RD" in m else None,
                       "l2_hit": m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"]) if "TCC_HIT_sum" in m else None,
-                      "l1_miss_req_per_gather": m["TCP_TCC_READ_REQ_sum"] / m["SQ_INSTS_VMEM_RD"] if "TCP_TCC_READ_REQ_sum" in m else None}
-if len(sys.argv) > 3:
-    for r in csv.DictReader(open(sys.argv[3])):
-        if "k_sweep_strong" in r["Name"]:
+                      "l1_miss_req_per_gather": m["TCP_TCC_READ_REQ_sum"] / m["SQ_INSTS_VMEM_RD"]
+                      if "TCP_TCC_READ_REQ_sum" in m and "SQ_INSTS_VMEM_RD" in m else None,
+                      "l1_miss_frac": m["TCP_TCC_READ_REQ_sum"] / m["TCP_TOTAL_CACHE_ACCESSES_sum"]
+                      if "TCP_TOTAL_CACHE_ACCESSES_sum" in m and "TCP_TCC_READ_REQ_sum" in m else None}
+if a.stats:
+    for r in csv.DictReader(open(a.stats)):
+        if a.kernel in r["Name"]:
             out["rocprof_avg_launch_ns"] = float(r["AverageNs"])
-out["source"] = "rocprofv3 --pmc, one pass per counter group (tools/pmc_profile.sh), bench.py --steps 2 --warmup 1"
-json.dump(out, open(dst, "w"), indent=1)
+out["source"] = a.source
+json.dump(out, open(a.dst, "w"), indent=1)
 print(json.dumps(out, indent=1))
