@@ -6,8 +6,7 @@
 set -e
 OUT=${1:-gpurun_out/pmc_c3}
 RE=${2:-"k_sweep_weak_vm|k_weak_cand_vm"}
-shift 2 || true
-EXTRA="$*"
+EXTRA="${*:3}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 CMD="python3 bench.py --steps 3 --warmup 0 --no-cpu-baseline --end-to-end 0 --c2 0 --rich 0 $EXTRA"
