@@ -264,6 +264,9 @@ struct Driver {
     std::mutex fit_mu;
     std::map<std::tuple<const uint8_t *, int, int>, std::pair<Mat, Mat>> fitted;
     Mat fit_cached(const Mat &m, int w, int h) {
+        // the key (buffer address) is stable only when reads are served from the MemoryCache: without
+        // it every read returns a fresh buffer, nothing would hit, and the map would pin every prior
+        if (!store->cached()) return resize_nearest(m, w, h);
         const auto key = std::make_tuple(m.bytes(), w, h);
         {
             std::lock_guard<std::mutex> g(fit_mu);
@@ -805,6 +808,11 @@ int main(int argc, char **argv) {
         printf("Write memory cache to disk!\n");
         store.flush_all();
         printf("All done!\n");
+    }
+    store.drain();
+    if (store.failed_writes()) {
+        std::cout << "Error: " << store.failed_writes() << " result file(s) could not be written" << std::endl;
+        return EXIT_FAILURE;
     }
     if (no_fuse) {
         printf("Skip fusion, all done!\n");

@@ -26,6 +26,18 @@ void apdhost_resize_nearest(const void *src, int sw, int sh, void *dst, int dw, 
     resize_nearest(src, sw, sh, dst, dw, dh, elem);
 }
 int apdhost_read_camera(const char *path, apd_camera *cam) { return read_camera(path, *cam) ? 0 : -1; }
+// ReadBinMat (APD.cpp:18-56): payload bytes (copied into out if out_cap suffices) or -1 when the file
+// is missing, malformed or truncated (then no Mat at all, not a partly filled one)
+long apdhost_read_binmat(const char *path, void *out, long out_cap, int *rows, int *cols, int *type) {
+    Mat m;
+    if (!read_binmat_file(path, m)) return m.empty() ? -1 : -2;
+    *rows = m.rows;
+    *cols = m.cols;
+    *type = m.type;
+    const long n = (long)m.size_bytes();
+    if (out && out_cap >= n) memcpy(out, m.bytes(), n);
+    return n;
+}
 }
 
 #include "fusion.h"

@@ -22,12 +22,18 @@
 #include <cstring>
 #include <fstream>
 
+#include <sys/stat.h>
+
 namespace apdhost {
 
 static bool read_file(const std::string &path, std::vector<uint8_t> &data) {
+    struct stat st;
+    if (stat(path.c_str(), &st) != 0 || !S_ISREG(st.st_mode)) return false;  // directories throw in the reads
     std::ifstream f(path, std::ios::binary);
     if (!f) return false;
-    data.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    data.resize((size_t)st.st_size);
+    f.read(reinterpret_cast<char *>(data.data()), (std::streamsize)data.size());
+    data.resize((size_t)f.gcount());
     return true;
 }
 
@@ -62,6 +68,7 @@ static bool png_raw(const std::vector<uint8_t> &file, PngRaw &png, std::string &
         if (pos + 12 + (size_t)len > file.size()) { err = "truncated PNG chunk"; return false; }
         const uint8_t *d = &file[pos + 8];
         if (type == "IHDR") {
+            if (len < 13) { err = "bad PNG IHDR"; return false; }
             w = (int)be32(d); h = (int)be32(d + 4); depth = d[8]; ctype = d[9]; interlace = d[12];
         } else if (type == "PLTE") {
             plte.assign(d, d + len);
@@ -73,6 +80,7 @@ static bool png_raw(const std::vector<uint8_t> &file, PngRaw &png, std::string &
         pos += 12 + len;
     }
     if (w <= 0 || h <= 0) { err = "PNG without IHDR"; return false; }
+    if ((size_t)w * (size_t)h > ((size_t)1 << 28)) { err = "unsupported PNG size"; return false; }
     if (depth != 8) { err = "only 8-bit PNG is supported"; return false; }
     if (interlace) { err = "interlaced PNG is not supported"; return false; }
     int ch;
@@ -374,6 +382,7 @@ static bool jpeg_decode(const std::vector<uint8_t> &f, bool all_comps, JpegPlane
         if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
         if (m == 0xD9) break;
         const size_t len = (size_t)f[pos] << 8 | f[pos + 1];
+        if (len < 2) { err = "bad JPEG segment length"; return false; }
         if (pos + len > f.size()) { err = "truncated JPEG segment"; return false; }
         const uint8_t *d = &f[pos + 2];
         const size_t dl = len - 2;
@@ -386,7 +395,7 @@ static bool jpeg_decode(const std::vector<uint8_t> &f, bool all_comps, JpegPlane
             while (i < dl) {
                 const int pq = d[i] >> 4, tq = d[i] & 15;
                 ++i;
-                if (tq > 3) { err = "bad DQT"; return false; }
+                if (tq > 3 || i + (pq ? 128 : 64) > dl) { err = "bad DQT"; return false; }
                 for (int k = 0; k < 64; ++k) {
                     uint16_t v = pq ? (uint16_t)(d[i] << 8 | d[i + 1]) : d[i];
                     i += pq ? 2 : 1;
@@ -399,13 +408,13 @@ static bool jpeg_decode(const std::vector<uint8_t> &f, bool all_comps, JpegPlane
             while (i < dl) {
                 const int tc = d[i] >> 4, th = d[i] & 15;
                 ++i;
-                if (th > 3) { err = "bad DHT"; return false; }
+                if (th > 3 || i + 16 > dl) { err = "bad DHT"; return false; }
                 Huff &h = tc ? hac[th] : hdc[th];
                 int counts[17] = {0};
                 int total = 0;
                 for (int l = 1; l <= 16; ++l) { counts[l] = d[i + l - 1]; total += counts[l]; }
                 i += 16;
-                if (total > 256) { err = "bad DHT"; return false; }
+                if (total > 256 || i + (size_t)total > dl) { err = "bad DHT"; return false; }
                 memcpy(h.vals, &d[i], total);
                 i += total;
                 int code = 0, k = 0;
@@ -421,18 +430,27 @@ static bool jpeg_decode(const std::vector<uint8_t> &f, bool all_comps, JpegPlane
                 h.present = true;
             }
         } else if (m == 0xDD) {  // DRI
+            if (dl < 2) { err = "bad DRI"; return false; }
             restart = d[0] << 8 | d[1];
         } else if (m == 0xC0 || m == 0xC1) {  // baseline / extended sequential Huffman
+            if (dl < 6) { err = "bad SOF"; return false; }
             if (d[0] != 8) { err = "only 8-bit JPEG is supported"; return false; }
             H = d[1] << 8 | d[2];
             W = d[3] << 8 | d[4];
             const int nc = d[5];
+            // corrupt headers must not index tables out of range or size huge buffers
+            if (nc < 1 || nc > 4 || dl < 6 + 3 * (size_t)nc) { err = "bad SOF"; return false; }
+            if (W < 1 || H < 1 || (size_t)W * H > ((size_t)1 << 28)) { err = "unsupported JPEG size"; return false; }
             comps.resize(nc);
             for (int c = 0; c < nc; ++c) {
                 comps[c].id = d[6 + 3 * c];
                 comps[c].h = d[7 + 3 * c] >> 4;
                 comps[c].v = d[7 + 3 * c] & 15;
                 comps[c].tq = d[8 + 3 * c];
+                if (comps[c].h < 1 || comps[c].h > 4 || comps[c].v < 1 || comps[c].v > 4 || comps[c].tq > 3) {
+                    err = "bad SOF component";
+                    return false;
+                }
                 hmax = std::max(hmax, comps[c].h);
                 vmax = std::max(vmax, comps[c].v);
             }
@@ -452,6 +470,7 @@ static bool jpeg_decode(const std::vector<uint8_t> &f, bool all_comps, JpegPlane
         } else if (m == 0xDA) {  // SOS
             if (!sof) { err = "SOS before SOF"; return false; }
             const int ns = d[0];
+            if (ns < 1 || ns > 4 || dl < 1 + 2 * (size_t)ns) { err = "bad SOS"; return false; }
             std::vector<int> sc(ns);
             for (int k = 0; k < ns; ++k) {
                 const int cid = d[1 + 2 * k];
@@ -461,6 +480,7 @@ static bool jpeg_decode(const std::vector<uint8_t> &f, bool all_comps, JpegPlane
                 sc[k] = idx;
                 comps[idx].td = d[2 + 2 * k] >> 4;
                 comps[idx].ta = d[2 + 2 * k] & 15;
+                if (comps[idx].td > 3 || comps[idx].ta > 3) { err = "bad SOS table index"; return false; }
                 comps[idx].pred = 0;
             }
             pos += len;
@@ -471,8 +491,8 @@ static bool jpeg_decode(const std::vector<uint8_t> &f, bool all_comps, JpegPlane
                 const Huff &dc = hdc[c.td], &ac = hac[c.ta];
                 if (!dc.present || !ac.present) return false;
                 const int t = huff_decode(br, dc);
-                if (t < 0) return false;
-                c.pred += extend(br.get(t), t);
+                if (t < 0 || t > 15) return false;  // DC categories are <= 11 for 8-bit data
+                c.pred = (int)((unsigned)c.pred + (unsigned)extend(br.get(t), t));  // wraps, never UB
                 blk[0] = (int16_t)c.pred;
                 for (int k = 1; k < 64;) {
                     const int rs = huff_decode(br, ac);

@@ -82,9 +82,21 @@ bool read_binmat_file(const std::string &path, Mat &m) {
     if (!in || hdr[0] != 1) return false;
     const int es = cv_elem_size(hdr[3]);
     if (es == 0 || hdr[1] < 0 || hdr[2] < 0) return false;
-    m = Mat(hdr[1], hdr[2], hdr[3]);
-    in.read(reinterpret_cast<char *>(m.bytes()), (std::streamsize)m.size_bytes());
-    return (bool)in;
+    // the payload must be in the file before a buffer of its size is allocated (a corrupt header
+    // could otherwise ask for terabytes)
+    const std::streampos here = in.tellg();
+    in.seekg(0, std::ios::end);
+    const std::streamoff avail = in.tellg() - here;
+    in.seekg(here);
+    if (avail < 0 || (uint64_t)avail < (uint64_t)hdr[1] * (uint64_t)hdr[2] * (uint64_t)es) return false;
+    Mat r(hdr[1], hdr[2], hdr[3]);
+    in.read(reinterpret_cast<char *>(r.bytes()), (std::streamsize)r.size_bytes());
+    if (!in) {  // truncated file: no Mat (a pooled buffer would expose another problem's bytes)
+        m = Mat();
+        return false;
+    }
+    m = r;
+    return true;
 }
 
 bool write_binmat_file(const std::string &path, const Mat &m) {
@@ -132,6 +144,7 @@ bool MatStore::write(const std::string &path, const Mat &m, bool flush) {
     if (!cache_) {
         if (!write_binmat_file(path, m)) {
             std::cout << "Error opening file: \"" << path << "\"" << std::endl;
+            ++failed_;
             return false;
         }
     }
@@ -146,8 +159,10 @@ void MatStore::writer_loop() {
         auto job = std::move(queue_.front());
         queue_.pop_front();
         l.unlock();
-        if (!write_binmat_file(job.first, job.second))
+        if (!write_binmat_file(job.first, job.second)) {
             std::cout << "Error opening file: \"" << job.first << "\"" << std::endl;
+            ++failed_;
+        }
         job.second = Mat();
         l.lock();
         if (--inflight_ == 0) qdone_.notify_all();
@@ -171,7 +186,11 @@ MatStore::~MatStore() {
 void MatStore::flush_all() {
     drain();
     std::lock_guard<std::mutex> g(mu_);
-    for (auto &kv : mats_) write_binmat_file(kv.first, kv.second);
+    for (auto &kv : mats_)
+        if (!write_binmat_file(kv.first, kv.second)) {
+            std::cout << "Error opening file: \"" << kv.first << "\"" << std::endl;
+            ++failed_;
+        }
     mats_.clear();
 }
 

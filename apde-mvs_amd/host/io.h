@@ -12,6 +12,7 @@
 #include <condition_variable>
 #include <deque>
 #include <thread>
+#include <atomic>
 
 #include "../../include/apd_hip.h"
 
@@ -61,6 +62,9 @@ public:
     void flush_all();                                              // main.cpp:381-393
     void drain();                                                  // wait for queued file writes
     bool cached() const { return cache_; }
+    // result files that could not be written so far (synchronous, queued and flushed writes alike);
+    // the caller waits with drain() before reading it, and main() exits non-zero when it is not 0
+    size_t failed_writes() const { return failed_.load(); }
 
 private:
     void writer_loop();
@@ -72,6 +76,7 @@ private:
     std::deque<std::pair<std::string, Mat>> queue_;
     size_t inflight_ = 0;
     bool stop_ = false;
+    std::atomic<size_t> failed_{0};
     std::thread writer_;
 };
 

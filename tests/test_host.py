@@ -30,6 +30,8 @@ def hostlib():
     lib.apdhost_resize_nearest.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]
     lib.apdhost_read_camera.restype = C.c_int
     lib.apdhost_read_camera.argtypes = [C.c_char_p, C.POINTER(A.ApdCamera)]
+    lib.apdhost_read_binmat.restype = C.c_long
+    lib.apdhost_read_binmat.argtypes = [C.c_char_p, C.c_void_p, C.c_long] + [C.POINTER(C.c_int)] * 3
     return lib
 
 
@@ -188,3 +190,20 @@ def test_cli_help_and_errors(hostlib):
 def test_cli_bad_scan_folder(hostlib, tmp_path):
     r = run_apd("--dense_folder", str(tmp_path), "--no_fuse", "true")
     assert r.returncode != 0
+
+
+def test_binmat_read_and_truncation(hostlib, tmp_path):
+    """ReadBinMat (APD.cpp:18-56): a complete file reads back; a truncated one is rejected as a whole
+    (no partly filled Mat whose tail would hold another problem's pooled bytes)."""
+    import synth
+    m = np.arange(37 * 23, dtype=np.float32).reshape(23, 37)
+    path = str(tmp_path / "d.bin")
+    synth.write_bin_mat(path, m)
+    r, c, t = C.c_int(), C.c_int(), C.c_int()
+    out = np.zeros_like(m)
+    n = hostlib.apdhost_read_binmat(path.encode(), out.ctypes.data, out.nbytes, C.byref(r), C.byref(c), C.byref(t))
+    assert n == m.nbytes and (r.value, c.value, t.value) == (23, 37, 5) and np.array_equal(out, m)
+    data = open(path, "rb").read()
+    for cut in (8, 16, 17, len(data) // 2, len(data) - 1):
+        open(path, "wb").write(data[:cut])
+        assert hostlib.apdhost_read_binmat(path.encode(), None, 0, C.byref(r), C.byref(c), C.byref(t)) == -1, cut
