@@ -1411,9 +1411,12 @@ struct WvLdsT : WvRefT<F16> {
 // 52.2 KiB with the cost table at N = 8 (fp16 reference taps): three workgroups per CU.
 static_assert(sizeof(WvLdsT<true>) + 9 * 8 * VM_P * sizeof(float) + 8 * VM_P <= 53 * 1024,
               "k_sweep_weak_vm at N = 8 must fit three workgroups per CU (160 KiB LDS)");
+// `direct` (k_weak_cand_vm handled every pixel, no SA masks): the sweep reads the anchor candidates'
+// costs from k_weak_cand_vm's buffer in P2 and its table holds [5][N][64] (current plane, fit plane,
+// refinement candidates) instead of [9][N][64]: 48 KiB at N = 10, three workgroups per CU instead of two.
 template <bool F16>
-static inline size_t wv_lds_bytes(int N) {
-    return sizeof(WvLdsT<F16>) + (size_t)9 * N * VM_P * sizeof(float) + (size_t)N * VM_P;
+static inline size_t wv_lds_bytes(int N, bool direct = false) {
+    return sizeof(WvLdsT<F16>) + (size_t)(direct ? 5 : 9) * N * VM_P * sizeof(float) + (size_t)N * VM_P;
 }
 __device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
     const long idx = (long)y * a.W + x;
@@ -1685,9 +1688,13 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
                                                                 int iter, const float *__restrict__ cand,
                                                                 const uint8_t *__restrict__ cand_done, int wc) {
     const int N = a.N, W = a.W;
+    // direct: k_weak_cand_vm evaluated every pixel's anchor candidates (no SA masks: no group is left
+    // to the sweep), so P2 reads their costs from `cand` and the table is [N][64] (current plane),
+    // later [5][N][64] (wv_lds_bytes)
+    const bool direct = cand != nullptr && !a.sa_any;
     WvLdsT<F16> &L = *reinterpret_cast<WvLdsT<F16> *>(apd_dyn_lds);
-    float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64], later [5][N][64]
-    uint8_t *wts = reinterpret_cast<uint8_t *>(costL + 9 * N * VM_P);    // [N][64] view weights
+    float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64] (direct: [N][64]), later [5][N][64]
+    uint8_t *wts = reinterpret_cast<uint8_t *>(costL + (direct ? 5 : 9) * N * VM_P);  // [N][64] view weights
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int first = blk * VM_P;
     const int np = min(VM_P, count - first);
@@ -1747,8 +1754,9 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     // anchor candidates' costs are read, and only the current plane is evaluated here
     const int wi1 = cand ? a.amap[c1] : 0;
     const bool cand_ok = cand && pv1 && cand_done[wi1];  // per pixel (groups of k_weak_cand_vm span both colours)
-    for (int u = wave; u < 9 * N; u += WV_WAVES) {  // view-major: the waves share a source image
-        const int v = u / 9, h = u - 9 * v, t = h * N + v;
+    const int ntask = direct ? N : 9 * N;
+    for (int u = wave; u < ntask; u += WV_WAVES) {  // view-major: the waves share a source image
+        const int v = direct ? u : u / 9, h = direct ? 8 : u - 9 * v, t = direct ? v : h * N + v;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
         const bool want = pv1 && (h == 8 || ((L.flags[p1] >> h) & 1u));
         if (cand && h < 8 && !__ballot(want && !cand_ok)) {  // every lane that needs it has its cost
@@ -1797,9 +1805,18 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             if (pk >= 0) prior += ((a.sel[(pk & 0xFFFF) + (pk >> 16) * W] >> v) & 1u) ? 0.9f : 0.1f;
         }
         float ca[8];
+        float cv_now;
+        if (direct) {  // the candidates' costs from k_weak_cand_vm; absent ones as P1 sets them
+            const size_t wi = (size_t)a.amap[c];
 #pragma unroll
-        for (int h = 0; h < 8; ++h) ca[h] = costL[(h * N + v) * VM_P + p];
-        const float cv_now = costL[(8 * N + v) * VM_P + p];
+            for (int h = 0; h < 8; ++h)
+                ca[h] = ((hflag >> h) & 1u) ? cand[((size_t)v * 8 + h) * (size_t)wc + wi] : ((h == 0 && v == 0) ? 2.0f : 0.0f);
+            cv_now = costL[v * VM_P + p];
+        } else {
+#pragma unroll
+            for (int h = 0; h < 8; ++h) ca[h] = costL[(h * N + v) * VM_P + p];
+            cv_now = costL[(8 * N + v) * VM_P + p];
+        }
         Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c, ord_weak(iter));
         const int w = view_selection(ca, prior, iter, rg, G, N);
         const uint32_t tsel = group_bits(w > 0, G);
@@ -4216,8 +4233,9 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             aw.evals = evals;
             if (!(ctx->wcur_fresh && iter == 0)) aw.wcur = nullptr;
             e0 = prof_begin(ctx);
+            const bool direct = cand != nullptr && !a.sa_any;  // k_sweep_weak_vm's small cost table
             if (ctx->sweep_vm)
-                LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N) : wv_lds_bytes<false>(a.N)), s,
+                LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N, direct) : wv_lds_bytes<false>(a.N, direct)), s,
                            aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, (const uint8_t *)ctx->wdone.p, wc);
             else
                 LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,

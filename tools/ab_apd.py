@@ -41,17 +41,21 @@ else:
     priors = [run(e0, cases.base_problem(sc, r, N)) for r in range(len(sc.images))]
     arr = cases.refine_problem(sc, priors, 0, N, state=A.REFINE_ITER, geom=True, apd=True,
                                sa=os.environ.get("AB_SA") == "1")  # AB_SA=1: the scene's plane labels as SA masks
+    if os.environ.get("AB_FINAL") == "1":  # bench.py's headline pass: main.cpp's last round (rotate_time 4)
+        arr.params.rotate_time, arr.params.ransac_threshold, arr.params.weak_peak_radius = 4, 0.01 - 3 * 0.00125, 4
 outs = {}
 res = {n: [] for n, _ in engines}
 for r in range(ROUNDS):
     for name, e in engines:
         out = run(e, arr)
         t = e.timing()
-        res[name].append((t.total_ms, t.anchors_ms, t.init_ms, t.sweep_ms, t.post_ms))
+        res[name].append((t.total_ms, t.anchors_ms, t.init_ms, t.sweep_ms, t.post_ms,
+                          statistics.median(list(t.iter_ms)[:t.iterations])))
         outs.setdefault(name, out)
 ref = outs[engines[0][0]]
 for name, v in res.items():
-    med = [statistics.median(x[i] for x in v) for i in range(5)]
+    med = [statistics.median(x[i] for x in v) for i in range(6)]
     d = cases.compare(ref, outs[name])
     print(f"{name}: total {med[0]:.1f} ms  anchors {med[1]:.1f}  init {med[2]:.1f}  sweep {med[3]:.1f}  "
-          f"post {med[4]:.1f}  identical={not any(d.values())}", flush=True)
+          f"post {med[4]:.1f}  iter {med[5]:.2f} ({W * H / med[5] / 1e3:.2f} Mpix/s)  identical={not any(d.values())}",
+          flush=True)
