@@ -733,6 +733,9 @@ __device__ __forceinline__ Cands refine_candidates(const Args &a, int px, int py
     const APD_C Cam &cam = a.cams[0];
     Cands C;
     C.drand = g.uniform() * (a.dmax - a.dmin) + a.dmin;
+#ifdef APD_ABLATE_RANDDEPTH  // timing-only experiment (wrong values): random-depth candidates kept local
+    C.drand = depth * 1.001f;
+#endif
     C.nrand = random_normal(cam, px, py, g, depth);
     float dp = depth;
     const float dminp = (1 - 0.02f) * dp;
