@@ -1891,20 +1891,63 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     __syncthreads();
     const bool refine = pv1 && (L.flags[p1] >> 31) != 0u;
     const float4 fit1 = a.fit[c1];
+    uint32_t issued_nn = 0, issued_g = 0;  // profiling: P3/P5 evaluations this lane issued
 
-    // ---- P3: fit-plane tasks (views with weight > 0)
-    for (int v = wave; v < N; v += WV_WAVES) {
-        float cv = 0.0f;
-        const bool want = refine && wts[v * VM_P + p1] > 0;
-        const float4 fit = fit1;
-        const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, fit, want);
-        if (want) {
-            cv = nv;
-            if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, fit), cv);
-        }
-        costL[v * VM_P + p1] = cv;
-    }
+    // ---- early exit for the fit plane and the refinement candidates (exact). A candidate is accepted
+    // only if its weighted cost tc = fl(S / wn) is below the running cost, which never exceeds the cost
+    // `thr` it starts from (P3: the cost after P2; P5: after the fit plane). S accumulates
+    // fmaf(w_v, c_v, .) over the weighted views in view order, with w_v > 0 and c_v >= 0, so every
+    // prefix P of that chain satisfies P <= S and fl(P / wn) <= fl(S / wn): once fl(P / wn) >= thr the
+    // candidate is rejected whatever its remaining views give, and they are not evaluated (P6 / P4
+    // skip it). Tasks run in batches of WV_WAVES (one per wave); before each batch every (candidate,
+    // pixel) folds the views completed by the previous batches into P in view order. The flags are
+    // read by other waves while they are set (a stale 0 only evaluates a view that is not needed).
+    // part / nxt / dead overlay hyp[5..7] (only P2 reads the anchor planes).
+    float *part = reinterpret_cast<float *>(&L.hyp[5 * VM_P]);          // [6][64]: 0 fit, 1..5 candidates
+    uint8_t *nxt = reinterpret_cast<uint8_t *>(part + 6 * VM_P);        // [6][64] next view to fold
+    uint8_t *dead = nxt + 6 * VM_P;                                     // [6][64]
+    static_assert(6 * VM_P * (sizeof(float) + 2) <= 3 * VM_P * sizeof(float4), "early-exit state overlays hyp[5..7]");
+    for (int i = tid; i < 6 * VM_P; i += WV_BLOCK) { part[i] = 0.0f; nxt[i] = 0; dead[i] = 0; }
     __syncthreads();
+    // fold the views of slot `s` (cost table row `row`, K tasks per view, candidate k) that the tasks
+    // below `done` completed; then flag the slot when its partial cost reaches thr
+    auto fold = [&](int s, int K, int k, int row, int done) {
+        for (int p = tid; p < VM_P; p += WV_BLOCK) {
+            const int it = s * VM_P + p;
+            if (dead[it]) continue;
+            int v = nxt[it];
+            float P = part[it];
+            const int v0 = v;
+            for (; v < N && v * K + k < done; ++v) {
+                const int wk = wts[v * VM_P + p];
+                if (wk > 0) P = fmaf((float)wk, costL[(row + v) * VM_P + p], P);
+            }
+            if (v == v0) continue;
+            nxt[it] = (uint8_t)v;
+            part[it] = P;
+            if (P / L.st[3 * VM_P + p] >= L.st[1 * VM_P + p]) dead[it] = 1;
+        }
+    };
+
+    // ---- P3: fit-plane tasks (views with weight > 0), early exit against the cost after P2
+    for (int v0 = 0; v0 < N; v0 += WV_WAVES) {
+        if (v0 > 0) fold(0, 1, 0, 0, v0);
+        const int v = v0 + wave;
+        if (v < N) {
+            float cv = 0.0f;
+            const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[p1];
+            const float4 fit = fit1;
+            const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, fit, want);
+            if (want) {
+                cv = nv;
+                if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, fit), cv);
+                ++issued_nn;
+                issued_g += geom;
+            }
+            costL[v * VM_P + p1] = cv;
+        }
+        __syncthreads();
+    }
 
     // ---- P4: fit acceptance, refinement candidates (PlaneHypothesisRefinementWeak, APD.cu:1008-1067)
     if (wave == 0 && refine) {
@@ -1912,14 +1955,16 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         float depth_now = L.st[0 * VM_P + p1], cost_now = L.st[1 * VM_P + p1];
         float4 pnow = L.pnow[p1];
         const float4 fit = fit1;
-        float tc = 0.0f;
-        for (int kk = 0; kk < N; ++kk) {
-            const int wk = wts[kk * VM_P + p1];
-            if (wk > 0) tc = fmaf((float)wk, costL[kk * VM_P + p1], tc);
+        if (!dead[p1]) {  // (dead: the fit plane's cost reaches cost_now -- rejected)
+            float tc = 0.0f;
+            for (int kk = 0; kk < N; ++kk) {
+                const int wk = wts[kk * VM_P + p1];
+                if (wk > 0) tc = fmaf((float)wk, costL[kk * VM_P + p1], tc);
+            }
+            tc /= wn;
+            const float db = depth_from_plane(cam0, fit, px1, py1);
+            if (db >= a.dmin && db <= a.dmax && tc < cost_now) { depth_now = db; pnow = fit; cost_now = tc; }
         }
-        tc /= wn;
-        const float db = depth_from_plane(cam0, fit, px1, py1);
-        if (db >= a.dmin && db <= a.dmax && tc < cost_now) { depth_now = db; pnow = fit; cost_now = tc; }
         Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c1, ord_weak(iter));
         rg.n = L.rng_n[p1];
         if (rg.n & 3u) rg.refill();
@@ -1936,20 +1981,28 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     }
     __syncthreads();
 
-    // ---- P5: candidate tasks (views with weight > 0)
-    for (int u = wave; u < 5 * N; u += WV_WAVES) {
-        const int v = u / 5, k = u - 5 * v, t = k * N + v;
-        float cv = 0.0f;
-        const bool want = refine && wts[v * VM_P + p1] > 0;
-        const float4 tp = WV_CAND(L)[k * VM_P + p1];
-        const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, tp, want);
-        if (want) {
-            cv = nv;
-            if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
+    // ---- P5: candidate tasks (views with weight > 0), view-major, early exit against the cost after
+    // the fit plane (slots 1..5)
+    for (int u0 = 0; u0 < 5 * N; u0 += WV_WAVES) {
+        if (u0 > 0)
+            for (int k = 0; k < 5; ++k) fold(1 + k, 5, k, k * N, u0);
+        const int u = u0 + wave;
+        if (u < 5 * N) {
+            const int v = u / 5, k = u - 5 * v, t = k * N + v;
+            float cv = 0.0f;
+            const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[(1 + k) * VM_P + p1];
+            const float4 tp = WV_CAND(L)[k * VM_P + p1];
+            const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, tp, want);
+            if (want) {
+                cv = nv;
+                if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
+                ++issued_nn;
+                issued_g += geom;
+            }
+            costL[t * VM_P + p1] = cv;
         }
-        costL[t * VM_P + p1] = cv;
+        __syncthreads();
     }
-    __syncthreads();
 
     if (a.evals && wave == 0) {
         // profiling: the NCC-New evaluations and geometric terms CheckerboardPropagationWeak issues
@@ -1962,10 +2015,15 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             int nsel = 0;
             for (int v = 0; v < N; ++v) nsel += wts[v * VM_P + p1] > 0;
             const int nh = __builtin_popcount(L.flags[p1] & 0xFFu);
-            const int nr = refine ? 6 * nsel : 0;
-            nn = (uint32_t)((nh + 1) * N + nr);
-            ng = geom ? (uint32_t)(nh * nsel + N + nr) : 0u;
+            nn = (uint32_t)((nh + 1) * N);
+            ng = geom ? (uint32_t)(nh * nsel + N) : 0u;
         }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) { nn += __shfl_xor(nn, o); ng += __shfl_xor(ng, o); }
+        if (lane == 0) { atomicAdd(a.evals + 1, (unsigned long long)nn); atomicAdd(a.evals + 2, (unsigned long long)ng); }
+    }
+    if (a.evals) {  // ... plus the fit-plane and refinement evaluations every wave issued (P3, P5)
+        uint32_t nn = issued_nn, ng = issued_g;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) { nn += __shfl_xor(nn, o); ng += __shfl_xor(ng, o); }
         if (lane == 0) { atomicAdd(a.evals + 1, (unsigned long long)nn); atomicAdd(a.evals + 2, (unsigned long long)ng); }
@@ -1980,6 +2038,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             float4 pnow = L.pnow[p1];
             if (refine) {
                 for (int k = 0; k < 5; ++k) {
+                    if (dead[(1 + k) * VM_P + p1]) continue;  // its partial cost already reached cost_now
                     const float4 t = WV_CAND(L)[k * VM_P + p1];
                     float tc = 0.0f;
                     for (int kk = 0; kk < N; ++kk) {
