@@ -1309,22 +1309,66 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     }
     __syncthreads();
 
-    // ---- P3: lane = pixel, wave = (candidate, view) tasks
+    // ---- P3: lane = pixel, wave = (candidate, view) tasks, view-major batches of VM_WAVES (one task per
+    // wave), with the exact early exit of k_sweep_weak_vm: a candidate is accepted only if
+    // fl(S / wn) < cost_now, cost_now never exceeds its value after P2b (L.st[1]), and every view-order
+    // prefix P of the fmaf chain S (weights > 0, costs >= 0) has fl(P / wn) <= fl(S / wn); so once
+    // fl(P / wn) >= L.st[1] the candidate's remaining views are not evaluated and P4 skips it. Before
+    // each batch wave 0 folds the views the earlier batches completed into P (lane = pixel); a task
+    // deferred to the out-of-line path holds -1 until it is evaluated, which stops its prefix there.
+    // part / nxt / dead overlay hyp[5..7] (P2b was their last reader).
+    float *part = reinterpret_cast<float *>(&L.hyp[5 * VM_P]);   // [5][64]
+    uint8_t *nxt = reinterpret_cast<uint8_t *>(part + 5 * VM_P); // [5][64] next view to fold
+    uint8_t *dead = nxt + 5 * VM_P;                              // [5][64]
+    static_assert(5 * VM_P * (sizeof(float) + 2) <= 3 * VM_P * sizeof(float4), "early-exit state overlays hyp[5..7]");
+    for (int i = tid; i < 5 * VM_P; i += VM_BLOCK) { part[i] = 0.0f; nxt[i] = 0; dead[i] = 0; }
+    __syncthreads();
     defer[0] = defer[1] = 0;
-    for (int u = wave, kt = 0; u < 5 * N; u += VM_WAVES, ++kt) {
-        const int v = u / 5, k = u - 5 * v, t = k * N + v;
-        float cv = 0.0f;
-        // a view with sampled weight 0 contributes fmaf(0, cv, tc) == tc for every finite cv (costs are
-        // clamped to [0, 2]), so its refinement NCCs are skipped without changing any result
-        if (pv1 && wts[v * VM_P + p1] > 0) {
-            const float4 tp = VM_CAND(L)[k * VM_P + p1];
-            bool slow;
-            ++issued;
-            cv = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, tp, rw, slow);
-            if (slow) defer[kt >> 6] |= 1ull << (kt & 63);
-            if (geom_imp) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
+    for (int u0 = 0, kt = 0; u0 < 5 * N; u0 += VM_WAVES, ++kt) {
+        if (u0 > 0 && wave == 0) {
+            const float thr = L.st[1 * VM_P + p1], wn = L.st[3 * VM_P + p1];
+#pragma unroll 1
+            for (int k = 0; k < 5; ++k) {
+                const int it = k * VM_P + p1;
+                if (dead[it]) continue;
+                int v = nxt[it];
+                float P = part[it];
+                const int v0 = v;
+                for (; v < N && v * 5 + k < u0; ++v) {
+                    const int wk = wts[v * VM_P + p1];
+                    if (wk > 0) {
+                        const float c = costL[(k * N + v) * VM_P + p1];
+                        if (c < 0.0f) break;  // deferred: not evaluated yet
+                        P = fmaf((float)wk, c, P);
+                    }
+                }
+                if (v == v0) continue;
+                nxt[it] = (uint8_t)v;
+                part[it] = P;
+                if (P / wn >= thr) dead[it] = 1;
+            }
         }
-        costL[t * VM_P + p1] = cv;
+        const int u = u0 + wave;
+        if (u < 5 * N) {
+            const int v = u / 5, k = u - 5 * v, t = k * N + v;
+            float cv = 0.0f;
+            // a view with sampled weight 0 contributes fmaf(0, cv, tc) == tc for every finite cv (costs are
+            // clamped to [0, 2]), so its refinement NCCs are skipped without changing any result
+            if (pv1 && wts[v * VM_P + p1] > 0 && !dead[k * VM_P + p1]) {
+                const float4 tp = VM_CAND(L)[k * VM_P + p1];
+                bool slow;
+                ++issued;
+                cv = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, tp, rw, slow);
+                if (slow) {
+                    defer[kt >> 6] |= 1ull << (kt & 63);
+                    cv = -1.0f;
+                } else if (geom_imp) {
+                    cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
+                }
+            }
+            costL[t * VM_P + p1] = cv;
+        }
+        __syncthreads();
     }
     for (int w2 = 0; w2 < 2; ++w2)
     while (defer[w2]) {
@@ -1355,6 +1399,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
             float4 pnow = L.pnow[p];
 #pragma unroll 1
             for (int k = 0; k < 5; ++k) {
+                if (dead[k * VM_P + p]) continue;  // its partial cost already reached cost_now
                 const float4 t = VM_CAND(L)[k * VM_P + p];
                 float tc = 0.0f;
                 for (int kk = 0; kk < N; ++kk) tc = fmaf((float)wts[kk * VM_P + p], costL[(k * N + kk) * VM_P + p], tc);
