@@ -86,10 +86,29 @@ def default_params(num_images: int, depth_min: float, depth_max: float, **kw) ->
     return p
 
 
-def _ptr(a: Optional[np.ndarray], ctype):
+def _ptr(a, ctype):
+    """ctypes pointer to a numpy array's or a torch tensor's data (host or device memory: the C ABI
+    accepts device pointers for the problem arrays and the outputs)."""
     if a is None:
         return C.POINTER(ctype)()
+    if hasattr(a, "data_ptr"):
+        return C.cast(C.c_void_p(a.data_ptr()), C.POINTER(ctype))
     return a.ctypes.data_as(C.POINTER(ctype))
+
+
+_TORCH_DTYPES = {np.dtype(np.float32): "float32", np.dtype(np.uint8): "uint8"}
+
+
+def _keep(a, dtype):
+    """A contiguous buffer of `dtype` holding `a` (numpy array or torch tensor, kept as a tensor)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        import torch
+        t = a.contiguous()
+        want = getattr(torch, _TORCH_DTYPES[np.dtype(dtype)])
+        return t if t.dtype == want else t.to(want)
+    return np.ascontiguousarray(a, dtype)
 
 
 @dataclass
@@ -110,7 +129,7 @@ class ProblemArrays:
 
     def build(self) -> ApdProblem:
         n = len(self.images)
-        self._imgs = [np.ascontiguousarray(i, np.float32) for i in self.images]
+        self._imgs = [_keep(i, np.float32) for i in self.images]
         self._img_ptrs = (C.POINTER(C.c_float) * n)(*[_ptr(i, C.c_float) for i in self._imgs])
         self._cams = (ApdCamera * n)()
         for i, cv in enumerate(self.cameras):
@@ -121,15 +140,15 @@ class ProblemArrays:
                 else:
                     setattr(cam, k, v)
         if self.depths is not None:
-            self._deps = [np.ascontiguousarray(d, np.float32) for d in self.depths]
+            self._deps = [_keep(d, np.float32) for d in self.depths]
             dptrs = (C.POINTER(C.c_float) * n)(*[_ptr(d, C.c_float) for d in self._deps])
             self._dep_ptrs = dptrs
         else:
             self._dep_ptrs = None
-        self._planes = None if self.init_planes is None else np.ascontiguousarray(self.init_planes, np.float32)
-        self._weak = None if self.weak_info is None else np.ascontiguousarray(self.weak_info, np.uint8)
-        self._conf = None if self.confidence is None else np.ascontiguousarray(self.confidence, np.uint8)
-        self._sa = None if self.sa_mask is None else np.ascontiguousarray(self.sa_mask, np.uint8)
+        self._planes = _keep(self.init_planes, np.float32)
+        self._weak = _keep(self.weak_info, np.uint8)
+        self._conf = _keep(self.confidence, np.uint8)
+        self._sa = _keep(self.sa_mask, np.uint8)
         pb = ApdProblem()
         pb.width, pb.height, pb.num_images = self.width, self.height, n
         pb.images = C.cast(self._img_ptrs, C.POINTER(C.POINTER(C.c_float)))
@@ -346,6 +365,21 @@ class Engine:
         s = out.struct()
         self._check(self.lib.apd_get_results(self.ctx, C.byref(s)), "apd_get_results")
         return out
+
+    def results_device(self, width: int, height: int, device: str):
+        """planes / weak_info / confidence as torch tensors on `device` (the ctx's device), copied
+        device to device by apd_get_results."""
+        import torch
+        from types import SimpleNamespace
+        o = SimpleNamespace(planes=torch.empty((height, width, 4), dtype=torch.float32, device=device),
+                            weak_info=torch.empty((height, width), dtype=torch.uint8, device=device),
+                            confidence=torch.empty((height, width), dtype=torch.uint8, device=device))
+        s = ApdOutputs()
+        s.planes = _ptr(o.planes, C.c_float)
+        s.weak_info = _ptr(o.weak_info, C.c_uint8)
+        s.confidence = _ptr(o.confidence, C.c_uint8)
+        self._check(self.lib.apd_get_results(self.ctx, C.byref(s)), "apd_get_results")
+        return o
 
     def timing(self) -> ApdTiming:
         t = ApdTiming()

@@ -106,6 +106,30 @@ __global__ __launch_bounds__(BLOCK) void k_check_f16(const float *__restrict__ i
     if (!ok) *flag = 0;
 }
 
+// Per-problem statistics of the uploaded maps, on the device (the inputs may be device pointers, and
+// at 6048x4032 three scalar host passes cost ~30 ms): out[0] += number of WEAK pixels, out[1] =
+// max(out[1], the largest confidence), out[2] |= any non-zero SA label.
+__global__ __launch_bounds__(BLOCK) void k_problem_stats(const uint8_t *__restrict__ weak, const uint8_t *__restrict__ conf,
+                                                       const uint8_t *__restrict__ sa, size_t n, int *out) {
+    int cnt = 0, mx = 0, any = 0;
+    for (size_t i = blockIdx.x * (size_t)BLOCK + threadIdx.x; i < n; i += (size_t)gridDim.x * BLOCK) {
+        cnt += weak[i] == APD_WEAK;
+        mx = max(mx, (int)conf[i]);
+        any |= sa[i] != 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        cnt += __shfl_xor(cnt, o);
+        mx = max(mx, __shfl_xor(mx, o));
+        any |= __shfl_xor(any, o);
+    }
+    if ((threadIdx.x & (WAVE - 1)) == 0) {
+        if (cnt) atomicAdd(&out[0], cnt);
+        atomicMax(&out[1], mx);
+        if (any) atomicOr(&out[2], 1);
+    }
+}
+
 // Source images -> fp16 vertical pairs P[(iy+1)*(W+2)+(ix+1)] = {half T(ix,iy), half T(ix,iy+1)},
 // ix in [-1, W], iy in [-1, H-1], clamp-to-edge (see SrcTex in apd_device.h).
 __global__ __launch_bounds__(BLOCK) void k_build_pairs(const float *__restrict__ imgs, uint32_t *__restrict__ pairs,
@@ -3666,6 +3690,7 @@ struct apd_ctx {
         fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, wdone, lrs, wcur,
         wlist;
     int n_near = 0;
+    int host_stat[4] = {0, 0, 0, 0};  // apd_set_problem's read-back (see there)
     int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
     Args args{};
     bool loaded = false, prepared = false;
@@ -3943,35 +3968,11 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     const size_t HW = (size_t)W * H;
     int st;
     hipStream_t s = ctx->stream;
+    // Every input may be a host or a device pointer (hipMemcpyDefault): a caller that keeps a scan's
+    // images and depth maps resident in HBM (scan_runner.py) hands device pointers over and nothing
+    // crosses PCIe here.
     if ((st = ensure(ctx, ctx->imgs, HW * NI * sizeof(float)))) return st;
-    if ((st = ensure(ctx, ctx->totals, 8 * sizeof(int)))) return st;
-    for (int i = 0; i < NI; ++i) {
-        if (!pb->images[i]) { ctx->err = "null image pointer"; return APD_EINVAL; }
-        HIP_OK(ctx, hipMemcpyAsync((float *)ctx->imgs.p + HW * i, pb->images[i], HW * sizeof(float),
-                                   hipMemcpyHostToDevice, s));
-    }
-    // source texel storage: fp16 vertical pairs when every texel -- the reference's too, whose taps
-    // k_sweep_weak_vm keeps in fp16 -- is a quarter-integer in [0, 256) (8-bit images and their
-    // INTER_LINEAR 2^-k downscales are): such texels AND their horizontal differences are exact in
-    // fp16 (FastTex::sample relies on both). Else fp32 quads. Checked on the device (one flag read).
-    bool tex_f16 = getenv("APD_TEX_F32") == nullptr;
-    if (tex_f16) {
-        int *flag = (int *)ctx->totals.p + 7;
-        const int one = 1;
-        HIP_OK(ctx, hipMemcpyAsync(flag, &one, sizeof(int), hipMemcpyHostToDevice, s));
-        const size_t n = HW * NI;
-        hipLaunchKernelGGL(k_check_f16, dim3((unsigned)std::min<size_t>(blocks_for(n, BLOCK), 8192)), dim3(BLOCK), 0, s,
-                           (const float *)ctx->imgs.p, n, flag);
-        if ((st = check_launch(ctx, "k_check_f16"))) return st;
-        int ok = 0;
-        HIP_OK(ctx, hipMemcpyAsync(&ok, flag, sizeof(int), hipMemcpyDeviceToHost, s));
-        HIP_OK(ctx, hipStreamSynchronize(s));
-        tex_f16 = ok != 0;
-    }
-    const size_t qstride = tex_f16 ? (size_t)(W + 2) * (H + 1) : (size_t)(W + 1) * (H + 1);
-    if ((st = ensure(ctx, ctx->quad, qstride * N * (tex_f16 ? sizeof(uint32_t) : sizeof(float4))))) return st;
-    if ((st = ensure(ctx, ctx->views, NI * sizeof(SrcView)))) return st;
-    if ((st = ensure(ctx, ctx->cams, NI * sizeof(Cam)))) return st;
+    if ((st = ensure(ctx, ctx->totals, 16 * sizeof(int)))) return st;
     if ((st = ensure(ctx, ctx->plane, HW * sizeof(float4)))) return st;
     if ((st = ensure(ctx, ctx->cost, HW * sizeof(float)))) return st;
     if ((st = ensure(ctx, ctx->sel, HW * sizeof(uint32_t)))) return st;
@@ -3981,18 +3982,61 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     if ((st = ensure(ctx, ctx->conf, HW))) return st;
     if ((st = ensure(ctx, ctx->sa, HW))) return st;
     if ((st = ensure(ctx, ctx->lists, (HW + 8) * sizeof(int)))) return st;
+    if ((st = ensure(ctx, ctx->views, NI * sizeof(SrcView)))) return st;
+    if ((st = ensure(ctx, ctx->cams, NI * sizeof(Cam)))) return st;
     const size_t units = std::max<size_t>((size_t)H, (size_t)(W + 3) / 4 * ((H + 3) / 4));  // any tile shape
     if ((st = ensure(ctx, ctx->rowcnt, units * sizeof(int)))) return st;
     if ((st = ensure(ctx, ctx->rowoff, units * sizeof(int)))) return st;
     const bool need_depth = P.geom_consistency || P.use_APD;
     if (need_depth && (st = ensure(ctx, ctx->depth, HW * NI * sizeof(float)))) return st;
+    for (int i = 0; i < NI; ++i) {
+        if (!pb->images[i]) { ctx->err = "null image pointer"; return APD_EINVAL; }
+        HIP_OK(ctx, hipMemcpyAsync((float *)ctx->imgs.p + HW * i, pb->images[i], HW * sizeof(float), hipMemcpyDefault, s));
+    }
     if (need_depth) {
         for (int i = 0; i < NI; ++i) {
             if (!pb->depths[i]) { ctx->err = "null depth pointer"; return APD_EINVAL; }
-            HIP_OK(ctx, hipMemcpyAsync((float *)ctx->depth.p + HW * i, pb->depths[i], HW * sizeof(float),
-                                       hipMemcpyHostToDevice, s));
+            HIP_OK(ctx, hipMemcpyAsync((float *)ctx->depth.p + HW * i, pb->depths[i], HW * sizeof(float), hipMemcpyDefault, s));
         }
     }
+    // priors (APD.cpp:612-683)
+    if (P.state != APD_FIRST_INIT && pb->init_planes)
+        HIP_OK(ctx, hipMemcpyAsync(ctx->plane.p, pb->init_planes, HW * sizeof(float4), hipMemcpyDefault, s));
+    else
+        HIP_OK(ctx, hipMemsetAsync(ctx->plane.p, 0, HW * sizeof(float4), s));
+    if (P.use_APD && pb->weak_info) HIP_OK(ctx, hipMemcpyAsync(ctx->weak.p, pb->weak_info, HW, hipMemcpyDefault, s));
+    else HIP_OK(ctx, hipMemsetAsync(ctx->weak.p, APD_STRONG, HW, s));
+    if (P.use_APD && pb->confidence) HIP_OK(ctx, hipMemcpyAsync(ctx->conf.p, pb->confidence, HW, hipMemcpyDefault, s));
+    else HIP_OK(ctx, hipMemsetAsync(ctx->conf.p, 1, HW, s));
+    if (pb->sa_mask) HIP_OK(ctx, hipMemcpyAsync(ctx->sa.p, pb->sa_mask, HW, hipMemcpyDefault, s));
+    else HIP_OK(ctx, hipMemsetAsync(ctx->sa.p, 0, HW, s));
+    // one read-back for everything the host needs to size the rest: the fp16-texel eligibility of the
+    // source images (a quarter-integer in [0, 256) -- 8-bit images and their INTER_LINEAR 2^-k
+    // downscales -- is exact in fp16 together with its horizontal differences, which FastTex::sample
+    // relies on; else fp32 quads), the WEAK count, the largest confidence and whether any SA label is set
+    bool tex_f16 = getenv("APD_TEX_F32") == nullptr;
+    {
+        int *stat = (int *)ctx->totals.p + 8;  // [8] f16 ok, [9] WEAK count, [10] max confidence, [11] SA any
+        const int init[4] = {1, 0, 0, 0};
+        HIP_OK(ctx, hipMemcpyAsync(stat, init, sizeof(init), hipMemcpyHostToDevice, s));
+        if (tex_f16) {
+            const size_t n = HW * NI;
+            hipLaunchKernelGGL(k_check_f16, dim3((unsigned)std::min<size_t>(blocks_for(n, BLOCK), 8192)), dim3(BLOCK), 0, s,
+                               (const float *)ctx->imgs.p, n, stat);
+        }
+        hipLaunchKernelGGL(k_problem_stats, dim3((unsigned)std::min<size_t>(blocks_for(HW, BLOCK), 4096)), dim3(BLOCK), 0, s,
+                           (const uint8_t *)ctx->weak.p, (const uint8_t *)ctx->conf.p, (const uint8_t *)ctx->sa.p, HW,
+                           stat + 1);
+        if ((st = check_launch(ctx, "problem statistics"))) return st;
+        HIP_OK(ctx, hipMemcpyAsync(ctx->host_stat, stat, 4 * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIP_OK(ctx, hipStreamSynchronize(s));
+        tex_f16 = tex_f16 && ctx->host_stat[0] != 0;
+    }
+    const int weak_count = P.use_APD ? ctx->host_stat[1] : 0;
+    const int max_conf = ctx->host_stat[2];
+    const int sa_any = ctx->host_stat[3];
+    const size_t qstride = tex_f16 ? (size_t)(W + 2) * (H + 1) : (size_t)(W + 1) * (H + 1);
+    if ((st = ensure(ctx, ctx->quad, qstride * N * (tex_f16 ? sizeof(uint32_t) : sizeof(float4))))) return st;
     std::vector<Cam> cams(NI);
     std::vector<SrcView> views(NI);
     for (int i = 0; i < NI; ++i) {
@@ -4006,28 +4050,6 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     precompute_views(pb->cameras, NI, views.data(), a);
     HIP_OK(ctx, hipMemcpyAsync(ctx->cams.p, cams.data(), NI * sizeof(Cam), hipMemcpyHostToDevice, s));
     HIP_OK(ctx, hipMemcpyAsync(ctx->views.p, views.data(), NI * sizeof(SrcView), hipMemcpyHostToDevice, s));
-    // priors (APD.cpp:612-683)
-    if (P.state != APD_FIRST_INIT && pb->init_planes)
-        HIP_OK(ctx, hipMemcpyAsync(ctx->plane.p, pb->init_planes, HW * sizeof(float4), hipMemcpyHostToDevice, s));
-    else
-        HIP_OK(ctx, hipMemsetAsync(ctx->plane.p, 0, HW * sizeof(float4), s));
-    int weak_count = 0;
-    if (P.use_APD && pb->weak_info) {
-        HIP_OK(ctx, hipMemcpyAsync(ctx->weak.p, pb->weak_info, HW, hipMemcpyHostToDevice, s));
-        for (size_t i = 0; i < HW; ++i) weak_count += pb->weak_info[i] == APD_WEAK;
-    } else {
-        HIP_OK(ctx, hipMemsetAsync(ctx->weak.p, APD_STRONG, HW, s));
-    }
-    if (P.use_APD && pb->confidence)
-        HIP_OK(ctx, hipMemcpyAsync(ctx->conf.p, pb->confidence, HW, hipMemcpyHostToDevice, s));
-    else
-        HIP_OK(ctx, hipMemsetAsync(ctx->conf.p, 1, HW, s));
-    int sa_any = 0;
-    if (pb->sa_mask) {
-        for (size_t i = 0; i < HW && !sa_any; ++i) sa_any = pb->sa_mask[i] != 0;
-    }
-    if (sa_any) HIP_OK(ctx, hipMemcpyAsync(ctx->sa.p, pb->sa_mask, HW, hipMemcpyHostToDevice, s));
-    else HIP_OK(ctx, hipMemsetAsync(ctx->sa.p, 0, HW, s));
     HIP_OK(ctx, hipMemsetAsync(ctx->vw.p, 0, HW * N, s));
     HIP_OK(ctx, hipMemsetAsync(ctx->cost.p, 0, HW * sizeof(float), s));
     HIP_OK(ctx, hipMemsetAsync(ctx->sel.p, 0, HW * sizeof(uint32_t), s));
@@ -4042,10 +4064,7 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
         HIP_OK(ctx, hipMemsetAsync(ctx->fit.p, 0, HW * sizeof(float4), s));
         if ((st = build_near_offsets(ctx))) return st;
         // per-level column distances for k_find_nearest_rows (confidence is an input here)
-        int maxc = 1;
-        if (pb->confidence)
-            for (size_t i = 0; i < HW; ++i) maxc = std::max<int>(maxc, pb->confidence[i]);
-        ctx->near_levels = maxc + 1;
+        ctx->near_levels = std::max(max_conf, 1) + 1;
         if (getenv("APD_NEAREST_RING") || (size_t)ctx->near_levels * HW > ((size_t)4 << 30)) ctx->near_levels = 0;
         if (ctx->near_levels && (st = ensure(ctx, ctx->near_g, (size_t)ctx->near_levels * HW))) return st;
     }
@@ -4445,18 +4464,19 @@ int32_t apd_get_results(apd_ctx *ctx, const apd_outputs *out) {
     hipStream_t s = ctx->stream;
     const Args &a = ctx->args;
     const size_t HW = (size_t)a.HW;
-    if (out->planes) HIP_OK(ctx, hipMemcpyAsync(out->planes, ctx->plane.p, HW * sizeof(float4), hipMemcpyDeviceToHost, s));
-    if (out->weak_info) HIP_OK(ctx, hipMemcpyAsync(out->weak_info, ctx->weak.p, HW, hipMemcpyDeviceToHost, s));
-    if (out->confidence) HIP_OK(ctx, hipMemcpyAsync(out->confidence, ctx->conf.p, HW, hipMemcpyDeviceToHost, s));
-    if (out->costs) HIP_OK(ctx, hipMemcpyAsync(out->costs, ctx->cost.p, HW * sizeof(float), hipMemcpyDeviceToHost, s));
+    // outputs may be host or device buffers (hipMemcpyDefault): scan_runner.py keeps them in HBM
+    if (out->planes) HIP_OK(ctx, hipMemcpyAsync(out->planes, ctx->plane.p, HW * sizeof(float4), hipMemcpyDefault, s));
+    if (out->weak_info) HIP_OK(ctx, hipMemcpyAsync(out->weak_info, ctx->weak.p, HW, hipMemcpyDefault, s));
+    if (out->confidence) HIP_OK(ctx, hipMemcpyAsync(out->confidence, ctx->conf.p, HW, hipMemcpyDefault, s));
+    if (out->costs) HIP_OK(ctx, hipMemcpyAsync(out->costs, ctx->cost.p, HW * sizeof(float), hipMemcpyDefault, s));
     if (out->selected_views)
-        HIP_OK(ctx, hipMemcpyAsync(out->selected_views, ctx->sel.p, HW * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    if (out->view_weights) HIP_OK(ctx, hipMemcpyAsync(out->view_weights, ctx->vw.p, HW * a.N, hipMemcpyDeviceToHost, s));
+        HIP_OK(ctx, hipMemcpyAsync(out->selected_views, ctx->sel.p, HW * sizeof(uint32_t), hipMemcpyDefault, s));
+    if (out->view_weights) HIP_OK(ctx, hipMemcpyAsync(out->view_weights, ctx->vw.p, HW * a.N, hipMemcpyDefault, s));
     if (out->anchors && a.use_apd && ctx->weak_count > 0)
         HIP_OK(ctx, hipMemcpyAsync(out->anchors, ctx->anchors.p, (size_t)ctx->weak_count * 9 * sizeof(short2),
-                                   hipMemcpyDeviceToHost, s));
+                                   hipMemcpyDefault, s));
     if (out->reliable_curve && ctx->want_curve)
-        HIP_OK(ctx, hipMemcpyAsync(out->reliable_curve, ctx->curve.p, HW * 61 * sizeof(float), hipMemcpyDeviceToHost, s));
+        HIP_OK(ctx, hipMemcpyAsync(out->reliable_curve, ctx->curve.p, HW * 61 * sizeof(float), hipMemcpyDefault, s));
     if (out->weak_count) *out->weak_count = ctx->weak_count;
     HIP_OK(ctx, hipStreamSynchronize(s));
     return APD_OK;

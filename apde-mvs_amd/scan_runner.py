@@ -4,13 +4,20 @@
         apde-mvs_amd/scan_runner.py --dense_folder SCAN [--dataset ETH3D] [--seed 24301]
 
 Runs the reference's whole depth schedule (main.cpp:290-367) over an MVSNet scan with the views of
-every pass sharded across ranks (rank r owns views r, r+W, ...). Within a pass a view depends on the
-other views only through their depth maps of the previous pass (geometric consistency / APD priors,
-APD.cpp:592-610), so the pass is Jacobi-ordered: every rank processes its views against the
-previous pass's maps, then ONE collective per pass -- an all-gather of the new depth maps, the only
-cross-view data -- gives every rank the inputs of the next pass. Each view's own normal / weak /
-confidence state stays on its owner. Results equal the `apd` binary with --ordering jacobi and are
-independent of the number of ranks. Owners write APD/<id>/{depths,normals,weak,confidence}.bin.
+every pass spread over the ranks. Within a pass a view depends on the other views only through their
+state of the previous pass (depth maps for geometric consistency / APD priors, APD.cpp:592-610, plus
+its own normals / pixel states / confidence), so the pass is Jacobi-ordered and its views are
+independent: the ranks take them from a dynamic queue (an atomic counter on the rendezvous store),
+longest first by the views' measured times in the previous pass -- per-view cost follows the WEAK
+fraction -- and the pass ends with ONE collective, an all-gather of the new view
+states, after which every rank holds every view's state. Results equal the `apd` binary with
+--ordering jacobi and do not depend on the number of ranks or on which rank took which view. Rank 0
+writes APD/<id>/{depths,normals,weak,confidence}.bin.
+
+On GPUs the whole scan state stays in HBM: each round's resized images are uploaded once, the view
+states live in torch tensors on the rank's device, libapd_hip.so reads its inputs from and writes
+its outputs to them (device pointers through the C ABI), the INTER_NEAREST prior resizes are index
+gathers on the device, and the all-gather runs device to device over RCCL (xGMI).
 
 Host decoding and resizing go through the same C++ host library as the `apd` binary
 (host/build/libapdhost.so); the PatchMatch itself is libapd_hip.so via apd_abi.Engine.
@@ -19,9 +26,9 @@ from __future__ import annotations
 
 import argparse
 import ctypes as C
-import math
 import os
 import sys
+import time
 from typing import Callable, Dict, List, Optional
 
 import numpy as np
@@ -122,92 +129,150 @@ def read_pairs(folder: str):
     return out
 
 
+def nearest_index(sw: int, sh: int, dw: int, dh: int):
+    """Source rows / columns of cv::resize INTER_NEAREST from sw x sh to dw x dh, in the host library's
+    arithmetic (host/image.cpp resize_nearest: floor(x * (1 / (dw / sw))) in double, clamped), so a
+    gather with them equals the C++ resize element for element."""
+    ifx, ify = 1.0 / (dw / sw), 1.0 / (dh / sh)
+    xo = np.minimum(np.floor(np.arange(dw, dtype=np.float64) * ifx).astype(np.int64), sw - 1)
+    yo = np.minimum(np.floor(np.arange(dh, dtype=np.float64) * ify).astype(np.int64), sh - 1)
+    return yo, xo
+
+
 class Exchange:
-    """The per-pass collective: all-gather of the owners' new depth maps (torch.distributed)."""
+    """The per-pass step across ranks (torch.distributed): a dynamic view queue on the rendezvous
+    store, and one all-gather of the new per-view state."""
 
     def __init__(self, world: int, rank: int, device: Optional[str]):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.world, self.rank, self.device = torch, dist, world, rank, device
+        self.store = dist.distributed_c10d._get_default_store()
 
-    def all_gather_depths(self, owned: Dict[int, np.ndarray], order: List[int], h: int, w: int):
+    def next_index(self, key: str) -> int:
+        """Dynamic work queue: every rank draws the next position of the pass's view order from one
+        atomic counter (TCPStore add), so a rank that finishes early takes more views."""
+        return int(self.store.add(key, 1)) - 1
+
+    def all_gather_state(self, mine: Dict[int, "object"], meta: Dict[int, float], h: int, w: int):
+        """Every rank's new view states ([6, h, w] float32: depth, normal xyz, weak, confidence) to every
+        rank, on the device with RCCL when the ranks run on GPUs (no host round trip), plus the views'
+        measured times for the next pass's queue order."""
         torch, dist = self.torch, self.dist
-        per = (len(order) + self.world - 1) // self.world
-        mine = [v for v in order[self.rank::self.world]]
-        buf = torch.zeros((per, h, w), dtype=torch.float32)
-        for k, v in enumerate(mine):
-            buf[k] = torch.from_numpy(owned[v])
-        if self.device:
-            buf = buf.to(self.device)
+        ids = sorted(mine)
+        lists = [None] * self.world
+        dist.all_gather_object(lists, [(v, meta[v]) for v in ids])
+        kmax = max(1, max(len(l) for l in lists))
+        dev = self.device or "cpu"
+        buf = torch.zeros((kmax, 6, h, w), dtype=torch.float32, device=dev)
+        for k, v in enumerate(ids):
+            buf[k] = mine[v]
         outs = [torch.empty_like(buf) for _ in range(self.world)]
         dist.all_gather(outs, buf)
-        res = {}
+        states, times = {}, {}
         for r in range(self.world):
-            host = outs[r].cpu().numpy()
-            for k, v in enumerate(order[r::self.world]):
-                res[v] = host[k].copy()
-        return res
+            for k, (v, t) in enumerate(lists[r]):
+                states[v] = outs[r][k]
+                times[v] = t
+        return states, times
 
     def barrier(self):
         self.dist.barrier()
 
 
+def _pack(depth, normal, weak, conf):
+    import torch
+    return torch.cat([depth[None], normal.permute(2, 0, 1), weak[None].float(), conf[None].float()], 0)
+
+
 def run_scan(folder: str, run_fn: Callable, rank: int = 0, world: int = 1, exchange: Optional[Exchange] = None,
              dataset: str = "ETH3D", use_sa: bool = True, use_impetus: bool = True, seed: int = 24301,
-             host: Optional[HostLib] = None, write: bool = True):
-    """The schedule of main.cpp:290-367 with Jacobi passes over the views owned by `rank`.
-    run_fn(ProblemArrays) -> apd_abi.Outputs. Returns {view: state} for the owned views."""
+             host: Optional[HostLib] = None, write: bool = True, device: Optional[str] = None):
+    """The schedule of main.cpp:290-367 with Jacobi passes. Within a pass the ranks take views from a
+    dynamic queue in longest-first order (the views' measured times in the previous pass: their cost
+    follows the WEAK fraction), and the pass ends with one all-gather of the new states. Per round
+    each image is decoded once and resized once (C++ host library), and -- with `device` -- kept on
+    the GPU with every view's state, so problems pass device pointers to libapd_hip.so and nothing
+    but the all-gather moves between passes. run_fn(ProblemArrays) -> outputs with planes, weak_info,
+    confidence (numpy, or torch tensors on `device`). Returns {view: state tensor [6, h, w]} (every
+    view on every rank)."""
+    import torch
     host = host or HostLib()
     problems = read_pairs(folder)
     order = [p[0] for p in problems]
-    owned_ids = order[rank::world]
-    imgs, cams = {}, {}
-    needed = set(owned_ids)
-    for ref, srcs, _ in problems:
-        if ref in needed:
-            needed.update(srcs)
+    prob = {p[0]: p for p in problems}
     ext = {p[0]: p[2] for p in problems}
     e0 = problems[0][2]
-    for v in sorted(needed):
-        imgs[v] = host.read_gray(os.path.join(folder, "images", f"{v:08d}{ext.get(v, e0)}")).astype(F32)
+    dev = torch.device(device) if device else torch.device("cpu")
+    needed = set(order)
+    for _, srcs, _ in problems:
+        needed.update(srcs)
+    gray, cams = {}, {}
+    for v in sorted(needed):  # decoded once per run (the apd binary's ImageCache)
+        gray[v] = host.read_gray(os.path.join(folder, "images", f"{v:08d}{ext.get(v, e0)}")).astype(F32)
         cams[v] = host.read_camera(os.path.join(folder, "cams", f"{v:08d}_cam.txt"))
-    H0, W0 = imgs[owned_ids[0]].shape if owned_ids else next(iter(imgs.values())).shape
+    H0, W0 = gray[order[0]].shape
     max_size, round_num = max(W0, H0), 1
     while max_size > 800:
         max_size //= 2
         round_num += 1
     geom_factor = 0.05 if dataset in ("TaT_a", "TaT_i") else 0.2
-    state: Dict[int, dict] = {}        # owned views: depth, normal, weak, conf
-    depths: Dict[int, np.ndarray] = {}  # every view's depth of the previous pass
     masks = os.path.join(folder, "sa_masks")
+    states: Dict[int, "torch.Tensor"] = {}  # every view: [6, h, w] of the previous pass
+    times: Dict[int, float] = {}
     iteration = 0
+    round_imgs: Dict[int, "torch.Tensor"] = {}
+    round_cams: Dict[int, dict] = {}
+    round_scale = [None]
+
+    def load_round(scale):
+        """Images and scaled cameras of one round: resized once per view (APD.cpp:562-590) and, with
+        a device, uploaded once for all of the round's passes."""
+        if round_scale[0] == scale:
+            return
+        round_imgs.clear()
+        round_cams.clear()
+        for v, img in gray.items():
+            cam = dict(cams[v])
+            ih, iw = img.shape
+            if scale != 1:
+                factor = F32(1.0) / F32(scale)
+                nc, nr = int(round(float(F32(iw) * factor))), int(round(float(F32(ih) * factor)))
+                sx, sy = F32(nc) / F32(iw), F32(nr) / F32(ih)
+                img = host.resize_linear(img, nc, nr)
+                K = cam["K"].copy()
+                K[0] *= sx; K[2] *= sx; K[4] *= sy; K[5] *= sy
+                cam["K"] = K
+            ih, iw = img.shape
+            cam["width"], cam["height"] = iw, ih
+            round_cams[v] = cam
+            round_imgs[v] = torch.from_numpy(np.ascontiguousarray(img)).to(dev)
+        round_scale[0] = scale
+
+    def fit(t, h, w):
+        """INTER_NEAREST resize of a [.., h0, w0] tensor (priors, APD.cpp:592-672) as an index gather."""
+        h0, w0 = t.shape[-2], t.shape[-1]
+        if (h0, w0) == (h, w):
+            return t
+        yo, xo = nearest_index(w0, h0, w, h)
+        yo, xo = torch.from_numpy(yo).to(t.device), torch.from_numpy(xo).to(t.device)
+        return t.index_select(-2, yo).index_select(-1, xo)
 
     def one_pass(i, pstate, use_apd, geom, peak):
-        nonlocal depths
+        nonlocal states, times
         scale = 2 ** (round_num - 1 - i)
-        w = h = None
-        for ref, srcs, _ in problems:
-            if ref not in owned_ids:
-                continue
+        load_round(scale)
+        h, w = round_imgs[order[0]].shape
+        # longest first: the previous pass's measured times (ties and the first pass: pair.txt order)
+        queue = sorted(order, key=lambda v: (-times.get(v, 0.0), order.index(v)))
+        mine, meta = {}, {}
+        key = f"apd_queue/{iteration}"
+        k = exchange.next_index(key) if exchange else 0
+        while k < len(queue):
+            ref = queue[k]
+            _, srcs, _ = prob[ref]
             ids = [ref] + srcs
-            images, cl = [], []
-            for k in ids:
-                cam = dict(cams[k])
-                img = imgs[k]
-                ih, iw = img.shape
-                if scale != 1:
-                    factor = F32(1.0) / F32(scale)
-                    nc, nr = int(round(float(F32(iw) * factor))), int(round(float(F32(ih) * factor)))
-                    sx, sy = F32(nc) / F32(iw), F32(nr) / F32(ih)
-                    img = host.resize_linear(img, nc, nr)
-                    K = cam["K"].copy()
-                    K[0] *= sx; K[2] *= sx; K[4] *= sy; K[5] *= sy
-                    cam["K"] = K
-                ih, iw = img.shape
-                cam["width"], cam["height"] = iw, ih
-                cl.append(cam)
-                images.append(img)
-            h, w = images[0].shape
+            cl = [round_cams[v] for v in ids]
             dmin = float(F32(cl[0]["depth_min"]) * F32(0.6))
             dmax = float(F32(cl[0]["depth_max"]) * F32(1.2))
             p = A.default_params(len(ids), dmin, dmax, state=pstate, use_APD=int(use_apd),
@@ -216,32 +281,37 @@ def run_scan(folder: str, run_fn: Callable, rank: int = 0, world: int = 1, excha
             if use_apd:
                 p.ransac_threshold = float(F32(0.01 - i * 0.00125))
                 p.rotate_time = min(int(2 ** i), 4)
-            arr = A.ProblemArrays(w, h, images, cl, p, seed=seed ^ (iteration << 32) ^ ref)
-            own = state.get(ref)
+            arr = A.ProblemArrays(w, h, [round_imgs[v] for v in ids], cl, p, seed=seed ^ (iteration << 32) ^ ref)
+            own = fit(states[ref], h, w) if ref in states else None
             if geom or use_apd:
-                arr.depths = [host.resize_nearest(depths[v], w, h) for v in ids]
+                arr.depths = [fit(states[v][0], h, w).contiguous() for v in ids]
             if use_apd:
-                arr.weak_info = host.resize_nearest(own["weak"], w, h)
-                arr.confidence = host.resize_nearest(own["conf"], w, h)
+                arr.weak_info = own[4].to(torch.uint8).contiguous()
+                arr.confidence = own[5].to(torch.uint8).contiguous()
                 if use_sa and os.path.isdir(masks):
-                    arr.sa_mask = host.resize_nearest(read_bin_mat(os.path.join(masks, f"{ref:08d}.bin")), w, h)
+                    sa = torch.from_numpy(read_bin_mat(os.path.join(masks, f"{ref:08d}.bin"))).to(dev)
+                    arr.sa_mask = fit(sa, h, w).contiguous()
             if pstate != A.FIRST_INIT:
-                d = host.resize_nearest(own["depth"], w, h)
-                n = host.resize_nearest(own["normal"], w, h)
-                arr.init_planes = np.concatenate([n, d[..., None]], -1).astype(F32)
+                arr.init_planes = torch.cat([own[1:4].permute(1, 2, 0), own[0][..., None]], -1).contiguous()
+            t0 = time.perf_counter()
             out = run_fn(arr)
-            d = out.planes[..., 3].copy()
-            wk = out.weak_info.copy()
+            el = time.perf_counter() - t0
+            planes = torch.as_tensor(out.planes, device=dev)
+            d = planes[..., 3].clone()
+            wk = torch.as_tensor(out.weak_info, device=dev).clone()
             bad = (d < F32(dmin)) | (d > F32(dmax))  # ProcessProblem epilogue (main.cpp:168-178)
             d[bad] = 0
             wk[bad] = A.UNKNOWN
-            conf = out.confidence.copy() if (geom or use_apd) else np.ones((h, w), np.uint8)
-            state[ref] = dict(depth=d, normal=out.planes[..., :3].copy(), weak=wk, conf=conf)
-        # the exchange step: every rank gets every view's new depth map
-        if h is None:  # a rank without views still takes part in the collective
-            h, w = (round(H0 / scale), round(W0 / scale))
-        new = {v: state[v]["depth"] for v in owned_ids}
-        depths = exchange.all_gather_depths(new, order, h, w) if exchange else dict(new)
+            conf = torch.as_tensor(out.confidence, device=dev) if (geom or use_apd) else \
+                torch.ones((h, w), dtype=torch.uint8, device=dev)
+            mine[ref] = _pack(d, planes[..., :3], wk, conf)
+            meta[ref] = el
+            k = exchange.next_index(key) if exchange else k + 1
+        # the exchange step: every rank gets every view's new state
+        if exchange:
+            states, times = exchange.all_gather_state(mine, meta, h, w)
+        else:
+            states, times = mine, meta
 
     for i in range(round_num):
         one_pass(i, A.FIRST_INIT if i == 0 else A.REFINE_INIT, i > 0, False, 6)
@@ -249,25 +319,30 @@ def run_scan(folder: str, run_fn: Callable, rank: int = 0, world: int = 1, excha
         for j in range(3):
             one_pass(i, A.REFINE_ITER, i > 0, True, max(4 - 2 * j, 2))
             iteration += 1
-    if write:
-        for v in owned_ids:
+    if write and rank == 0:
+        for v in order:
+            st = states[v].cpu()
             d = os.path.join(folder, "APD", f"{v:08d}")
             os.makedirs(d, exist_ok=True)
-            write_bin_mat(os.path.join(d, "depths.bin"), state[v]["depth"])
-            write_bin_mat(os.path.join(d, "normals.bin"), state[v]["normal"])
-            write_bin_mat(os.path.join(d, "weak.bin"), state[v]["weak"])
-            write_bin_mat(os.path.join(d, "confidence.bin"), state[v]["conf"])
+            write_bin_mat(os.path.join(d, "depths.bin"), st[0].numpy().copy())
+            write_bin_mat(os.path.join(d, "normals.bin"), st[1:4].permute(1, 2, 0).contiguous().numpy())
+            write_bin_mat(os.path.join(d, "weak.bin"), st[4].numpy().astype(np.uint8))
+            write_bin_mat(os.path.join(d, "confidence.bin"), st[5].numpy().astype(np.uint8))
     if exchange:
         exchange.barrier()  # every view written before any rank reports completion (fusion reads all)
-    return state
+    return states
 
 
-def hip_run_fn(device: int) -> Callable:
+def hip_run_fn(device: int, on_device: bool = False) -> Callable:
+    """The HIP engine as run_fn; with on_device the outputs stay in HBM as torch tensors (inputs may be
+    torch tensors on the same device: apd_set_problem / apd_get_results take device pointers)."""
     eng = A.Engine(device)
 
     def fn(arr):
         eng.set_problem(arr)
         eng.run()
+        if on_device:
+            return eng.results_device(arr.width, arr.height, f"cuda:{device}")
         return eng.results(A.Outputs(arr.width, arr.height, len(arr.images) - 1))
     fn.engine = eng
     return fn
@@ -293,10 +368,12 @@ def main():
             torch.cuda.set_device(local)
         dist.init_process_group(backend)
         exchange = Exchange(world, rank, f"cuda:{local}" if backend == "nccl" else None)
-    run_fn = hip_run_fn(local)
+    on_device = torch.cuda.is_available()
+    run_fn = hip_run_fn(local, on_device)
     run_scan(args.dense_folder, run_fn, rank, world, exchange, dataset=args.dataset,
              use_sa=args.use_sa.lower() in ("1", "true", "yes", "on"),
-             use_impetus=args.use_impetus.lower() in ("1", "true", "yes", "on"), seed=args.seed)
+             use_impetus=args.use_impetus.lower() in ("1", "true", "yes", "on"), seed=args.seed,
+             device=f"cuda:{local}" if on_device else None)
     if exchange:
         dist.destroy_process_group()
     if rank == 0:

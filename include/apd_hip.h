@@ -165,7 +165,12 @@ void apd_destroy(apd_ctx *ctx);
 const char *apd_last_error(const apd_ctx *ctx);
 
 /* Upload one problem: images (plus the LDS/quad gather layout built on device), cameras, priors,
-   masks, params. Device buffers are reused across problems of the same or smaller size. */
+   masks, params. Device buffers are reused across problems of the same or smaller size. Every array
+   pointer of the problem (images, depths, init_planes, weak_info, confidence, sa_mask) may be a host
+   pointer or a device pointer on the ctx's device (the copies use hipMemcpyDefault): a caller that
+   keeps a scan's images and depth maps resident in HBM passes device pointers and nothing crosses
+   PCIe. The per-problem statistics (WEAK count, largest confidence, SA labels present, fp16-texel
+   eligibility) are computed on the device. */
 int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *problem);
 
 /* Run the full RunPatchMatch kernel sequence (APD.cu:2663-2737) on the loaded problem. */
@@ -183,7 +188,8 @@ int32_t apd_stage_finish(apd_ctx *ctx);
 /* Block until every launch on the ctx stream completed. */
 int32_t apd_synchronize(apd_ctx *ctx);
 
-/* Copy results to host (GetPlaneHypothesis/GetPixelStates/GetConfidence, APD.cpp:816-826). */
+/* Copy results out (GetPlaneHypothesis/GetPixelStates/GetConfidence, APD.cpp:816-826); every
+   output pointer may be a host buffer or a device buffer on the ctx's device. */
 int32_t apd_get_results(apd_ctx *ctx, const apd_outputs *out);
 
 /* Device timing of the last apd_run_patchmatch. */

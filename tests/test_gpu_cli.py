@@ -116,3 +116,19 @@ def test_run_scans_drives_the_binary(tmp_path):
         assert os.path.getsize(root / name / "APD" / "APD.ply") > 0
         assert os.path.exists(root / name / "APD" / "00000000" / "depths.bin")
         assert "RunPatchMatch time" in (root / name / "APD" / "log.txt").read_text()
+
+
+def test_scan_runner_device_resident(scan, engine, tmp_path):
+    """scan_runner.py with the scan's state resident in HBM (torch tensors on cuda:0, device pointers
+    through apd_set_problem / apd_get_results, prior resizes as device index gathers): one rank, its
+    files equal the Jacobi schedule restated on the host (the same data as the apd binary's
+    --ordering jacobi) bit for bit."""
+    import shutil
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "apde-mvs_amd"))
+    import scan_runner as SR
+    folder = str(tmp_path / "run")
+    shutil.copytree(scan, folder)
+    SR.run_scan(folder, SR.hip_run_fn(0, on_device=True), 0, 1, None, device="cuda:0")
+    expected = HS.run_schedule(folder, run_engine(engine), ordering="jacobi")
+    check_outputs(folder, expected)

@@ -23,15 +23,25 @@ def _oracle_fn():
     return lambda arr: oracle_lib.run(lib, arr, nthreads=2)
 
 
-def _rank_main(rank, world, folder, port):
+def _rank_main(rank, world, folder, port, slow_rank=-1, log=None):
     import sys
+    import time
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, os.path.join(os.path.dirname(here), "apde-mvs_amd")]
     import torch.distributed as dist
     import scan_runner as SR
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    SR.run_scan(folder, _oracle_fn(), rank, world, SR.Exchange(world, rank, None))
+    fn = _oracle_fn()
+
+    def run_fn(arr):
+        if rank == slow_rank:
+            time.sleep(2.0)
+        if log:
+            with open(f"{log}.{rank}", "a") as fh:
+                fh.write(f"{arr.seed}\n")
+        return fn(arr)
+    SR.run_scan(folder, run_fn, rank, world, SR.Exchange(world, rank, None))
     dist.destroy_process_group()
 
 
@@ -88,3 +98,32 @@ def test_runner_matches_restated_host_io(scan):
     exp = HS.read_cam(os.path.join(folder, "cams", "00000001_cam.txt"))
     for k in ("K", "R", "t", "c"):
         assert np.array_equal(cam[k], exp[k])
+
+
+def test_dynamic_queue_balances_a_slow_rank(scan, tmp_path):
+    """The views of a pass come from a dynamic queue: with rank 0 slowed down, rank 1 takes more of
+    them, every (view, pass) is processed exactly once, and the files still equal the Jacobi schedule."""
+    folder, expected = scan
+    run = str(tmp_path / "run")
+    shutil.copytree(folder, run)
+    log = str(tmp_path / "seeds")
+    port = 31500 + (os.getpid() % 2000)
+    mp.spawn(_rank_main, args=(2, run, port, 0, log), nprocs=2, join=True)
+    _check(run, expected)
+    seeds = [open(f"{log}.{r}").read().split() for r in (0, 1)]
+    assert len(seeds[1]) > len(seeds[0])
+    allseeds = seeds[0] + seeds[1]
+    assert len(allseeds) == len(set(allseeds))  # seed = f(view, pass): no view ran twice in a pass
+    n_views = len(expected)
+    assert len(allseeds) % n_views == 0
+
+
+def test_nearest_index_equals_host_resize():
+    """The runner's INTER_NEAREST index gather == the C++ host resize (host/image.cpp) on an index map."""
+    import scan_runner as SR
+    host = SR.HostLib()
+    for (sw, sh, dw, dh) in [(96, 72, 48, 36), (50, 37, 100, 75), (61, 43, 33, 91), (31, 17, 31, 17)]:
+        idx = np.arange(sw * sh, dtype=np.int32).reshape(sh, sw)
+        ref = host.resize_nearest(idx, dw, dh)
+        yo, xo = SR.nearest_index(sw, sh, dw, dh)
+        assert np.array_equal(idx[yo][:, xo], ref)
