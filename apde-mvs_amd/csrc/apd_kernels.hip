@@ -28,6 +28,24 @@ using namespace apd;
 
 #define WAVE 64
 #define BLOCK 256
+// profiling slots: APD_PROF_COUNTERS public counters (apd_hip.h), then per-phase cycle sums of
+// instrumented builds (-DAPD_PHASE_STAMPS: wave 0 of every workgroup adds the clock64() delta of each
+// phase -- barrier to barrier -- to slot 8 + phase; read with apd_profile_counters(ctx, c, 32))
+#define APD_PROF_SLOTS 32
+#ifdef APD_PHASE_STAMPS
+#define PHASE_STAMP(i)                                                                       \
+    do {                                                                                     \
+        if (a.evals && threadIdx.x == 0) {                                                   \
+            const long long t_ = clock64();                                                  \
+            atomicAdd(a.evals + 8 + (i), (unsigned long long)(t_ - t_phase_));               \
+            t_phase_ = t_;                                                                   \
+        }                                                                                    \
+    } while (0)
+#define PHASE_BEGIN long long t_phase_ = clock64()
+#else
+#define PHASE_STAMP(i) do { } while (0)
+#define PHASE_BEGIN do { } while (0)
+#endif
 #ifndef APD_SWEEP_WAVES
 #define APD_SWEEP_WAVES 2  // min waves per SIMD requested for the sweep kernels (VGPR budget 512/w)
 #endif
@@ -1760,6 +1778,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
                                                                 int iter, const float *__restrict__ cand,
                                                                 const uint8_t *__restrict__ cand_done, int wc) {
     const int N = a.N, W = a.W;
+    PHASE_BEGIN;
     // direct: k_weak_cand_vm evaluated every pixel's anchor candidates (no SA masks: no group is left
     // to the sweep), so P2 reads their costs from `cand` and the table is [N][64] (current plane),
     // later [5][N][64] (wv_lds_bytes)
@@ -1821,6 +1840,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         wv_build_windows<F16>(a, L, p1, anc, cid, wave, WV_WAVES);
     }
     __syncthreads();
+    PHASE_STAMP(0);
 
     // ---- P1: (hypothesis, view) tasks; where k_weak_cand_vm handled this group (`cand_done`), the
     // anchor candidates' costs are read, and only the current plane is evaluated here
@@ -1852,6 +1872,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         costL[t * VM_P + p1] = val;
     }
     __syncthreads();
+    PHASE_STAMP(1);
 
     // ---- P2: lane = (pixel, view) groups
     const int Gp = WAVE / N;
@@ -1958,6 +1979,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         }
     }
     __syncthreads();
+    PHASE_STAMP(2);
     const bool refine = pv1 && (L.flags[p1] >> 31) != 0u;
     const float4 fit1 = a.fit[c1];
     uint32_t issued_nn = 0, issued_g = 0;  // profiling: P3/P5 evaluations this lane issued
@@ -2017,6 +2039,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         }
         __syncthreads();
     }
+    PHASE_STAMP(3);
 
     // ---- P4: fit acceptance, refinement candidates (PlaneHypothesisRefinementWeak, APD.cu:1008-1067)
     if (wave == 0 && refine) {
@@ -2049,6 +2072,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         L.st[1 * VM_P + p1] = cost_now;
     }
     __syncthreads();
+    PHASE_STAMP(4);
 
     // ---- P5: candidate tasks (views with weight > 0), view-major, early exit against the cost after
     // the fit plane (slots 1..5)
@@ -2072,6 +2096,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         }
         __syncthreads();
     }
+    PHASE_STAMP(5);
 
     if (a.evals && wave == 0) {
         // profiling: the NCC-New evaluations and geometric terms CheckerboardPropagationWeak issues
@@ -2128,6 +2153,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             }
         }
     }
+    PHASE_STAMP(6);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2241,6 +2267,7 @@ __device__ __forceinline__ int pk_compact(const bool (&used)[PER], int (&ids)[PE
 template <bool F16>
 __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a, const int *__restrict__ list, int count,
                                                            float *__restrict__ out, uint8_t *__restrict__ done, int wc) {
+    PHASE_BEGIN;
     const int N = a.N, W = a.W, H = a.H;
     PkLds<F16> &L = *reinterpret_cast<PkLds<F16> *>(apd_dyn_lds);
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
@@ -2518,6 +2545,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
     const int nP = L.nP;
 
     if (pv1 && wave == 0) done[wi1] = 1;
+    PHASE_STAMP(8);
     // ---- D: per view
     for (int v = 0; v < N; ++v) {
         const int s = v + 1;
@@ -2552,6 +2580,10 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
             }
             if (act) L.u.pcost[pid] = res;
         }
+#ifdef APD_PHASE_STAMPS
+        __syncthreads();  // instrumented builds only: pair windows and centre windows timed apart
+        PHASE_STAMP(9);
+#endif
         // centre windows: lane = pixel, wave = candidate
         {
             const uint32_t cb = pv1 ? L.cand[p1] : 0u;
@@ -2589,6 +2621,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
             }
         }
         __syncthreads();
+        PHASE_STAMP(10);
         // focal combination (APD.cu:576-593, Softmax 431-446) per (candidate, pixel)
         if (pv1) {
             const uint32_t cb = L.cand[p1];
@@ -2635,6 +2668,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
             }
         }
         __syncthreads();
+        PHASE_STAMP(11);
     }
 }
 
@@ -4496,9 +4530,9 @@ int32_t apd_profile_reset(apd_ctx *ctx, int32_t enable) {
     ctx->prof_ev.clear();
     ctx->prof = enable != 0;
     if (ctx->prof) {
-        int st = ensure(ctx, ctx->evals, APD_PROF_COUNTERS * sizeof(unsigned long long));
+        int st = ensure(ctx, ctx->evals, APD_PROF_SLOTS * sizeof(unsigned long long));
         if (st) return st;
-        HIP_OK(ctx, hipMemsetAsync(ctx->evals.p, 0, APD_PROF_COUNTERS * sizeof(unsigned long long), ctx->stream));
+        HIP_OK(ctx, hipMemsetAsync(ctx->evals.p, 0, APD_PROF_SLOTS * sizeof(unsigned long long), ctx->stream));
     }
     return APD_OK;
 }
@@ -4507,9 +4541,9 @@ int32_t apd_profile_counters(apd_ctx *ctx, int64_t *counts, int32_t n) {
     if (!ctx || !counts || n < 0) return APD_EINVAL;
     (void)hipSetDevice(ctx->device);
     HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
-    unsigned long long c[APD_PROF_COUNTERS] = {};
+    unsigned long long c[APD_PROF_SLOTS] = {};
     if (ctx->evals.p) HIP_OK(ctx, hipMemcpy(c, ctx->evals.p, sizeof(c), hipMemcpyDeviceToHost));
-    for (int i = 0; i < n; ++i) counts[i] = i < APD_PROF_COUNTERS ? (int64_t)c[i] : 0;
+    for (int i = 0; i < n; ++i) counts[i] = i < APD_PROF_SLOTS ? (int64_t)c[i] : 0;
     return APD_OK;
 }
 
