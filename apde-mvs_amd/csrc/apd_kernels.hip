@@ -1914,6 +1914,9 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         const int w = view_selection(ca, prior, iter, rg, G, N);
         const uint32_t tsel = group_bits(w > 0, G);
         float gval[8];
+#ifdef APD_PHASE_STAMPS
+        const long long tg0_ = clock64();
+#endif
 #pragma unroll 1
         for (int j = 0; j < 8; ++j) {
             float cj = ca[0];
@@ -1925,6 +1928,9 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
 #pragma unroll
             for (int k = 0; k < 8; ++k) if (j == k) gval[k] = vv;
         }
+#ifdef APD_PHASE_STAMPS
+        if (a.evals && threadIdx.x == 0) atomicAdd(a.evals + 8 + 7, (unsigned long long)(clock64() - tg0_));
+#endif
         float fc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         float wn = 0.0f, cost_now = 0.0f;
         for (int k = 0; k < N; ++k) {
@@ -4379,8 +4385,10 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
                 return APD_ESTATE;
             }
             e0 = prof_begin(ctx);
+            Args ac = a;
+            ac.evals = evals;  // (only instrumented builds write it)
             LAUNCH_TEX(k_weak_cand_vm, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK),
-                       (ctx->args.tex_f16 ? pk_lds_bytes<true>() : pk_lds_bytes<false>()), s, a,
+                       (ctx->args.tex_f16 ? pk_lds_bytes<true>() : pk_lds_bytes<false>()), s, ac,
                        (const int *)ctx->wlist.p, nw, (float *)ctx->wcand.p, (uint8_t *)ctx->wdone.p, wc);
             prof_end(ctx, e0, APD_PROF_WEAK_CAND, nw);
             cand = (const float *)ctx->wcand.p;

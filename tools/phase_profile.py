@@ -29,5 +29,7 @@ for lo, hi, title in ((8, 12, "k_weak_cand_vm"), (0, 7, "k_sweep_weak_vm")):
     print(title)
     for i in range(lo, hi):
         print(f"  {names[i]:32s} {100.0 * c[8 + i] / tot:6.1f} %")
+    if lo == 0:
+        print(f"  (of P2: geometric terms, thread 0's own time {100.0 * c[15] / max(c[10], 1):5.1f} %)")
 t = eng.timing()
 print(f"iteration ms {list(t.iter_ms)[:t.iterations]}")
