@@ -1481,7 +1481,8 @@ struct WvRefT {
     float wsr[9 * VM_P], wsrr[9 * VM_P];  // per window moments over its valid taps
     int anc[9 * VM_P];           // packed (x, y) of anchors 0..8, -1 = none
     uint32_t flags[VM_P];        // bits 0-8: hypothesis h present (anchor STRONG); 16-24: window k evaluated
-                                 // (anchor present and SA label matches); 31: refine (fit normal != 0)
+                                 // (anchor present and SA label matches); 25-27: the best anchor
+                                 // hypothesis (Weak sweep P2a); 31: refine (fit normal != 0)
     // [tap][p]: window 0 taps 0..35 (6x6, step 2), anchor k taps 36+9(k-1).. (3x3, step 5); fp16 when
     // the images are (exactly) fp16-representable, see apd_set_problem
     typename std::conditional<F16, _Float16, float>::type rref[108 * VM_P];
@@ -1495,6 +1496,7 @@ struct WvLdsT : WvRefT<F16> {
                                  // with the refinement candidates (WV_CAND) after P2's last read
     float4 pnow[VM_P];
     float st[4 * VM_P];          // depth_now, cost_now, cost_init, weight norm
+    uint32_t tsel[VM_P];         // views with weight > 0 (the selection the best anchor hypothesis brings)
     uint16_t rng_n[VM_P];
 };
 #define WV_CAND(L) ((L).hyp)
@@ -1842,39 +1844,33 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     __syncthreads();
     PHASE_STAMP(0);
 
-    // ---- P1: (hypothesis, view) tasks; where k_weak_cand_vm handled this group (`cand_done`), the
-    // anchor candidates' costs are read, and only the current plane is evaluated here
+    // ---- P1: (anchor hypothesis, view) tasks, lane = pixel; where k_weak_cand_vm handled this group
+    // (`cand_done`) the candidates' costs are read instead (direct: P2 reads them itself, no tasks).
+    // The current plane is evaluated after the view selection (P1b), for the views it weights only:
+    // cost_now = sum of fmaf(w_v, c_v) over all views, and a weight-0 view adds fmaf(0, c_v, .) == the
+    // sum itself (c_v finite), so its value is never needed.
     const int wi1 = cand ? a.amap[c1] : 0;
     const bool cand_ok = cand && pv1 && cand_done[wi1];  // per pixel (groups of k_weak_cand_vm span both colours)
-    const int ntask = direct ? N : 9 * N;
+    const int ntask = direct ? 0 : 8 * N;
     for (int u = wave; u < ntask; u += WV_WAVES) {  // view-major: the waves share a source image
-        const int v = direct ? u : u / 9, h = direct ? 8 : u - 9 * v, t = direct ? v : h * N + v;
+        const int v = u / 8, h = u - 8 * v, t = h * N + v;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
-        const bool want = pv1 && (h == 8 || ((L.flags[p1] >> h) & 1u));
-        if (cand && h < 8 && !__ballot(want && !cand_ok)) {  // every lane that needs it has its cost
+        const bool want = pv1 && ((L.flags[p1] >> h) & 1u);
+        if (cand && !__ballot(want && !cand_ok)) {  // every lane that needs it has its cost
             if (want) val = cand[((size_t)v * 8 + h) * (size_t)wc + wi1];
             costL[t * VM_P + p1] = val;
             continue;
         }
         const float4 pl = L.hyp[h * VM_P + p1];
-        float nv;
-        // iteration 0: the current plane is RandomInitialization's, whose NCC-New it kept (a.wcur)
-        // unless the value read a selected view; the task runs only if a lane lacks it
-        const float kept = (h == 8 && iter == 0 && a.wcur && want) ? a.wcur[(size_t)v * a.HW + c1] : 0.0f;
-        if (h == 8 && iter == 0 && a.wcur && !__ballot(want && __builtin_isnan(kept)))
-            nv = kept;
-        else
-            nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want);
-        if (want) {
-            val = nv;
-            if (h == 8 && geom) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
-        }
+        const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want);
+        if (want) val = nv;
         costL[t * VM_P + p1] = val;
     }
     __syncthreads();
     PHASE_STAMP(1);
 
-    // ---- P2: lane = (pixel, view) groups
+    // ---- P2a: lane = (pixel, view) groups: view selection, the anchor hypotheses' weighted costs
+    // (with their geometric terms) and their argmin
     const int Gp = WAVE / N;
     const int ppr = WV_WAVES * Gp;
     for (int r0 = 0; r0 < np; r0 += ppr) {
@@ -1898,17 +1894,14 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             if (pk >= 0) prior += ((a.sel[(pk & 0xFFFF) + (pk >> 16) * W] >> v) & 1u) ? 0.9f : 0.1f;
         }
         float ca[8];
-        float cv_now;
         if (direct) {  // the candidates' costs from k_weak_cand_vm; absent ones as P1 sets them
             const size_t wi = (size_t)a.amap[c];
 #pragma unroll
             for (int h = 0; h < 8; ++h)
                 ca[h] = ((hflag >> h) & 1u) ? cand[((size_t)v * 8 + h) * (size_t)wc + wi] : ((h == 0 && v == 0) ? 2.0f : 0.0f);
-            cv_now = costL[v * VM_P + p];
         } else {
 #pragma unroll
             for (int h = 0; h < 8; ++h) ca[h] = costL[(h * N + v) * VM_P + p];
-            cv_now = costL[(8 * N + v) * VM_P + p];
         }
         Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c, ord_weak(iter));
         const int w = view_selection(ca, prior, iter, rg, G, N);
@@ -1932,7 +1925,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         if (a.evals && threadIdx.x == 0) atomicAdd(a.evals + 8 + 7, (unsigned long long)(clock64() - tg0_));
 #endif
         float fc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        float wn = 0.0f, cost_now = 0.0f;
+        float wn = 0.0f;
         for (int k = 0; k < N; ++k) {
             const int wk = __shfl(w, G.base + k);
             const float fwk = (float)wk;
@@ -1942,47 +1935,80 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
                 if (wk > 0) fc[j] = fmaf(fwk, vk, fc[j]);
             }
             if (wk > 0) wn += fwk;
-            cost_now = fmaf(fwk, __shfl(cv_now, G.base + k), cost_now);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) fc[j] /= wn;
-        cost_now /= wn;
-        const float cost_init = cost_now;
         int mi = 0;
-        {
-            float m = fc[0];
+        float fcm = fc[0];
 #pragma unroll
-            for (int j = 1; j < 8; ++j) if (fc[j] <= m) { m = fc[j]; mi = j; }
-        }
-        const float4 cur = L.hyp[8 * VM_P + p];
-        float depth_now = depth_from_plane(cam0, cur, px, py);
-        float4 pnow = cur;
-        {
-            float fcm = fc[0];
-#pragma unroll
-            for (int k = 1; k < 8; ++k) if (mi == k) fcm = fc[k];
-            if ((hflag >> mi) & 1u) {
-                const float4 cand = L.hyp[mi * VM_P + p];
-                const float db = depth_from_plane(cam0, cand, px, py);
-                if (db >= a.dmin && db <= a.dmax && fcm < cost_now) {
-                    depth_now = db; pnow = cand; cost_now = fcm;
-                    if (G.valid && G.v == 0) a.sel[c] = tsel;
-                }
-            }
-        }
+        for (int j = 1; j < 8; ++j) if (fc[j] <= fcm) { fcm = fc[j]; mi = j; }
         if (G.valid) {
             wts[v * VM_P + p] = (uint8_t)w;
             if (G.v == 0) {
                 const float4 fit = a.fit[c];
-                L.pnow[p] = pnow;
-                L.st[0 * VM_P + p] = depth_now;
-                L.st[1 * VM_P + p] = cost_now;
-                L.st[2 * VM_P + p] = cost_init;
+                L.st[2 * VM_P + p] = fcm;  // (P1c: the argmin's weighted cost, then cost_init)
                 L.st[3 * VM_P + p] = wn;
-                if (!(fit.x == 0 && fit.y == 0 && fit.z == 0)) L.flags[p] |= 1u << 31;
+                L.tsel[p] = tsel;
+                uint32_t fl = (L.flags[p] & ~(7u << 25)) | ((uint32_t)mi << 25);
+                if (!(fit.x == 0 && fit.y == 0 && fit.z == 0)) fl |= 1u << 31;
+                L.flags[p] = fl;
                 L.rng_n[p] = (uint16_t)rg.n;  // a few dozen draws
             }
         }
+    }
+    __syncthreads();
+
+    // ---- P1b: current-plane tasks, lane = pixel, for the views with weight > 0
+    const int cur_row = direct ? 0 : 8 * N;
+    for (int v = wave; v < N; v += WV_WAVES) {
+        float val = 0.0f;
+        const bool want = pv1 && wts[v * VM_P + p1] > 0;
+        if (__ballot(want)) {
+            const float4 pl = L.hyp[8 * VM_P + p1];
+            float nv;
+            // iteration 0: the current plane is RandomInitialization's, whose NCC-New it kept (a.wcur)
+            // unless the value read a selected view; the task runs only if a lane lacks it
+            const float kept = (iter == 0 && a.wcur && want) ? a.wcur[(size_t)v * a.HW + c1] : 0.0f;
+            if (iter == 0 && a.wcur && !__ballot(want && __builtin_isnan(kept)))
+                nv = kept;
+            else
+                nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want);
+            if (want) {
+                val = nv;
+                if (geom) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
+            }
+        }
+        costL[(cur_row + v) * VM_P + p1] = val;
+    }
+    __syncthreads();
+
+    // ---- P1c: lane = pixel (wave 0): the current plane's cost, acceptance of the best anchor hypothesis
+    if (wave == 0 && pv1) {
+        const float wn = L.st[3 * VM_P + p1];
+        float cost_now = 0.0f;
+        for (int k = 0; k < N; ++k) {
+            const int wk = wts[k * VM_P + p1];
+            if (wk > 0) cost_now = fmaf((float)wk, costL[(cur_row + k) * VM_P + p1], cost_now);
+        }
+        cost_now /= wn;
+        const float cost_init = cost_now;
+        const int mi = (int)((L.flags[p1] >> 25) & 7u);
+        const float fcm = L.st[2 * VM_P + p1];
+        const float4 cur = L.hyp[8 * VM_P + p1];
+        float depth_now = depth_from_plane(cam0, cur, px1, py1);
+        float4 pnow = cur;
+        if ((L.flags[p1] >> mi) & 1u) {
+            const float4 cnd = L.hyp[mi * VM_P + p1];
+            const float db = depth_from_plane(cam0, cnd, px1, py1);
+            if (db >= a.dmin && db <= a.dmax && fcm < cost_now) {
+                depth_now = db; pnow = cnd; cost_now = fcm;
+                a.sel[c1] = L.tsel[p1];
+            }
+        }
+        L.pnow[p1] = pnow;
+        L.st[0 * VM_P + p1] = depth_now;
+        L.st[1 * VM_P + p1] = cost_now;
+        L.st[2 * VM_P + p1] = cost_init;
     }
     __syncthreads();
     PHASE_STAMP(2);
@@ -2115,8 +2141,8 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             int nsel = 0;
             for (int v = 0; v < N; ++v) nsel += wts[v * VM_P + p1] > 0;
             const int nh = __builtin_popcount(L.flags[p1] & 0xFFu);
-            nn = (uint32_t)((nh + 1) * N);
-            ng = geom ? (uint32_t)(nh * nsel + N) : 0u;
+            nn = (uint32_t)(nh * N + nsel);
+            ng = geom ? (uint32_t)(nh * nsel + nsel) : 0u;
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) { nn += __shfl_xor(nn, o); ng += __shfl_xor(ng, o); }

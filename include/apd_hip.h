@@ -213,11 +213,11 @@ int32_t apd_profile_query(apd_ctx *ctx, double *sweep_ms_total, int64_t *sweep_l
    upper bound. counts[0..n-1] (n <= APD_PROF_COUNTERS; extra entries are zeroed):
    [0] NCC-Old evaluations the Strong sweep launches issued (valid propagation candidates + current
        plane + refinement candidates of views with weight > 0);
-   [1] NCC-New evaluations of the Weak sweep: valid anchor candidates x N + current plane x N (the
-       values CheckerboardPropagationWeak needs, however the engine obtained them: shared anchor
-       windows in k_weak_cand_vm, RandomInitialization's kept costs, or the sweep itself), plus the
-       fit-plane and refinement-candidate evaluations of views with weight > 0 the sweep actually
-       issued (those its exact early exit proves unnecessary are not counted);
+   [1] NCC-New evaluations of the Weak sweep: valid anchor candidates x N + current plane x views
+       with weight > 0 (the values CheckerboardPropagationWeak needs, however the engine obtained
+       them: shared anchor windows in k_weak_cand_vm, RandomInitialization's kept costs, or the
+       sweep itself), plus the fit-plane and refinement-candidate evaluations of views with weight
+       > 0 the sweep actually issued (those its exact early exit proves unnecessary are not counted);
    [2] geometric-consistency terms of the same evaluations (APD.cu:1561, 1583, 1037, 1079).
    apd_profile_evaluations(ctx, &n) == apd_profile_counters(ctx, &n, 1). */
 #define APD_PROF_COUNTERS 4
