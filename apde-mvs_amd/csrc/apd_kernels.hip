@@ -3727,6 +3727,40 @@ __global__ __launch_bounds__(BLOCK) void k_local_refine(Args a) {
     if (run && G.valid && G.v == 0 && (double)(cost_now - min_cost) > 0.1) a.plane[c].w = best;
 }
 
+// cv::resize INTER_NEAREST between device buffers with the host library's index arithmetic
+// (host/image.cpp resize_nearest: floor(x * (1 / (dw / sw))) in double, clamped to the source)
+__global__ __launch_bounds__(BLOCK) void k_resize_nearest(const uint8_t *__restrict__ src, int sw, int sh,
+                                                        uint8_t *__restrict__ dst, int dw, int dh, int elem) {
+    const double ifx = 1.0 / ((double)dw / sw), ify = 1.0 / ((double)dh / sh);
+    const size_t n = (size_t)dw * dh;
+    for (size_t i = blockIdx.x * (size_t)BLOCK + threadIdx.x; i < n; i += (size_t)gridDim.x * BLOCK) {
+        const int y = (int)(i / dw), x = (int)(i - (size_t)y * dw);
+        const int sx = min((int)floor(x * ifx), sw - 1), sy = min((int)floor(y * ify), sh - 1);
+        const uint8_t *s = src + ((size_t)sy * sw + sx) * elem;
+        uint8_t *d = dst + i * elem;
+        if (elem == 4) {
+            *reinterpret_cast<uint32_t *>(d) = *reinterpret_cast<const uint32_t *>(s);
+        } else if (elem == 16) {
+            *reinterpret_cast<uint4 *>(d) = *reinterpret_cast<const uint4 *>(s);
+        } else {
+            for (int b = 0; b < elem; ++b) d[b] = s[b];
+        }
+    }
+}
+
+// ProcessProblem's epilogue (main.cpp:168-178) on the device: depth = plane.w, 0 outside
+// [depth_min, depth_max] (NaN kept, as apd_epilogue); planes_out = (normal, that depth)
+__global__ __launch_bounds__(BLOCK) void k_result_epilogue(const float4 *__restrict__ planes, size_t n, float dmin,
+                                                         float dmax, float *__restrict__ depth_out,
+                                                         float4 *__restrict__ planes_out) {
+    for (size_t i = blockIdx.x * (size_t)BLOCK + threadIdx.x; i < n; i += (size_t)gridDim.x * BLOCK) {
+        float4 p = planes[i];
+        if (p.w < dmin || p.w > dmax) p.w = 0.0f;
+        if (depth_out) depth_out[i] = p.w;
+        if (planes_out) planes_out[i] = p;
+    }
+}
+
 // =============================================================================================
 // host side: context, buffers, C ABI
 // =============================================================================================
@@ -4608,6 +4642,65 @@ int32_t apd_profile_kernel(apd_ctx *ctx, int32_t kind, double *ms_total, int64_t
 
 int32_t apd_profile_query(apd_ctx *ctx, double *sweep_ms_total, int64_t *sweep_launches, int64_t *sweep_pixels) {
     return apd_profile_kernel(ctx, APD_PROF_STRONG_SWEEP, sweep_ms_total, sweep_launches, sweep_pixels);
+}
+
+int32_t apd_device_alloc(apd_ctx *ctx, size_t bytes, void **ptr) {
+    if (!ctx || !ptr) return APD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    *ptr = nullptr;
+    if (hipMalloc(ptr, bytes ? bytes : 16) != hipSuccess) {
+        (void)hipGetLastError();
+        *ptr = nullptr;
+        ctx->err = "hipMalloc(" + std::to_string(bytes) + ") failed";
+        return APD_ENOMEM;
+    }
+    return APD_OK;
+}
+
+int32_t apd_device_free(apd_ctx *ctx, void *ptr) {
+    if (!ctx) return APD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    if (ptr) {
+        HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_OK(ctx, hipFree(ptr));
+    }
+    return APD_OK;
+}
+
+int32_t apd_device_copy(apd_ctx *ctx, void *dst, const void *src, size_t bytes) {
+    if (!ctx || (!dst && bytes) || (!src && bytes)) return APD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    HIP_OK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, ctx->stream));
+    HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+    return APD_OK;
+}
+
+int32_t apd_device_resize_nearest(apd_ctx *ctx, const void *src, int32_t sw, int32_t sh, void *dst, int32_t dw,
+                                  int32_t dh, int32_t elem_bytes) {
+    if (!ctx || !src || !dst || sw < 1 || sh < 1 || dw < 1 || dh < 1 || elem_bytes < 1) return APD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    const size_t n = (size_t)dw * dh;
+    hipLaunchKernelGGL(k_resize_nearest, dim3((unsigned)std::min<size_t>(blocks_for(n, BLOCK), 65535)), dim3(BLOCK), 0,
+                       ctx->stream, (const uint8_t *)src, sw, sh, (uint8_t *)dst, dw, dh, elem_bytes);
+    int st = check_launch(ctx, "k_resize_nearest");
+    if (st) return st;
+    HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+    return APD_OK;
+}
+
+int32_t apd_result_device(apd_ctx *ctx, float *depth_dev, float *planes_dev) {
+    if (!ctx) return APD_EINVAL;
+    if (!ctx->loaded) return APD_ESTATE;
+    (void)hipSetDevice(ctx->device);
+    const Args &a = ctx->args;
+    const size_t n = (size_t)a.HW;
+    hipLaunchKernelGGL(k_result_epilogue, dim3((unsigned)std::min<size_t>(blocks_for(n, BLOCK), 65535)), dim3(BLOCK), 0,
+                       ctx->stream, (const float4 *)ctx->plane.p, n, ctx->params.depth_min, ctx->params.depth_max,
+                       depth_dev, (float4 *)planes_dev);
+    int st = check_launch(ctx, "k_result_epilogue");
+    if (st) return st;
+    HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+    return APD_OK;
 }
 
 int32_t apd_epilogue(int32_t width, int32_t height, const float *planes, float depth_min, float depth_max,

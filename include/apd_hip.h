@@ -224,6 +224,22 @@ int32_t apd_profile_query(apd_ctx *ctx, double *sweep_ms_total, int64_t *sweep_l
 int32_t apd_profile_counters(apd_ctx *ctx, int64_t *counts, int32_t n);
 int32_t apd_profile_evaluations(apd_ctx *ctx, int64_t *ncc_evaluations);
 
+/* Device memory for hosts that keep a scan resident in HBM without linking HIP themselves (the `apd`
+   binary; APD.cpp:687-788 re-uploads every image and prior per problem instead). Allocations live on
+   the ctx's device; copies go in any direction (hipMemcpyDefault) and return when done. */
+int32_t apd_device_alloc(apd_ctx *ctx, size_t bytes, void **ptr);
+int32_t apd_device_free(apd_ctx *ctx, void *ptr);
+int32_t apd_device_copy(apd_ctx *ctx, void *dst, const void *src, size_t bytes);
+/* cv::resize INTER_NEAREST (the priors' resize, APD.cpp:605-672) from a device buffer of sw x sh
+   elements of elem_bytes to one of dw x dh, with the host library's index arithmetic. */
+int32_t apd_device_resize_nearest(apd_ctx *ctx, const void *src, int32_t sw, int32_t sh, void *dst,
+                                  int32_t dw, int32_t dh, int32_t elem_bytes);
+/* The last run's results after ProcessProblem's epilogue (main.cpp:168-178), on the device: depth
+   (H*W fp32; 0 outside [depth_min, depth_max], as apd_epilogue) and/or planes (H*W x (normal xyz,
+   that depth)) -- exactly the depths.bin and the (normals.bin, depths.bin) pair the next pass reads
+   as priors. Either pointer may be NULL. */
+int32_t apd_result_device(apd_ctx *ctx, float *depth_dev, float *planes_dev);
+
 /* Host epilogue of ProcessProblem (main.cpp:168-178): depth = plane.w clipped to
    [depth_min, depth_max] (else 0 and PixelState UNKNOWN), normal = plane.xyz. Pure host code. */
 int32_t apd_epilogue(int32_t width, int32_t height, const float *planes, float depth_min,
