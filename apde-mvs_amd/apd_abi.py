@@ -212,9 +212,23 @@ class ApdFusionView(C.Structure):  # include/apd_fusion.h
                 ("depth", C.c_void_p), ("normal", C.c_void_p), ("weak", C.c_void_p), ("confidence", C.c_void_p)]
 
 
+def torch_runtime_first():
+    """One HIP runtime per process. torch ships its own libamdhip64 (soname libamdhip64.so.7) and its
+    libraries load it by the file name libamdhip64.so: loaded after ours (/opt/rocm's, the same
+    soname) it would be a second runtime, which finds no GPU. Loaded first, it satisfies our
+    dependency too, so torch tensors and this library share one runtime (device pointers pass
+    through the C ABI). Call before loading anything that links libapd_hip.so; without torch the
+    library uses /opt/rocm's runtime."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load_library(path: str = LIB_PATH) -> C.CDLL:
     if not os.path.exists(path):
         raise ApdError(f"libapd_hip.so not built at {path}: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    torch_runtime_first()
     lib = C.CDLL(path)
     lib.apd_abi_version.restype = C.c_int32
     lib.apd_device_count.restype = C.c_int32
@@ -246,6 +260,17 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
                                        C.POINTER(C.c_int64)]
     lib.apd_profile_counters.restype = C.c_int32
     lib.apd_profile_counters.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.c_int32]
+    lib.apd_device_alloc.restype = C.c_int32
+    lib.apd_device_alloc.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]
+    lib.apd_device_free.restype = C.c_int32
+    lib.apd_device_free.argtypes = [C.c_void_p, C.c_void_p]
+    lib.apd_device_copy.restype = C.c_int32
+    lib.apd_device_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+    lib.apd_device_resize_nearest.restype = C.c_int32
+    lib.apd_device_resize_nearest.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
+                                              C.c_int32, C.c_int32]
+    lib.apd_result_device.restype = C.c_int32
+    lib.apd_result_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.apd_fusion_create.restype = C.c_void_p
     lib.apd_fusion_create.argtypes = [C.c_int32]
     lib.apd_fusion_destroy.argtypes = [C.c_void_p]
@@ -381,6 +406,25 @@ class Engine:
         s.confidence = _ptr(o.confidence, C.c_uint8)
         self._check(self.lib.apd_get_results(self.ctx, C.byref(s)), "apd_get_results")
         return o
+
+    def resize_nearest_device(self, src, dw: int, dh: int):
+        """apd_device_resize_nearest of a contiguous (H, W[, C]) torch tensor on the ctx's device."""
+        import torch
+        src = src.contiguous()
+        sh, sw = src.shape[:2]
+        dst = torch.empty((dh, dw) + tuple(src.shape[2:]), dtype=src.dtype, device=src.device)
+        elem = src.element_size() * (src[0, 0].numel() if src.dim() > 2 else 1)
+        self._check(self.lib.apd_device_resize_nearest(self.ctx, src.data_ptr(), sw, sh, dst.data_ptr(), dw, dh, elem),
+                    "apd_device_resize_nearest")
+        return dst
+
+    def result_device(self, width: int, height: int, device: str):
+        """apd_result_device: (depth (H, W), planes (H, W, 4)) of the last run, epilogue applied, on `device`."""
+        import torch
+        depth = torch.empty((height, width), dtype=torch.float32, device=device)
+        planes = torch.empty((height, width, 4), dtype=torch.float32, device=device)
+        self._check(self.lib.apd_result_device(self.ctx, depth.data_ptr(), planes.data_ptr()), "apd_result_device")
+        return depth, planes
 
     def timing(self) -> ApdTiming:
         t = ApdTiming()

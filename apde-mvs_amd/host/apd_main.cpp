@@ -247,6 +247,89 @@ struct Pending {  // Jacobi ordering: outputs committed at the end of the pass
     Mat mat;
 };
 
+// Device-resident view state (one context): the round's images and every view's last depth and
+// (normal, depth) planes stay in HBM between problems. The reference re-reads and re-uploads all of
+// them per problem (APD.cpp:508-684): at 6048x4032 with 10 sources that is 2.5 GB of uploads per
+// problem. The files are still written (fusion and later runs read them) and the maps here hold the
+// same values: depth = the epilogue's depth, planes = (normals.bin, depths.bin) interleaved, the
+// INTER_NEAREST resize to a new round's size done by the same index map on the device. A view whose
+// map is not here (none yet) falls back to the store.
+struct DevStore {
+    struct Map {
+        void *p = nullptr;
+        int w = 0, h = 0;
+        size_t bytes = 0;
+    };
+    apd_ctx *ctx = nullptr;
+    std::map<std::string, Map> images;          // this round's images, by path
+    std::map<int, Map> depth, planes;           // committed maps, by view id
+    std::map<int, Map> pend_depth, pend_planes;  // Jacobi: this pass's outputs until commit()
+    Map scratch;                                 // resized priors of one problem
+    long uploaded = 0;                           // bytes copied from the host (images)
+
+    bool reserve(Map &m, size_t bytes) {
+        if (m.p && m.bytes >= bytes) return true;
+        release(m);
+        if (apd_device_alloc(ctx, bytes, &m.p) != APD_OK) return false;
+        m.bytes = bytes;
+        return true;
+    }
+    void release(Map &m) {
+        if (m.p) apd_device_free(ctx, m.p);
+        m = Map{};
+    }
+    void release_all(std::map<int, Map> &ms) {
+        for (auto &kv : ms) release(kv.second);
+        ms.clear();
+    }
+    const float *image(const std::string &key, const ImageCache::Scaled &s) {
+        Map &m = images[key];
+        if (!m.p) {
+            const size_t b = (size_t)s.w * s.h * sizeof(float);
+            if (!reserve(m, b) || apd_device_copy(ctx, m.p, s.img.data(), b) != APD_OK) return nullptr;
+            m.w = s.w;
+            m.h = s.h;
+            uploaded += (long)b;
+        }
+        return static_cast<const float *>(m.p);
+    }
+    void drop_images() {
+        for (auto &kv : images) release(kv.second);
+        images.clear();
+    }
+    // the map of view `id` at w x h: the committed map itself, or its nearest resize into `dst`
+    const void *fitted(const Map &m, int w, int h, int elem, uint8_t *dst) {
+        if (m.w == w && m.h == h) return m.p;
+        if (apd_device_resize_nearest(ctx, m.p, m.w, m.h, dst, w, h, elem) != APD_OK) return nullptr;
+        return dst;
+    }
+    // device buffers for view `id`'s new maps at w x h
+    bool output(int id, bool pending, int w, int h, float **d, float **pl) {
+        Map &md = (pending ? pend_depth : depth)[id], &mp = (pending ? pend_planes : planes)[id];
+        const size_t n = (size_t)w * h;
+        if (!reserve(md, n * sizeof(float)) || !reserve(mp, n * 4 * sizeof(float))) return false;
+        md.w = mp.w = w;
+        md.h = mp.h = h;
+        *d = static_cast<float *>(md.p);
+        *pl = static_cast<float *>(mp.p);
+        return true;
+    }
+    void commit() {
+        for (auto pair : {std::make_pair(&pend_depth, &depth), std::make_pair(&pend_planes, &planes)})
+            for (auto &kv : *pair.first)
+                std::swap((*pair.second)[kv.first], kv.second);  // the old buffer serves the next pass
+    }
+    ~DevStore() {
+        if (!ctx) return;
+        drop_images();
+        release_all(depth);
+        release_all(planes);
+        release_all(pend_depth);
+        release_all(pend_planes);
+        release(scratch);
+    }
+};
+
 struct Driver {
     std::string dense;
     bool use_sa = true, flush = false;
@@ -254,6 +337,7 @@ struct Driver {
     bool jacobi = false;
     MatStore *store = nullptr;
     ImageCache images;
+    std::unique_ptr<DevStore> dev;  // single context only (the maps live on its device)
     std::mutex pend_mu;
     std::vector<Pending> pending;
 
@@ -288,8 +372,13 @@ struct Driver {
     void commit() {
         for (auto &p : pending) store->write(p.path, p.mat, flush);
         pending.clear();
+        if (dev) dev->commit();
         std::lock_guard<std::mutex> g(fit_mu);
         fitted.clear();
+    }
+    void new_round() {  // each round uses one scale
+        images.drop_scaled();
+        if (dev) dev->drop_images();
     }
 
     // APD::InuputInitialization + CudaSpaceInitialization + RunPatchMatch + ProcessProblem
@@ -385,10 +474,47 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     SAY("Image size: " << width << " * " << height);
     const size_t HW = (size_t)width * height;
     auto fit = [&](Mat m) { return (m.cols != width || m.rows != height) ? fit_cached(m, width, height) : m; };
+    // device-resident inputs: every image, and every depth / plane prior this problem reads when the
+    // DevStore holds all of them (else the priors come from the store as below)
+    const bool need_depths = P.geom_consistency || P.use_APD, need_planes = P.state != APD_FIRST_INIT;
+    std::vector<const float *> img_ptrs(NI), dep_ptrs(NI);
+    const float *dev_planes = nullptr;
+    bool dev_priors = false;
+    if (dev) {
+        for (int i = 0; i < NI; ++i) {
+            img_ptrs[i] = dev->image(dense + "/images/" + format_index(ids[i]) + pb.img_ext, *scaled[i]);
+            if (!img_ptrs[i]) { SAY("device image upload failed: " << apd_last_error(ctx)); return false; }
+        }
+        auto held = [](const std::map<int, DevStore::Map> &ms, int id) {
+            auto it = ms.find(id);
+            return it != ms.end() && it->second.p;
+        };
+        dev_priors = need_depths || need_planes;
+        for (int i = 0; i < NI && dev_priors && need_depths; ++i) dev_priors = held(dev->depth, ids[i]);
+        if (dev_priors && need_planes) dev_priors = held(dev->planes, ids[0]);
+        if (dev_priors) {
+            const size_t slots = need_depths ? (size_t)NI : 0;
+            if (!dev->reserve(dev->scratch, HW * sizeof(float) * (slots + 4))) {
+                SAY("device scratch allocation failed: " << apd_last_error(ctx));
+                return false;
+            }
+            uint8_t *s = static_cast<uint8_t *>(dev->scratch.p);
+            for (size_t i = 0; i < slots; ++i) {
+                dep_ptrs[i] = static_cast<const float *>(
+                    dev->fitted(dev->depth[ids[i]], width, height, 4, s + i * HW * sizeof(float)));
+                if (!dep_ptrs[i]) { SAY("device resize failed: " << apd_last_error(ctx)); return false; }
+            }
+            if (need_planes) {
+                dev_planes = static_cast<const float *>(
+                    dev->fitted(dev->planes[ids[0]], width, height, 16, s + slots * HW * sizeof(float)));
+                if (!dev_planes) { SAY("device resize failed: " << apd_last_error(ctx)); return false; }
+            }
+        }
+    }
     const auto t_img = std::chrono::steady_clock::now();
     // ---- priors (APD.cpp:592-684)
     std::vector<Mat> depths;
-    if (P.geom_consistency || P.use_APD) {
+    if (need_depths && !dev_priors) {
         Mat d;
         store->read(result_folder + "/depths.bin", d);
         depths.push_back(fit(d));
@@ -435,7 +561,7 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
         SAY("Weak count: " << weak_count << " / " << HW << " = " << (float)weak_count / (float)HW * 100 << "%");
     }
     std::shared_ptr<uint8_t[]> init_planes;  // pooled, not zero-filled: every element is written below
-    if (P.state != APD_FIRST_INIT) {
+    if (need_planes && !dev_priors) {
         Mat d, n;
         store->read(result_folder + "/depths.bin", d);
         store->read(result_folder + "/normals.bin", n);
@@ -460,9 +586,10 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     }
     const auto t_pri = std::chrono::steady_clock::now();
     // ---- device (CudaSpaceInitialization + RunPatchMatch)
-    std::vector<const float *> img_ptrs(NI), dep_ptrs(NI);
-    for (int i = 0; i < NI; ++i) img_ptrs[i] = scaled[i]->img.data();
-    for (size_t i = 0; i < depths.size(); ++i) dep_ptrs[i] = depths[i].ptr<float>();
+    if (!dev)
+        for (int i = 0; i < NI; ++i) img_ptrs[i] = scaled[i]->img.data();
+    if (!dev_priors)
+        for (size_t i = 0; i < depths.size(); ++i) dep_ptrs[i] = depths[i].ptr<float>();
     apd_problem prob{};
     prob.width = width;
     prob.height = height;
@@ -470,8 +597,8 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     prob.images = img_ptrs.data();
     prob.cameras = cams.data();
     prob.params = P;
-    prob.depths = depths.empty() ? nullptr : dep_ptrs.data();
-    prob.init_planes = reinterpret_cast<const float *>(init_planes.get());
+    prob.depths = need_depths ? dep_ptrs.data() : nullptr;
+    prob.init_planes = dev_priors ? dev_planes : reinterpret_cast<const float *>(init_planes.get());
     prob.weak_info = P.use_APD ? weak.ptr<uint8_t>() : nullptr;
     prob.confidence = P.use_APD ? conf.ptr<uint8_t>() : nullptr;
     prob.sa_mask = (P.use_APD && !sa.empty()) ? sa.ptr<uint8_t>() : nullptr;
@@ -515,6 +642,14 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     st = apd_get_results(ctx, &out);
     const auto t_get = std::chrono::steady_clock::now();
     if (st != APD_OK) { SAY("apd_get_results failed: " << apd_last_error(ctx)); return false; }
+    if (dev) {  // this view's next priors, kept in HBM (Jacobi: visible after the pass, as the files)
+        float *dd = nullptr, *dp = nullptr;
+        if (!dev->output(pb.ref_image_id, jacobi, width, height, &dd, &dp) ||
+            apd_result_device(ctx, dd, dp) != APD_OK) {
+            SAY("apd_result_device failed: " << apd_last_error(ctx));
+            return false;
+        }
+    }
     if (!(P.geom_consistency || P.use_APD)) memset(confidence.bytes(), 1, confidence.size_bytes());
     {  // the epilogue is element-wise: row chunks on host threads
         const int rows = 64;
@@ -704,6 +839,10 @@ int main(int argc, char **argv) {
         }
         ctxs.push_back(c);
     }
+    if (ctxs.size() == 1 && !(getenv("APD_DEVICE_STATE") && std::string(getenv("APD_DEVICE_STATE")) == "0")) {
+        drv.dev = std::make_unique<DevStore>();
+        drv.dev->ctx = ctxs[0];
+    }
     std::vector<Job> jobs(problems.size());
     for (size_t i = 0; i < problems.size(); ++i) jobs[i].pb = problems[i];
     bool ok = true;
@@ -746,7 +885,7 @@ int main(int argc, char **argv) {
     const int geom_iteration = 3;
     const auto start = std::chrono::steady_clock::now();
     for (int i = 0; i < round_num && ok; ++i) {
-        drv.images.drop_scaled();  // each round uses one scale
+        drv.new_round();
         drv.prefetch_round((int)std::pow(2, round_num - 1 - i), problems);
         std::cout << "========================== Round " << i << " ==========================" << std::endl;
         std::cout << "======== iteration " << iteration_index << "========" << std::endl;
@@ -795,6 +934,8 @@ int main(int argc, char **argv) {
         }
         std::cout << "=============================================================" << std::endl;
     }
+    if (drv.dev) printf("Device-resident state: %.1f MB of image uploads\n", drv.dev->uploaded / 1048576.0);
+    drv.dev.reset();  // its buffers belong to ctxs[0]
     for (apd_ctx *c : ctxs) apd_destroy(c);
     if (!ok) return EXIT_FAILURE;
     const auto end = std::chrono::steady_clock::now();

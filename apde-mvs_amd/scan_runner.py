@@ -48,6 +48,7 @@ class HostLib:
     def __init__(self, path: str = HOSTLIB_PATH):
         if not os.path.exists(path):
             raise A.ApdError(f"{path} not built: run `make -C apde-mvs_amd/host`")
+        A.torch_runtime_first()  # libapdhost.so links libapd_hip.so
         lib = C.CDLL(path)
         lib.apdhost_read_gray8.restype = C.c_long
         lib.apdhost_read_gray8.argtypes = [C.c_char_p, C.c_void_p, C.c_long, C.POINTER(C.c_int), C.POINTER(C.c_int)]

@@ -191,6 +191,62 @@ typedef struct {
     float *curve;
 } octx;
 
+/* ------------------------------------------------------------------------------------------------
+ * Access-set checking ("a CPU oracle with a per-colour write-set ∩ read-set = ∅
+ * assertion mode"). Every access to the per-pixel state goes through RD / WR. In the normal build
+ * they are the plain subscript. Built with -DORACLE_RACECHECK (liboracle_rc.so, single-threaded),
+ * each FOR_ALL / FOR_COLOUR phase records, per state element, the pixel task that wrote it and the
+ * task(s) that read it, and counts a conflict whenever one task's write meets another task's read or
+ * write in the same phase: exactly the accesses whose outcome would depend on the order in which
+ * the GPU's threads run (the reference's kernels and ours run a phase's pixels concurrently; the
+ * in-place DepthToWeak / LocalRefine / filter tiles and the checkerboard colours rely on this).
+ * ----------------------------------------------------------------------------------------------*/
+#ifdef ORACLE_RACECHECK
+enum { RC_plane, RC_cost, RC_sel, RC_sel_next, RC_vw, RC_weak, RC_conf, RC_fit, RC_reliable, RC_nearest,
+       RC_anchors, RC_curve, RC_amap, RC_COUNT };
+static const char *const rc_names[RC_COUNT] = {"plane", "cost", "sel", "sel_next", "vw", "weak", "conf", "fit",
+                                               "reliable", "nearest", "anchors", "curve", "amap"};
+typedef struct { int32_t *wr, *rd; size_t n, cap; } rc_shadow;
+static rc_shadow rc_sh[RC_COUNT];
+static int32_t rc_task = -1;        /* the pixel task running, -1 outside a phase */
+static char rc_phase_name[96];
+static int64_t rc_conflicts, rc_phases, rc_accesses;
+static char rc_first[320];
+static int rc_merge_colours;        /* negative control: both colours of a checkerboard in one phase */
+
+static void rc_conflict(int a, size_t i, int32_t t1, int32_t t2, const char *what) {
+    if (!rc_conflicts)
+        snprintf(rc_first, sizeof rc_first, "%s: %s[%zu] %s (tasks %d, %d)", rc_phase_name, rc_names[a], i, what,
+                 (int)t1, (int)t2);
+    rc_conflicts++;
+}
+static inline void rc_touch(int a, size_t i, int write) {
+    if (rc_task < 0) return;
+    rc_shadow *s = &rc_sh[a];
+    if (i >= s->n) { rc_conflict(a, i, rc_task, -1, "out of range"); return; }
+    rc_accesses++;
+    const int32_t t = rc_task;
+    if (write) {
+        if (s->wr[i] >= 0 && s->wr[i] != t) rc_conflict(a, i, s->wr[i], t, "written by two tasks");
+        if (s->rd[i] == -2 || (s->rd[i] >= 0 && s->rd[i] != t)) rc_conflict(a, i, s->rd[i], t, "read by one task, written by another");
+        s->wr[i] = t;
+    } else {
+        if (s->wr[i] >= 0 && s->wr[i] != t) rc_conflict(a, i, s->wr[i], t, "written by one task, read by another");
+        s->rd[i] = s->rd[i] == -1 ? t : (s->rd[i] == t ? t : -2);
+    }
+}
+static void rc_span(int a, size_t first, size_t count, int write) {
+    for (size_t k = 0; k < count; ++k) rc_touch(a, first + k, write);
+}
+#define RD(o, arr, i) (*(rc_touch(RC_##arr, (size_t)(i), 0), &(o)->arr[i]))
+#define WR(o, arr, i) (*(rc_touch(RC_##arr, (size_t)(i), 1), &(o)->arr[i]))
+#define RC_SPAN_W(o, arr, first, count) rc_span(RC_##arr, (size_t)(first), (size_t)(count), 1)
+#else
+#define RD(o, arr, i) ((o)->arr[i])
+#define WR(o, arr, i) ((o)->arr[i])
+#define RC_SPAN_W(o, arr, first, count) ((void)0)
+#endif
+
 static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 static inline int is_set(uint32_t v, int n) { return (int)((v >> n) & 1u); }
 
@@ -445,8 +501,8 @@ float o_ncc_old(const octx *o, int px, int py, int s, f4 pl) {
     return ncc_finalize(sr, srr, ss, sss, srs, wsum);
 }
 
-static inline int16_t anchor_x(const octx *o, int pix, int k) { return o->anchors[2 * (o->amap[pix] * ANCHOR_NUM + k)]; }
-static inline int16_t anchor_y(const octx *o, int pix, int k) { return o->anchors[2 * (o->amap[pix] * ANCHOR_NUM + k) + 1]; }
+static inline int16_t anchor_x(const octx *o, int pix, int k) { return RD(o, anchors, 2 * (RD(o, amap, pix) * ANCHOR_NUM + k)); }
+static inline int16_t anchor_y(const octx *o, int pix, int k) { return RD(o, anchors, 2 * (RD(o, amap, pix) * ANCHOR_NUM + k) + 1); }
 
 /* sa label at a possibly out-of-image linear index (APD.cu:494,527 read it unchecked): inside the
    H*W buffer -> that byte; outside -> treated as a label mismatch. Returns -1 for "outside". */
@@ -476,7 +532,7 @@ float o_ncc_new(const octx *o, int px, int py, int s, f4 pl) {
     float ptx, pty;
     project(Hm, (float)px, (float)py, &ptx, &pty);
     if (ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f) return COST_MAX;
-    if (o->weak[center] != WEAK) return 0.0f; /* printf("error") branch, unreachable */
+    if (RD(o, weak, center) != WEAK) return 0.0f; /* printf("error") branch, unreachable */
     float strong_costs[9];
     int ns = 0;
     float center_cost = 0.0f, strong_weight = 0.0f;
@@ -488,7 +544,7 @@ float o_ncc_new(const octx *o, int px, int py, int s, f4 pl) {
         project(Hm, (float)ax, (float)ay, &asx, &asy);
         if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) {
             if (k != 0) {
-                if (is_set(o->sel[ax + ay * W], s - 1)) { strong_costs[ns++] = COST_MAX; strong_weight += 1.0f; }
+                if (is_set(RD(o, sel, ax + ay * W), s - 1)) { strong_costs[ns++] = COST_MAX; strong_weight += 1.0f; }
                 continue;
             }
             return COST_MAX;
@@ -557,16 +613,16 @@ static void k_random_init(octx *o, int px, int py) {
         float depth = orng_uniform(&g) * (o->P.depth_max - o->P.depth_min) + o->P.depth_min;
         f4 n = random_normal(cam, px, py, &g, depth);
         n.w = dist2origin(cam, px, py, depth, n);
-        o->plane[c] = n;
+        WR(o, plane, c) = n;
     } else {
-        f4 n = to_ref(cam, o->plane[c]);
+        f4 n = to_ref(cam, RD(o, plane, c));
         float depth = n.w;
         n.w = dist2origin(cam, px, py, depth, n);
-        o->plane[c] = n;
+        WR(o, plane, c) = n;
     }
-    f4 pl = o->plane[c];
+    f4 pl = RD(o, plane, c);
     const int N = o->N;
-    const int use_new = o->P.use_APD && o->weak[c] == WEAK;
+    const int use_new = o->P.use_APD && RD(o, weak, c) == WEAK;
     float cv[32], sorted[32];
     int nvalid = 0;
     for (int i = 1; i <= N; ++i) {
@@ -585,7 +641,7 @@ static void k_random_init(octx *o, int px, int py) {
     /* The reference writes selected_views[center] here while ComputeBilateralNCCNew of other WEAK pixels
        reads the anchors' selected_views in the same launch (APD.cu:502 vs 755-766): a race on
        uninitialised memory. Defined here as launch-start snapshot: results go to sel_next. */
-    o->sel_next[c] = 0;
+    WR(o, sel_next, c) = 0;
     int top_k = nvalid < o->P.top_k ? nvalid : o->P.top_k;
     if (top_k > 0) {
         float cost = 0.0f;
@@ -593,10 +649,10 @@ static void k_random_init(octx *o, int px, int py) {
         float thr = sorted[top_k - 1];
         uint32_t sv = 0;
         for (int i = 0; i < N; ++i) if (cv[i] <= thr) sv |= (1u << i);
-        o->sel_next[c] = sv;
-        o->cost[c] = cost / (float)top_k;
+        WR(o, sel_next, c) = sv;
+        WR(o, cost, c) = cost / (float)top_k;
     } else {
-        o->cost[c] = COST_MAX;
+        WR(o, cost, c) = COST_MAX;
     }
 }
 
@@ -667,58 +723,58 @@ static void k_sweep_strong(octx *o, int px, int py, int iter) {
     int up_near = c - W, up_far = c - 3 * W, down_near = c + W, down_far = c + 3 * W;
     int left_near = c - 1, left_far = c - 3, right_near = c + 1, right_far = c + 3;
     if (py > 2) {
-        flag[1] = 1; cmin = o->cost[up_far]; cminp = up_far;
+        flag[1] = 1; cmin = RD(o, cost, up_far); cminp = up_far;
         for (int i = 1; i < 11; ++i)
-            if (py > 2 + 2 * i) { int t = up_far - 2 * i * W; if (o->cost[t] < cmin) { cmin = o->cost[t]; cminp = t; } }
+            if (py > 2 + 2 * i) { int t = up_far - 2 * i * W; if (RD(o, cost, t) < cmin) { cmin = RD(o, cost, t); cminp = t; } }
         up_far = cminp;
     }
     if (py < H - 3) {
-        flag[3] = 1; cmin = o->cost[down_far]; cminp = down_far;
+        flag[3] = 1; cmin = RD(o, cost, down_far); cminp = down_far;
         for (int i = 1; i < 11; ++i)
-            if (py < H - 3 - 2 * i) { int t = down_far + 2 * i * W; if (o->cost[t] < cmin) { cmin = o->cost[t]; cminp = t; } }
+            if (py < H - 3 - 2 * i) { int t = down_far + 2 * i * W; if (RD(o, cost, t) < cmin) { cmin = RD(o, cost, t); cminp = t; } }
         down_far = cminp;
     }
     if (px > 2) {
-        flag[5] = 1; cmin = o->cost[left_far]; cminp = left_far;
+        flag[5] = 1; cmin = RD(o, cost, left_far); cminp = left_far;
         for (int i = 1; i < 11; ++i)
-            if (px > 2 + 2 * i) { int t = left_far - 2 * i; if (o->cost[t] < cmin) { cmin = o->cost[t]; cminp = t; } }
+            if (px > 2 + 2 * i) { int t = left_far - 2 * i; if (RD(o, cost, t) < cmin) { cmin = RD(o, cost, t); cminp = t; } }
         left_far = cminp;
     }
     if (px < W - 3) {
-        flag[7] = 1; cmin = o->cost[right_far]; cminp = right_far;
+        flag[7] = 1; cmin = RD(o, cost, right_far); cminp = right_far;
         for (int i = 1; i < 11; ++i)
-            if (px < W - 3 - 2 * i) { int t = right_far + 2 * i; if (o->cost[t] < cmin) { cmin = o->cost[t]; cminp = t; } }
+            if (px < W - 3 - 2 * i) { int t = right_far + 2 * i; if (RD(o, cost, t) < cmin) { cmin = RD(o, cost, t); cminp = t; } }
         right_far = cminp;
     }
     if (py > 0) {
-        flag[0] = 1; cmin = o->cost[up_near]; cminp = up_near;
+        flag[0] = 1; cmin = RD(o, cost, up_near); cminp = up_near;
         for (int i = 0; i < 3; ++i) {
-            if (py > 1 + i && px > i) { int t = up_near - (1 + i) * W - (i + 1); if (o->cost[t] < cmin) { cmin = o->cost[t]; cminp = t; } }
-            if (py > 1 + i && px < W - 1 - i) { int t = up_near - (1 + i) * W + (i + 1); if (o->cost[t] < cmin) { cmin = o->cost[t]; cminp = t; } }
+            if (py > 1 + i && px > i) { int t = up_near - (1 + i) * W - (i + 1); if (RD(o, cost, t) < cmin) { cmin = RD(o, cost, t); cminp = t; } }
+            if (py > 1 + i && px < W - 1 - i) { int t = up_near - (1 + i) * W + (i + 1); if (RD(o, cost, t) < cmin) { cmin = RD(o, cost, t); cminp = t; } }
         }
         up_near = cminp;
     }
     if (py < H - 1) {
-        flag[2] = 1; cmin = o->cost[down_near]; cminp = down_near;
+        flag[2] = 1; cmin = RD(o, cost, down_near); cminp = down_near;
         for (int i = 0; i < 3; ++i) {
-            if (py < H - 2 - i && px > i) { int t = down_near + (1 + i) * W - (i + 1); if (o->cost[t] < cmin) { cmin = o->cost[t]; cminp = t; } }
-            if (py < H - 2 - i && px < W - 1 - i) { int t = down_near + (1 + i) * W + (i + 1); if (o->cost[t] < cmin) { cmin = o->cost[t]; cminp = t; } }
+            if (py < H - 2 - i && px > i) { int t = down_near + (1 + i) * W - (i + 1); if (RD(o, cost, t) < cmin) { cmin = RD(o, cost, t); cminp = t; } }
+            if (py < H - 2 - i && px < W - 1 - i) { int t = down_near + (1 + i) * W + (i + 1); if (RD(o, cost, t) < cmin) { cmin = RD(o, cost, t); cminp = t; } }
         }
         down_near = cminp;
     }
     if (px > 0) {
-        flag[4] = 1; cmin = o->cost[left_near]; cminp = left_near;
+        flag[4] = 1; cmin = RD(o, cost, left_near); cminp = left_near;
         for (int i = 0; i < 3; ++i) {
-            if (px > 1 + i && py > i) { int t = left_near - (1 + i) - (i + 1) * W; if (o->cost[t] < cmin) { cmin = o->cost[t]; cminp = t; } }
-            if (px > 1 + i && py < H - 1 - i) { int t = left_near - (1 + i) + (i + 1) * W; if (o->cost[t] < cmin) { cmin = o->cost[t]; cminp = t; } }
+            if (px > 1 + i && py > i) { int t = left_near - (1 + i) - (i + 1) * W; if (RD(o, cost, t) < cmin) { cmin = RD(o, cost, t); cminp = t; } }
+            if (px > 1 + i && py < H - 1 - i) { int t = left_near - (1 + i) + (i + 1) * W; if (RD(o, cost, t) < cmin) { cmin = RD(o, cost, t); cminp = t; } }
         }
         left_near = cminp;
     }
     if (px < W - 1) {
-        flag[6] = 1; cmin = o->cost[right_near]; cminp = right_near;
+        flag[6] = 1; cmin = RD(o, cost, right_near); cminp = right_near;
         for (int i = 0; i < 3; ++i) {
-            if (px < W - 2 - i && py > i) { int t = right_near + (1 + i) - (i + 1) * W; if (o->cost[t] < cmin) { cmin = o->cost[t]; cminp = t; } }
-            if (px < W - 2 - i && py < H - 1 - i) { int t = right_near + (1 + i) + (i + 1) * W; if (o->cost[t] < cmin) { cmin = o->cost[t]; cminp = t; } }
+            if (px < W - 2 - i && py > i) { int t = right_near + (1 + i) - (i + 1) * W; if (RD(o, cost, t) < cmin) { cmin = RD(o, cost, t); cminp = t; } }
+            if (px < W - 2 - i && py < H - 1 - i) { int t = right_near + (1 + i) + (i + 1) * W; if (RD(o, cost, t) < cmin) { cmin = RD(o, cost, t); cminp = t; } }
         }
         right_near = cminp;
     }
@@ -726,14 +782,14 @@ static void k_sweep_strong(octx *o, int px, int py, int iter) {
     pos[4] = left_near; pos[5] = left_far; pos[6] = right_near; pos[7] = right_far;
     for (int j = 0; j < 8; ++j)
         if (flag[j])
-            for (int i = 1; i <= N; ++i) ca[j][i - 1] = o_ncc_old(o, px, py, i, o->plane[pos[j]]);
+            for (int i = 1; i <= N; ++i) ca[j][i - 1] = o_ncc_old(o, px, py, i, RD(o, plane, pos[j]));
 
     /* view selection priors, APD.cu:1323-1337 */
     float prior[32] = {0};
     const int nb[4] = {c - W, c + W, c - 1, c + 1};
     for (int i = 0; i < 4; ++i)
         if (flag[2 * i])
-            for (int j = 0; j < N; ++j) prior[j] += is_set(o->sel[nb[i]], j) ? 0.9f : 0.1f;
+            for (int j = 0; j < N; ++j) prior[j] += is_set(RD(o, sel, nb[i]), j) ? 0.9f : 0.1f;
     orng g;
     orng_init(&g, o->seed, (uint32_t)c, ORD_STRONG(iter));
     uint8_t vw[APD_MAX_IMAGES];
@@ -752,7 +808,7 @@ static void k_sweep_strong(octx *o, int px, int py, int iter) {
 
     const int geom_imp = o->P.geom_consistency && o->P.use_impetus;
     const float gf = o->P.geom_factor;
-    f4 cur = o->plane[c];
+    f4 cur = RD(o, plane, c);
     float cost_now = 0.0f;
     for (int i = 0; i < N; ++i) {
         float v = o_ncc_old(o, px, py, i + 1, cur);
@@ -764,11 +820,11 @@ static void k_sweep_strong(octx *o, int px, int py, int iter) {
     float depth_now = depth_from_plane(cam, cur, px, py);
     f4 pnow = cur;
     if (flag[mi]) {
-        f4 cand = o->plane[pos[mi]];
+        f4 cand = RD(o, plane, pos[mi]);
         float db = depth_from_plane(cam, cand, px, py);
         if (db >= o->P.depth_min && db <= o->P.depth_max && fc[mi] < cost_now) {
             depth_now = db; pnow = cand; cost_now = fc[mi];
-            o->sel[c] = tsel;
+            WR(o, sel, c) = tsel;
         }
     }
     /* PlaneHypothesisRefinementStrong, APD.cu:950-1006 */
@@ -791,12 +847,12 @@ static void k_sweep_strong(octx *o, int px, int py, int iter) {
         }
     }
     if (o->P.state == APD_REFINE_INIT) {
-        if ((double)cost_now < (double)cost_init - 0.1) { o->cost[c] = cost_now; o->plane[c] = pnow; }
-        else o->cost[c] = cost_init;
+        if ((double)cost_now < (double)cost_init - 0.1) { WR(o, cost, c) = cost_now; WR(o, plane, c) = pnow; }
+        else WR(o, cost, c) = cost_init;
     } else {
-        o->cost[c] = cost_now; o->plane[c] = pnow;
+        WR(o, cost, c) = cost_now; WR(o, plane, c) = pnow;
     }
-    for (int i = 0; i < N; ++i) o->vw[(size_t)i * o->HW + c] = vw[i];
+    for (int i = 0; i < N; ++i) WR(o, vw, (size_t)i * o->HW + c) = vw[i];
 }
 
 /* CheckerboardPropagationWeak + PlaneHypothesisRefinementWeak, APD.cu:1442-1615, 1008-1096 */
@@ -811,17 +867,17 @@ static void k_sweep_weak(octx *o, int px, int py, int iter) {
     f4 newp[8];
     for (int i = 0; i < 8; ++i) {
         int ax = anchor_x(o, c, i + 1), ay = anchor_y(o, c, i + 1);
-        if (ax == -1 || ay == -1 || o->weak[ax + ay * W] != STRONG) continue;
+        if (ax == -1 || ay == -1 || RD(o, weak, ax + ay * W) != STRONG) continue;
         pos[i] = ax + ay * W;
         flag[i] = 1;
-        for (int s = 1; s <= N; ++s) ca[i][s - 1] = o_ncc_new(o, px, py, s, o->plane[pos[i]]);
-        newp[i] = o->plane[pos[i]];
+        for (int s = 1; s <= N; ++s) ca[i][s - 1] = o_ncc_new(o, px, py, s, RD(o, plane, pos[i]));
+        newp[i] = RD(o, plane, pos[i]);
     }
     float prior[32] = {0};
     for (int i = 0; i < 8; ++i) {
         int ax = anchor_x(o, c, i + 1), ay = anchor_y(o, c, i + 1);
         if (ax == -1 || ay == -1) continue;
-        for (int j = 0; j < N; ++j) prior[j] += is_set(o->sel[ax + ay * W], j) ? 0.9f : 0.1f;
+        for (int j = 0; j < N; ++j) prior[j] += is_set(RD(o, sel, ax + ay * W), j) ? 0.9f : 0.1f;
     }
     orng g;
     orng_init(&g, o->seed, (uint32_t)c, ORD_WEAK(iter));
@@ -838,7 +894,7 @@ static void k_sweep_weak(octx *o, int px, int py, int iter) {
         for (int i = 0; i < N; ++i) {
             if (vw[i] > 0) {
                 float v = ca[j][i];
-                if (geom) v = flag[j] ? fmaf(gf, o_geom_cost(o, px, py, i + 1, o->plane[pos[j]]), v) : fmaf(gf, 3.0f, v);
+                if (geom) v = flag[j] ? fmaf(gf, o_geom_cost(o, px, py, i + 1, RD(o, plane, pos[j])), v) : fmaf(gf, 3.0f, v);
                 acc = fmaf((float)vw[i], v, acc);
             }
         }
@@ -846,7 +902,7 @@ static void k_sweep_weak(octx *o, int px, int py, int iter) {
     }
     int mi = 0;
     { float m = fc[0]; for (int j = 1; j < 8; ++j) if (fc[j] <= m) { m = fc[j]; mi = j; } }
-    f4 cur = o->plane[c];
+    f4 cur = RD(o, plane, c);
     float cost_now = 0.0f;
     for (int i = 0; i < N; ++i) {
         float v = o_ncc_new(o, px, py, i + 1, cur);
@@ -861,11 +917,11 @@ static void k_sweep_weak(octx *o, int px, int py, int iter) {
         float db = depth_from_plane(cam, newp[mi], px, py);
         if (db >= o->P.depth_min && db <= o->P.depth_max && fc[mi] < cost_now) {
             depth_now = db; pnow = newp[mi]; cost_now = fc[mi];
-            o->sel[c] = tsel;
+            WR(o, sel, c) = tsel;
         }
     }
     /* PlaneHypothesisRefinementWeak, APD.cu:1008-1096 */
-    f4 fit = o->fit[c];
+    f4 fit = RD(o, fit, c);
     if (!(fit.x == 0 && fit.y == 0 && fit.z == 0)) {
         {
             float tc = 0.0f;
@@ -900,12 +956,12 @@ static void k_sweep_weak(octx *o, int px, int py, int iter) {
         }
     }
     if (o->P.state == APD_REFINE_INIT) {
-        if ((double)cost_now < (double)cost_init - 0.1) { o->cost[c] = cost_now; o->plane[c] = pnow; }
-        else o->cost[c] = cost_init;
+        if ((double)cost_now < (double)cost_init - 0.1) { WR(o, cost, c) = cost_now; WR(o, plane, c) = pnow; }
+        else WR(o, cost, c) = cost_init;
     } else {
-        o->cost[c] = cost_now; o->plane[c] = pnow;
+        WR(o, cost, c) = cost_now; WR(o, plane, c) = pnow;
     }
-    for (int i = 0; i < N; ++i) o->vw[(size_t)i * o->HW + c] = vw[i];
+    for (int i = 0; i < N; ++i) WR(o, vw, (size_t)i * o->HW + c) = vw[i];
 }
 
 /* PointinTriangle, APD.cu:122-143 */
@@ -929,9 +985,10 @@ static int point_in_triangle(int ax, int ay, int bx, int by, int cx, int cy, int
 static void k_find_nearest(octx *o, int px, int py) {
     const int W = o->W, H = o->H, c = px + py * W;
     int16_t *out = &o->nearest[2 * c];
+    RC_SPAN_W(o, nearest, 2 * c, 2);
     out[0] = -1; out[1] = -1;
-    const uint8_t cc = o->conf[c];
-    if (o->weak[c] == WEAK || o->weak[c] == UNKNOWN) {
+    const uint8_t cc = RD(o, conf, c);
+    if (RD(o, weak, c) == WEAK || RD(o, weak, c) == UNKNOWN) {
         uint8_t bc = 0;
         int bx = -1, by = -1;
         float md = FLT_MAX;
@@ -940,15 +997,15 @@ static void k_find_nearest(octx *o, int px, int py) {
                 int tx = px + x, ty = py + y;
                 if (tx < 0 || tx >= W || ty < 0 || ty >= H) continue;
                 int t = tx + ty * W;
-                if (o->weak[t] != STRONG) continue;
-                if (o->conf[t] < cc) continue;
+                if (RD(o, weak, t) != STRONG) continue;
+                if (RD(o, conf, t) < cc) continue;
                 float d = sqrtf((float)(x * x + y * y));
-                if (d < md) { md = d; bx = tx; by = ty; bc = o->conf[t]; }
-                else if (d == md) { if (o->conf[t] > bc) { bx = tx; by = ty; bc = o->conf[t]; } }
+                if (d < md) { md = d; bx = tx; by = ty; bc = RD(o, conf, t); }
+                else if (d == md) { if (RD(o, conf, t) > bc) { bx = tx; by = ty; bc = RD(o, conf, t); } }
             }
         }
         out[0] = (int16_t)bx; out[1] = (int16_t)by;
-    } else if (o->weak[c] == STRONG) {
+    } else if (RD(o, weak, c) == STRONG) {
         out[0] = (int16_t)px; out[1] = (int16_t)py;
     }
 }
@@ -969,11 +1026,12 @@ static anchor_consts make_anchor_consts(int rotate_time) {
 /* GenAnchors, APD.cu:1857-2082 */
 static void k_gen_anchors(octx *o, int px, int py, anchor_consts K) {
     const int W = o->W, H = o->H, c = px + py * W;
-    if (o->weak[c] != WEAK) return;
+    if (RD(o, weak, c) != WEAK) return;
     const int margin = 6;
     const float depth_diff = o->P.depth_max - o->P.depth_min;
     const apd_camera *cam = &o->cam[0];
-    int16_t *anc = &o->anchors[2 * (o->amap[c] * ANCHOR_NUM)];
+    int16_t *anc = &o->anchors[2 * (RD(o, amap, c) * ANCHOR_NUM)];
+    RC_SPAN_W(o, anchors, 2 * (RD(o, amap, c) * ANCHOR_NUM), 2 * ANCHOR_NUM);
     orng g;
     orng_init(&g, o->seed, (uint32_t)c, ORD_ANCHORS);
     for (int i = 0; i < ANCHOR_NUM; ++i) { anc[2 * i] = -1; anc[2 * i + 1] = -1; }
@@ -1007,7 +1065,7 @@ static void k_gen_anchors(octx *o, int px, int py, anchor_consts K) {
                         int ay = (int16_t)(int)((float)py + ddy * (float)radius);
                         if (ax < margin || ay < margin || ax >= W - margin || ay >= H - margin) continue;
                         int ac = ax + ay * W;
-                        int nx = o->nearest[2 * ac], ny = o->nearest[2 * ac + 1];
+                        int nx = RD(o, nearest, 2 * ac), ny = RD(o, nearest, 2 * ac + 1);
                         if (nx == -1 || ny == -1) continue;
                         float tdx = (float)(nx - px), tdy = (float)(ny - py);
                         normalize2(&tdx, &tdy);
@@ -1023,18 +1081,18 @@ static void k_gen_anchors(octx *o, int px, int py, anchor_consts K) {
             }
         }
     }
-    if (nsp <= 3) { o->reliable[c] = 0; return; }
+    if (nsp <= 3) { WR(o, reliable, c) = 0; return; }
     int vx[32], vy[32], vc = 0;
     float v3[32][3];
     float X[3];
-    get3d(cam, (float)px, (float)py, o->plane[c].w, X);
+    get3d(cam, (float)px, (float)py, RD(o, plane, c).w, X);
     float cw[3] = {X[0], X[1], X[2]};
     for (int i = 0; i < 32; ++i) {
         vx[i] = -1; vy[i] = -1;
         if (dvalid[i]) {
             int sc = spx[i] + spy[i] * W;
             vx[vc] = spx[i]; vy[vc] = spy[i];
-            get3d(cam, (float)spx[i], (float)spy[i], o->plane[sc].w, X);
+            get3d(cam, (float)spx[i], (float)spy[i], RD(o, plane, sc).w, X);
             v3[vc][0] = X[0]; v3[vc][1] = X[1]; v3[vc][2] = X[2];
             vc++;
         }
@@ -1072,7 +1130,7 @@ static void k_gen_anchors(octx *o, int px, int py, anchor_consts K) {
             if (cd < min_cost) { min_cost = cd; best = cr; ua = a; ub = b; uc = cc; }
         }
     }
-    if (!has) { o->reliable[c] = 0; return; }
+    if (!has) { WR(o, reliable, c) = 0; return; }
     float wgt[32];
     for (int i = 0; i < vc; ++i) {
         float d = fabsf(best.x * v3[i][0] + best.y * v3[i][1] + best.z * v3[i][2] + best.w);
@@ -1089,13 +1147,13 @@ static void k_gen_anchors(octx *o, int px, int py, anchor_consts K) {
         vx[j] = tx; vy[j] = ty; wgt[j] = tw;
     }
     for (int i = 1; i < ANCHOR_NUM; ++i) { anc[2 * i] = (int16_t)vx[i - 1]; anc[2 * i + 1] = (int16_t)vy[i - 1]; }
-    o->reliable[c] = 1;
+    WR(o, reliable, c) = 1;
 }
 
 /* RANSACToGetFitPlane, APD.cu:2486-2598 */
 static void k_ransac_fit(octx *o, int px, int py, int iter) {
     const int W = o->W, c = px + py * W;
-    if (o->weak[c] != WEAK) { o->fit[c] = o->plane[c]; return; }
+    if (RD(o, weak, c) != WEAK) { WR(o, fit, c) = RD(o, plane, c); return; }
     const apd_camera *cam = &o->cam[0];
     int sx[8], sy[8], cnt = 0;
     float s3[8][3], X[3];
@@ -1103,12 +1161,12 @@ static void k_ransac_fit(octx *o, int px, int py, int iter) {
         int ax = anchor_x(o, c, i), ay = anchor_y(o, c, i);
         if (ax == -1 || ay == -1) continue;
         sx[cnt] = ax; sy[cnt] = ay;
-        float d = depth_from_plane(cam, o->plane[ax + ay * W], ax, ay);
+        float d = depth_from_plane(cam, RD(o, plane, ax + ay * W), ax, ay);
         get3d(cam, (float)ax, (float)ay, d, X);
         s3[cnt][0] = X[0]; s3[cnt][1] = X[1]; s3[cnt][2] = X[2];
         cnt++;
     }
-    if (cnt < 3) { o->fit[c] = o->plane[c]; return; }
+    if (cnt < 3) { WR(o, fit, c) = RD(o, plane, c); return; }
     orng g;
     orng_init(&g, o->seed, (uint32_t)c, ORD_FIT(iter));
     float min_cost = FLT_MAX;
@@ -1136,23 +1194,23 @@ static void k_ransac_fit(octx *o, int px, int py, int iter) {
         if (min_cost == 0) break;
     }
     if (has) {
-        float d = depth_from_plane(cam, o->plane[c], px, py);
+        float d = depth_from_plane(cam, RD(o, plane, c), px, py);
         f4 vd = view_dir(cam, px, py, d);
         float dot = best.x * vd.x + best.y * vd.y + best.z * vd.z;
         if (dot > 0) { best.x = -best.x; best.y = -best.y; best.z = -best.z; best.w = -best.w; }
-        o->fit[c] = best;
+        WR(o, fit, c) = best;
     } else {
         f4 z = {0, 0, 0, 0};
-        o->fit[c] = z;
+        WR(o, fit, c) = z;
     }
 }
 
 /* GetDepthandNormal, APD.cu:1694-1709 */
 static void k_depth_normal(octx *o, int px, int py) {
     const int c = py * o->W + px;
-    f4 p = o->plane[c];
+    f4 p = RD(o, plane, c);
     p.w = depth_from_plane(&o->cam[0], p, px, py);
-    o->plane[c] = to_world(&o->cam[0], p);
+    WR(o, plane, c) = to_world(&o->cam[0], p);
 }
 
 /* CheckerboardFilterStrong, APD.cu:1711-1821 */
@@ -1160,12 +1218,11 @@ static void k_filter(octx *o, int px, int py) {
     const int W = o->W, H = o->H, c = py * W + px;
     float f[21];
     int n = 0;
-    f[n++] = o->plane[c].w;
+    f[n++] = RD(o, plane, c).w;
     const int left = c - 1, leftleft = c - 3, up = c - W, upup = c - 3 * W;
     const int down = c + W, downdown = c + 3 * W, right = c + 1, rightright = c + 3;
-    if (o->cost[c] < 0.001f) return;
-    const uint8_t *wk = o->weak;
-#define FADD(cond, idx) if ((cond) && wk[(idx)] == STRONG) f[n++] = o->plane[(idx)].w
+    if (RD(o, cost, c) < 0.001f) return;
+#define FADD(cond, idx) if ((cond) && RD(o, weak, (idx)) == STRONG) f[n++] = RD(o, plane, (idx)).w
     FADD(py > 0, up);
     FADD(py > 2, upup);
     FADD(py > 4, upup - W * 2);
@@ -1194,7 +1251,7 @@ static void k_filter(octx *o, int px, int py) {
         f[j] = t;
     }
     int m = n / 2;
-    o->plane[c].w = (n % 2 == 0) ? (f[m - 1] + f[m]) / 2 : f[m];
+    WR(o, plane, c).w = (n % 2 == 0) ? (f[m - 1] + f[m]) / 2 : f[m];
 }
 
 /* DepthToWeak's classification of a 61-sample cost curve (disparities -30..30), APD.cu:2200-2249:
@@ -1225,23 +1282,23 @@ static int o_classify_curve(const float *pc, int weak_peak_radius) {
 /* DepthToWeak, APD.cu:2103-2250 */
 static void k_depth_to_weak(octx *o, int px, int py) {
     const int W = o->W, H = o->H, c = px + py * W, N = o->N;
-    if (px < 6 || py < 6 || px >= W - 6 || py >= H - 6) { o->weak[c] = UNKNOWN; return; }
+    if (px < 6 || py < 6 || px >= W - 6 || py >= H - 6) { WR(o, weak, c) = UNKNOWN; return; }
     const apd_camera *cam = &o->cam[0];
-    f4 pl = to_ref(cam, o->plane[c]);
+    f4 pl = to_ref(cam, RD(o, plane, c));
     float od = pl.w;
-    if (od == 0) { o->weak[c] = UNKNOWN; return; }
-    const uint32_t sv = o->sel[c];
+    if (od == 0) { WR(o, weak, c) = UNKNOWN; return; }
+    const uint32_t sv = RD(o, sel, c);
     float base = 0.0f, wn = 0.0f;
     int valid = 0;
     for (int s = 1; s <= N; ++s) {
         if (is_set(sv, s - 1)) {
-            wn += (float)o->vw[(size_t)(s - 1) * o->HW + c];
+            wn += (float)RD(o, vw, (size_t)(s - 1) * o->HW + c);
             float d0 = cam->c[0] - o->cam[s].c[0], d1 = cam->c[1] - o->cam[s].c[1], d2 = cam->c[2] - o->cam[s].c[2];
             base += sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
             valid++;
         }
     }
-    if (valid == 0) { o->weak[c] = UNKNOWN; return; }
+    if (valid == 0) { WR(o, weak, c) = UNKNOWN; return; }
     base /= (float)valid;
     float disp = cam->K[0] * base / od;
     float pc[61];
@@ -1257,24 +1314,27 @@ static void k_depth_to_weak(octx *o, int px, int py) {
             if (is_set(sv, s - 1)) {
                 float tc = o_ncc_old(o, px, py, s, t);
                 if (geom) tc = fmaf(gf, o_geom_cost(o, px, py, s, t), tc);
-                p = fmaf(tc, (float)o->vw[(size_t)(s - 1) * o->HW + c], p);
+                p = fmaf(tc, (float)RD(o, vw, (size_t)(s - 1) * o->HW + c), p);
             }
         }
         p /= wn;
         pc[pd + 30] = CV_MIN(2.0f, p);
     }
-    if (o->curve) memcpy(&o->curve[(size_t)c * 61], pc, sizeof(pc));
-    o->weak[c] = (uint8_t)o_classify_curve(pc, o->P.weak_peak_radius);
+    if (o->curve) {
+        RC_SPAN_W(o, curve, (size_t)c * 61, 61);
+        memcpy(&o->curve[(size_t)c * 61], pc, sizeof(pc));
+    }
+    WR(o, weak, c) = (uint8_t)o_classify_curve(pc, o->P.weak_peak_radius);
 }
 
 /* ConfidenceCompute, APD.cu:2282-2344 */
 static void k_confidence(octx *o, int px, int py) {
     const int W = o->W, c = px + py * W;
-    o->conf[c] = 0;
+    WR(o, conf, c) = 0;
     const apd_camera *rc = &o->cam[0];
-    const uint32_t sv = o->sel[c];
-    const float rd = o->plane[c].w;
-    if (rd <= 0.0f) { o->weak[c] = UNKNOWN; return; }
+    const uint32_t sv = RD(o, sel, c);
+    const float rd = RD(o, plane, c).w;
+    if (rd <= 0.0f) { WR(o, weak, c) = UNKNOWN; return; }
     float P[3];
     world_point(rc, (float)px, (float)py, rd, P);
     int nc = 1;
@@ -1296,17 +1356,17 @@ static void k_confidence(octx *o, int px, int py) {
         if (fabsf(rd - refd) / rd <= 0.02f) nc += 2;
     }
     if (nc > 255) nc = 255;
-    o->conf[c] = (uint8_t)nc;
+    WR(o, conf, c) = (uint8_t)nc;
 }
 
 /* LocalRefine, APD.cu:2346-2432 */
 static void k_local_refine(octx *o, int px, int py) {
     const int W = o->W, c = px + py * W, N = o->N;
     const apd_camera *cam = &o->cam[0];
-    f4 pl = to_ref(cam, o->plane[c]);
+    f4 pl = to_ref(cam, RD(o, plane, c));
     float od = pl.w;
     if (od == 0) return;
-    const uint32_t sv = o->sel[c];
+    const uint32_t sv = RD(o, sel, c);
     const int geom = o->P.geom_consistency;
     const float gf = o->P.geom_factor;
     float cost_now = 0.0f, base = 0.0f, wn = 0.0f;
@@ -1317,7 +1377,7 @@ static void k_local_refine(octx *o, int px, int py) {
             t.w = dist2origin(cam, px, py, od, t);
             float tc = o_ncc_old(o, px, py, s, t);
             if (geom) tc = fmaf(gf, o_geom_cost(o, px, py, s, t), tc);
-            float w = (float)o->vw[(size_t)(s - 1) * o->HW + c];
+            float w = (float)RD(o, vw, (size_t)(s - 1) * o->HW + c);
             cost_now = fmaf(tc, w, cost_now);
             wn += w;
             float d0 = cam->c[0] - o->cam[s].c[0], d1 = cam->c[1] - o->cam[s].c[1], d2 = cam->c[2] - o->cam[s].c[2];
@@ -1338,7 +1398,7 @@ static void k_local_refine(octx *o, int px, int py) {
         float tc = 0.0f;
         for (int s = 1; s <= N; ++s) {
             if (is_set(sv, s - 1)) {
-                float w = (float)o->vw[(size_t)(s - 1) * o->HW + c];
+                float w = (float)RD(o, vw, (size_t)(s - 1) * o->HW + c);
                 tc = fmaf(o_ncc_old(o, px, py, s, t), w, tc);
                 if (geom) tc = fmaf(gf * o_geom_cost(o, px, py, s, t), w, tc);
             }
@@ -1346,12 +1406,13 @@ static void k_local_refine(octx *o, int px, int py) {
         tc /= wn;
         if (tc < min_cost) { min_cost = tc; best = pdepth; }
     }
-    if ((double)(cost_now - min_cost) > 0.1) o->plane[c].w = best;
+    if ((double)(cost_now - min_cost) > 0.1) WR(o, plane, c).w = best;
 }
 
 /* ------------------------------------------------------------------------------------------------
  * RunPatchMatch, APD.cu:2663-2737
  * ----------------------------------------------------------------------------------------------*/
+#ifndef ORACLE_RACECHECK
 #define FOR_ALL(o, body)                                                   \
     _Pragma("omp parallel for schedule(dynamic, 4)")                       \
     for (int py = 0; py < (o)->H; ++py)                                    \
@@ -1360,6 +1421,54 @@ static void k_local_refine(octx *o, int px, int py) {
     _Pragma("omp parallel for schedule(dynamic, 4)")                       \
     for (int py = 0; py < (o)->row_limit; ++py)                            \
         for (int px = ((py + (colour)) & 1); px < (o)->W; px += 2) { body; }
+#else
+/* one phase = one launch of the reference: fresh access sets, each pixel a task */
+static void rc_phase(const octx *o, const char *fn, int line, int colour) {
+    const size_t HW = (size_t)o->HW;
+    for (int a = 0; a < RC_COUNT; ++a) {
+        size_t n = HW;
+        if (a == RC_vw) n = HW * (size_t)o->N;
+        else if (a == RC_nearest) n = 2 * HW;
+        else if (a == RC_anchors) n = (size_t)(o->weak_count > 0 ? o->weak_count : 1) * ANCHOR_NUM * 2;
+        else if (a == RC_curve) n = o->curve ? HW * 61 : 0;
+        rc_shadow *sh = &rc_sh[a];
+        if (n > sh->cap) {
+            free(sh->wr); free(sh->rd);
+            sh->wr = (int32_t *)malloc((n ? n : 1) * sizeof(int32_t));
+            sh->rd = (int32_t *)malloc((n ? n : 1) * sizeof(int32_t));
+            sh->cap = n;
+        }
+        sh->n = n;
+        memset(sh->wr, 0xff, n * sizeof(int32_t));
+        memset(sh->rd, 0xff, n * sizeof(int32_t));
+    }
+    snprintf(rc_phase_name, sizeof rc_phase_name, "%s:%d%s", fn, line,
+             colour < 0 ? "" : (colour ? " (colour 1)" : " (colour 0)"));
+    rc_phases++;
+}
+#define FOR_ALL(o, body)                                                   \
+    do {                                                                   \
+        rc_phase((o), __func__, __LINE__, -1);                             \
+        for (int py = 0; py < (o)->H; ++py)                                \
+            for (int px = 0; px < (o)->W; ++px) {                          \
+                rc_task = py * (o)->W + px;                                \
+                body;                                                      \
+            }                                                              \
+        rc_task = -1;                                                      \
+    } while (0)
+#define FOR_COLOUR(o, colour, body)                                        \
+    do {                                                                   \
+        if (rc_merge_colours && (colour)) break;                           \
+        rc_phase((o), __func__, __LINE__, rc_merge_colours ? -1 : (colour)); \
+        for (int py = 0; py < (o)->row_limit; ++py)                        \
+            for (int px = rc_merge_colours ? 0 : ((py + (colour)) & 1); px < (o)->W; \
+                 px += rc_merge_colours ? 1 : 2) {                         \
+                rc_task = py * (o)->W + px;                                \
+                body;                                                      \
+            }                                                              \
+        rc_task = -1;                                                      \
+    } while (0)
+#endif
 
 static double now_s(void) {
     struct timespec ts;
@@ -1374,25 +1483,25 @@ static void run_prepare(octx *o) {
         FOR_ALL(o, k_gen_anchors(o, px, py, K));
         FOR_ALL(o, {
             int c = py * o->W + px;
-            if (o->weak[c] == WEAK && o->reliable[c] != 1) o->weak[c] = UNKNOWN;
+            if (RD(o, weak, c) == WEAK && RD(o, reliable, c) != 1) WR(o, weak, c) = UNKNOWN;
         });
     }
     FOR_ALL(o, k_random_init(o, px, py));
     memcpy(o->sel, o->sel_next, (size_t)o->HW * sizeof(uint32_t));
 }
 static void run_iteration(octx *o, int it) {
-    FOR_COLOUR(o, 0, if (o->weak[py * o->W + px] != WEAK) k_sweep_strong(o, px, py, it));
-    FOR_COLOUR(o, 1, if (o->weak[py * o->W + px] != WEAK) k_sweep_strong(o, px, py, it));
+    FOR_COLOUR(o, 0, if (RD(o, weak, py * o->W + px) != WEAK) k_sweep_strong(o, px, py, it));
+    FOR_COLOUR(o, 1, if (RD(o, weak, py * o->W + px) != WEAK) k_sweep_strong(o, px, py, it));
     if (o->P.use_APD) {
         FOR_ALL(o, k_ransac_fit(o, px, py, it));
-        FOR_COLOUR(o, 0, if (o->weak[py * o->W + px] == WEAK) k_sweep_weak(o, px, py, it));
-        FOR_COLOUR(o, 1, if (o->weak[py * o->W + px] == WEAK) k_sweep_weak(o, px, py, it));
+        FOR_COLOUR(o, 0, if (RD(o, weak, py * o->W + px) == WEAK) k_sweep_weak(o, px, py, it));
+        FOR_COLOUR(o, 1, if (RD(o, weak, py * o->W + px) == WEAK) k_sweep_weak(o, px, py, it));
     }
 }
 static void run_finish(octx *o) {
     FOR_ALL(o, k_depth_normal(o, px, py));
-    FOR_COLOUR(o, 0, if (o->weak[py * o->W + px] != WEAK) k_filter(o, px, py));
-    FOR_COLOUR(o, 1, if (o->weak[py * o->W + px] != WEAK) k_filter(o, px, py));
+    FOR_COLOUR(o, 0, if (RD(o, weak, py * o->W + px) != WEAK) k_filter(o, px, py));
+    FOR_COLOUR(o, 1, if (RD(o, weak, py * o->W + px) != WEAK) k_filter(o, px, py));
     FOR_ALL(o, k_depth_to_weak(o, px, py));
     if (o->P.geom_consistency || o->P.use_APD) FOR_ALL(o, k_confidence(o, px, py));
     FOR_ALL(o, k_local_refine(o, px, py));
@@ -1439,7 +1548,7 @@ static int ctx_init(octx *o, const apd_problem *pb) {
     if (pb->params.state != APD_FIRST_INIT && pb->init_planes) memcpy(o->plane, pb->init_planes, HW * sizeof(f4));
     /* anchors_map = running row-major index of WEAK pixels (APD.cpp:627-640) */
     int32_t wc = 0;
-    for (size_t i = 0; i < HW; ++i) o->amap[i] = (o->P.use_APD && o->weak[i] == WEAK) ? wc++ : -1;
+    for (size_t i = 0; i < HW; ++i) WR(o, amap, i) = (o->P.use_APD && RD(o, weak, i) == WEAK) ? wc++ : -1;
     o->weak_count = wc;
     o->anchors = (int16_t *)calloc((size_t)(wc > 0 ? wc : 1) * ANCHOR_NUM * 2, sizeof(int16_t));
     if (!o->anchors) return APD_ENOMEM;
@@ -1563,8 +1672,8 @@ float oracle_ncc_new(const apd_problem *pb, int px, int py, int src, const float
                      const uint32_t *sel) {
     octx *o = (octx *)malloc(sizeof(octx));
     float r = -1.0f;
-    if (kat_ctx(o, pb) == APD_OK && o->amap[px + py * o->W] >= 0) {
-        memcpy(&o->anchors[2 * (o->amap[px + py * o->W] * ANCHOR_NUM)], anchors9, ANCHOR_NUM * 2 * sizeof(int16_t));
+    if (kat_ctx(o, pb) == APD_OK && RD(o, amap, px + py * o->W) >= 0) {
+        memcpy(&o->anchors[2 * (RD(o, amap, px + py * o->W) * ANCHOR_NUM)], anchors9, ANCHOR_NUM * 2 * sizeof(int16_t));
         if (sel) memcpy(o->sel, sel, (size_t)o->HW * sizeof(uint32_t));
         f4 p = {plane4[0], plane4[1], plane4[2], plane4[3]};
         r = o_ncc_new(o, px, py, src, p);
@@ -1599,8 +1708,8 @@ int oracle_kat_stage(const apd_problem *pb, int stage, const uint32_t *sel, cons
     if (conf) memcpy(o->conf, conf, HW);
     switch (stage) {
     case 0:
-        FOR_COLOUR(o, 0, if (o->weak[py * o->W + px] != WEAK) k_filter(o, px, py));
-        FOR_COLOUR(o, 1, if (o->weak[py * o->W + px] != WEAK) k_filter(o, px, py));
+        FOR_COLOUR(o, 0, if (RD(o, weak, py * o->W + px) != WEAK) k_filter(o, px, py));
+        FOR_COLOUR(o, 1, if (RD(o, weak, py * o->W + px) != WEAK) k_filter(o, px, py));
         break;
     case 1:
         FOR_ALL(o, k_confidence(o, px, py));
@@ -1614,7 +1723,7 @@ int oracle_kat_stage(const apd_problem *pb, int stage, const uint32_t *sel, cons
         FOR_ALL(o, k_gen_anchors(o, px, py, K));
         FOR_ALL(o, {
             int c = py * o->W + px;
-            if (o->weak[c] == WEAK && o->reliable[c] != 1) o->weak[c] = UNKNOWN;
+            if (RD(o, weak, c) == WEAK && RD(o, reliable, c) != 1) WR(o, weak, c) = UNKNOWN;
         });
         break;
     }
@@ -1633,3 +1742,19 @@ int oracle_kat_stage(const apd_problem *pb, int stage, const uint32_t *sel, cons
     free(o);
     return st;
 }
+
+#ifdef ORACLE_RACECHECK
+/* access-set report since the last call (and reset): returns the number of conflicts; phases and
+ * accesses counted, the first conflict described in `first`. merge_colours: the negative control
+ * (see rc_merge_colours) for the runs that follow. */
+int64_t oracle_racecheck_report(int merge_colours, int64_t *phases, int64_t *accesses, char *first, int first_len) {
+    const int64_t c = rc_conflicts;
+    if (phases) *phases = rc_phases;
+    if (accesses) *accesses = rc_accesses;
+    if (first && first_len > 0) snprintf(first, (size_t)first_len, "%s", rc_conflicts ? rc_first : "");
+    rc_conflicts = rc_phases = rc_accesses = 0;
+    rc_first[0] = 0;
+    rc_merge_colours = merge_colours;
+    return c;
+}
+#endif

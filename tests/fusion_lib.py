@@ -41,6 +41,7 @@ def oracle():
 
 
 def hostlib():
+    A.torch_runtime_first()  # libapdhost.so links libapd_hip.so
     lib = C.CDLL(HOST_SO)
     lib.apdhost_read_bgr8.restype = C.c_long
     lib.apdhost_read_bgr8.argtypes = [C.c_char_p, C.c_void_p, C.c_long, C.POINTER(C.c_int), C.POINTER(C.c_int)]

@@ -6,7 +6,8 @@ APD passes at full size. Every view's final depths.bin / normals.bin / weak.bin 
 equal, bit for bit, the same schedule restated in Python (tests/host_schedule.py) driving the HIP
 library directly -- which the parity tests tie to the oracle. This checks the whole host side:
 image decode + resize, cam parsing, K scaling, prior resizing, anchors map, epilogue, bin-mat
-files, seeds, and the sequential vs jacobi pass orderings (jacobi on two device contexts).
+files, seeds, the sequential vs jacobi pass orderings (jacobi on two device contexts), and the
+single-context device-resident state (images and priors kept in HBM) against the host-upload path.
 """
 import os
 import subprocess
@@ -63,16 +64,24 @@ def check_outputs(folder, expected):
         assert (depth > 0).mean() > 0.5
 
 
-@pytest.mark.parametrize("ordering,gpus", [("sequential", "0"), ("jacobi", "0,0")])
-def test_cli_matches_schedule(scan, engine, ordering, gpus, tmp_path):
+@pytest.mark.parametrize("ordering,gpus,device_state", [
+    ("sequential", "0", "1"),   # one context: images and depth/plane priors resident in HBM
+    ("sequential", "0", "0"),   # APD_DEVICE_STATE=0: every input uploaded from the host per problem
+    ("jacobi", "0", "1"),       # resident state with this pass's maps held back until the pass ends
+    ("jacobi", "0,0", "1"),     # two contexts: host-side state (the device store is single-context)
+])
+def test_cli_matches_schedule(scan, engine, ordering, gpus, device_state, tmp_path):
     import shutil
     folder = str(tmp_path / "run")
     shutil.copytree(scan, folder)
+    env = dict(os.environ, APD_DEVICE_STATE=device_state)
     r = subprocess.run([APD_BIN, "--dense_folder", folder, "--dataset", "ETH3D", "--no_fuse", "true",
                         "--memory_cache", "false", "--gpus", gpus, "--ordering", ordering],
-                       capture_output=True, text=True, timeout=600)
+                       capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "Round nums: 2" in r.stdout
+    resident = device_state == "1" and "," not in gpus
+    assert ("Device-resident state:" in r.stdout) == resident
     assert r.stdout.count("RunPatchMatch time:") == 5 * 8
     expected = HS.run_schedule(folder, run_engine(engine), ordering=ordering)
     check_outputs(folder, expected)

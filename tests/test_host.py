@@ -23,6 +23,7 @@ def hostlib():
     if not os.path.exists(os.path.join(REPO, "apde-mvs_amd", "lib", "libapd_hip.so")):
         subprocess.run(["make", "-C", os.path.join(REPO, "apde-mvs_amd")], check=True, capture_output=True)
     subprocess.run(["make", "-C", HOST], check=True, capture_output=True)
+    A.torch_runtime_first()  # libapdhost.so links libapd_hip.so
     lib = C.CDLL(HOST_LIB)
     lib.apdhost_read_gray8.restype = C.c_long
     lib.apdhost_read_gray8.argtypes = [C.c_char_p, C.c_void_p, C.c_long, C.POINTER(C.c_int), C.POINTER(C.c_int)]
