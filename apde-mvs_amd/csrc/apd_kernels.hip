@@ -42,9 +42,19 @@ using namespace apd;
         }                                                                                    \
     } while (0)
 #define PHASE_BEGIN long long t_phase_ = clock64()
+// lane-use statistics (instrumented builds): slot += waves that issue the task, slot + 1 += active lanes
+#define LANE_STAT(slot, pred)                                                                \
+    do {                                                                                     \
+        const unsigned long long b_ = __ballot(pred);                                        \
+        if (a.evals && b_ && (threadIdx.x & 63) == 0) {                                      \
+            atomicAdd(a.evals + (slot), 1ull);                                               \
+            atomicAdd(a.evals + (slot) + 1, (unsigned long long)__builtin_popcountll(b_));   \
+        }                                                                                    \
+    } while (0)
 #else
 #define PHASE_STAMP(i) do { } while (0)
 #define PHASE_BEGIN do { } while (0)
+#define LANE_STAT(slot, pred) do { } while (0)
 #endif
 #ifndef APD_SWEEP_WAVES
 #define APD_SWEEP_WAVES 2  // min waves per SIMD requested for the sweep kernels (VGPR budget 512/w)
@@ -87,6 +97,19 @@ __device__ __forceinline__ float *lds_slot(const Group &G, int P, int floats_per
 }
 static inline size_t group_lds_bytes(int N, int floats_per_px) {
     return (size_t)(BLOCK / WAVE) * (WAVE / N) * floats_per_px * sizeof(float);
+}
+// position of the r-th (0-based) set bit of m (m has more than r set bits)
+__device__ __forceinline__ int nth_set_bit(uint64_t m, int r) {
+    int pos = 0;
+    uint32_t x = (uint32_t)m;
+    int c = __builtin_popcount(x);
+    if (r >= c) { r -= c; pos = 32; x = (uint32_t)(m >> 32); }
+#pragma unroll
+    for (int w = 16; w >= 1; w >>= 1) {
+        c = __builtin_popcount(x & ((1u << w) - 1u));
+        if (r >= c) { r -= c; pos += w; x >>= w; }
+    }
+    return pos;
 }
 __device__ __forceinline__ uint32_t group_bits(bool pred, const Group &G) {
     unsigned long long m = __ballot(pred);
@@ -1498,6 +1521,7 @@ struct WvLdsT : WvRefT<F16> {
     float st[4 * VM_P];          // depth_now, cost_now, cost_init, weight norm
     uint32_t tsel[VM_P];         // views with weight > 0 (the selection the best anchor hypothesis brings)
     uint16_t rng_n[VM_P];
+    int pxy[VM_P];               // packed (x, y) of pixel slot p (P5's packed items)
 };
 #define WV_CAND(L) ((L).hyp)
 // 52.2 KiB with the cost table at N = 8 (fp16 reference taps): three workgroups per CU.
@@ -1774,6 +1798,12 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
 #ifndef WV_WAVES
 #define WV_WAVES 4  // waves per Weak-sweep workgroup (64 pixels)
 #endif
+#ifndef WV_P5_PACKED
+#define WV_P5_PACKED 1  // P5's (candidate, pixel) items packed per view into dense lanes
+#endif
+#ifndef WV_P5_CHUNKS
+#define WV_P5_CHUNKS 3  // P5 batches: whole views until at least this many 64-item chunks
+#endif
 #define WV_BLOCK (WV_WAVES * WAVE)
 template <bool F16>
 __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
@@ -1838,6 +1868,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             }
             L.flags[p1] = hflag | (awin << 16);
             L.hyp[8 * VM_P + p1] = cur;
+            L.pxy[p1] = px1 | (py1 << 16);
         }
         wv_build_windows<F16>(a, L, p1, anc, cid, wave, WV_WAVES);
     }
@@ -1963,6 +1994,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     for (int v = wave; v < N; v += WV_WAVES) {
         float val = 0.0f;
         const bool want = pv1 && wts[v * VM_P + p1] > 0;
+        LANE_STAT(24, want);
         if (__ballot(want)) {
             const float4 pl = L.hyp[8 * VM_P + p1];
             float nv;
@@ -2059,6 +2091,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         if (v < N) {
             float cv = 0.0f;
             const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[p1];
+            LANE_STAT(22, want);
             const float4 fit = fit1;
             const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, fit, want);
             if (want) {
@@ -2106,6 +2139,88 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     __syncthreads();
     PHASE_STAMP(4);
 
+#if WV_P5_PACKED
+    // ---- P5: candidate evaluations (views with weight > 0), early exit against the cost after the fit
+    // plane (slots 1..5). Per view the (candidate, pixel) items that are still wanted are packed into
+    // dense lanes (a (candidate, view) task keeps only ~half of its 64 lanes: the view's weight is 0 or
+    // the candidate is already rejected), in (candidate, pixel) order; a wave takes 64 items of ONE view
+    // (the waves still sample one source image). Batches of whole views (at least WV_P5_CHUNKS chunks,
+    // dealt round-robin over the waves) end with the fold, so a rejection found in a batch stops the
+    // candidate's later views. Item masks are ballots of LDS state every wave computes alike.
+    {
+        auto view_masks = [&](int v, uint64_t (&m)[5]) {
+            const bool base = refine && wts[v * VM_P + p1] > 0;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) m[k] = __ballot(base && !dead[(1 + k) * VM_P + p1]);
+        };
+        for (int v0 = 0; v0 < N;) {
+            int v1 = v0, nch = 0;
+            while (v1 < N && nch < WV_P5_CHUNKS) {
+                uint64_t m[5];
+                view_masks(v1, m);
+                int t = 0;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) t += __builtin_popcountll(m[k]);
+                nch += (t + WAVE - 1) / WAVE;
+                ++v1;
+            }
+            int g = 0;  // chunk index within the batch
+            for (int v = v0; v < v1; ++v) {
+                uint64_t m[5];
+                view_masks(v, m);
+                int off[6];
+                off[0] = 0;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) off[k + 1] = off[k] + __builtin_popcountll(m[k]);
+                const int nv_items = off[5];
+                for (int j = 0; j * WAVE < nv_items; ++j, ++g) {
+                    if (g % WV_WAVES != wave) continue;
+                    const int it = j * WAVE + lane;
+                    const bool want = it < nv_items;
+                    int k = 0;
+#pragma unroll
+                    for (int q = 1; q < 5; ++q) k += it >= off[q];
+                    uint64_t mk = m[0];
+#pragma unroll
+                    for (int q = 1; q < 5; ++q) if (k == q) mk = m[q];
+                    int pk = 0;
+#pragma unroll
+                    for (int q = 1; q < 5; ++q) if (k == q) pk = off[q];
+                    const int p = want ? nth_set_bit(mk, it - pk) : p1;
+                    const int pxy = L.pxy[p];
+                    const int px = pxy & 0xFFFF, py = pxy >> 16;
+                    const float4 tp = WV_CAND(L)[k * VM_P + p];
+                    LANE_STAT(20, want);
+                    const float nv = ncc_new_vm<F16>(a, L, p, px, py, v + 1, tp, want);
+                    if (want) {
+                        float cv = nv;
+                        if (geom) cv = fmaf(gf, geom_cost(a, px, py, v + 1, tp), cv);
+                        ++issued_nn;
+                        issued_g += geom;
+                        costL[(k * N + v) * VM_P + p] = cv;
+                    }
+                }
+            }
+            __syncthreads();
+            // fold views [nxt, v1) of the refining pixels' 5 slots (all threads: slot 1 + i / 64)
+            for (int i = tid; i < 5 * VM_P; i += WV_BLOCK) {
+                const int k = i / VM_P, p = i - k * VM_P, sl = (1 + k) * VM_P + p;
+                if (dead[sl] || !(p < np && (L.flags[p] >> 31))) continue;
+                int v = nxt[sl];
+                float P = part[sl];
+                for (; v < v1; ++v) {
+                    const int wk = wts[v * VM_P + p];
+                    if (wk > 0) P = fmaf((float)wk, costL[(k * N + v) * VM_P + p], P);
+                }
+                nxt[sl] = (uint8_t)v;
+                part[sl] = P;
+                if (P / L.st[3 * VM_P + p] >= L.st[1 * VM_P + p]) dead[sl] = 1;
+            }
+            __syncthreads();
+            v0 = v1;
+        }
+    }
+#else
     // ---- P5: candidate tasks (views with weight > 0), view-major, early exit against the cost after
     // the fit plane (slots 1..5)
     for (int u0 = 0; u0 < 5 * N; u0 += WV_WAVES) {
@@ -2116,6 +2231,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             const int v = u / 5, k = u - 5 * v, t = k * N + v;
             float cv = 0.0f;
             const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[(1 + k) * VM_P + p1];
+            LANE_STAT(20, want);
             const float4 tp = WV_CAND(L)[k * VM_P + p1];
             const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, tp, want);
             if (want) {
@@ -2128,6 +2244,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         }
         __syncthreads();
     }
+#endif
     PHASE_STAMP(5);
 
     if (a.evals && wave == 0) {
@@ -2596,6 +2713,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
             project(Hm, (float)ax, (float)ay, asx, asy);
             bool live = act;
             float res = -1.0f;  // absent
+            LANE_STAT(26, act);
             if (act && (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H)) {
                 live = false;
                 if ((a.sel[ax + ay * W] >> (s - 1)) & 1u) res = APD_COST_MAX;
@@ -2622,6 +2740,7 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
             for (int h = wave; h < 8; h += PK_WAVES) {
                 const bool want = (cb >> h) & 1u;
                 const uint16_t hid = L.aid[h * VM_P + p1];
+                LANE_STAT(28, want);
                 const float4 pl = want ? L.apl[hid] : make_float4(0.0f, 0.0f, 1.0f, 1.0f);
                 const Hom Hm = homography(a, s, pl);
                 float ptx, pty;
