@@ -23,6 +23,7 @@
 
 #include "../../include/apd_hip.h"
 #include "apd_device.h"
+#include <rocprim/device/device_scan.hpp>
 
 using namespace apd;
 
@@ -2718,6 +2719,9 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
                 live = false;
                 if ((a.sel[ax + ay * W] >> (s - 1)) & 1u) res = APD_COST_MAX;
             }
+#ifdef APD_ABLATE_PAIRS  // timing-only (wrong values): no pair-window taps
+            live = false;
+#endif
             if (__ballot(live)) {
                 const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
                 float ss = 0.0f, sss = 0.0f, srs = 0.0f;
@@ -2822,6 +2826,447 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
         PHASE_STAMP(11);
     }
 }
+
+// ---------------------------------------------------------------------------------------------
+// Image-wide anchor-window pairs (no SA masks). A WEAK pixel's anchor candidate h (the plane of its
+// STRONG anchor h+1) is scored by ComputeBilateralNCCNew (APD.cu:448-593): the centre window at its
+// anchor 0 and the 3x3 windows at its anchors 1..8, combined by the focal softmax. The cost of the
+// window at anchor k under the plane of anchor h in view v is a function of (position of k, position
+// of h, v) only -- the out-of-frame rule reads sel[k], which only the Strong sweep writes -- and the
+// anchors are STRONG points on the borders of the textureless regions, shared by the region's pixels:
+// at C3 (6048x4032, N = 10) 1.43 G (window, candidate) pairs per view are 102.6 M distinct pairs
+// image-wide (13.9x), against 2.1x within a 64-pixel group (tools/pair_sharing.py). So:
+//   per pass (apd_stage_prepare, anchors fixed): the (pixel, window slot) references are counting-
+//     sorted by window anchor (k_gp_count, scan, k_gp_fill); chunks of GP_CHUNK consecutive
+//     references deduplicate their (window anchor, candidate anchor) pairs in an LDS hash
+//     (k_gp_dedup: pass 0 counts, a scan places the chunks, pass 1 writes the pair list and every
+//     (pixel, candidate, window) slot's pair id). Pair ids are labels: their order (atomics) may
+//     differ between runs, the costs never do.
+//   per iteration: k_gp_cost evaluates every pair in every view (lane = pair, consecutive pairs share
+//     a window anchor) into pcost[pair][view]; k_weak_cand_g evaluates the centre windows (lane =
+//     pixel, wave = candidate) and the focal combination reading the pair costs, and writes the same
+//     [view][candidate][WEAK index] costs as k_weak_cand_vm.
+// ---------------------------------------------------------------------------------------------
+#define GP_CHUNK 256   // references per batch of k_gp_dedup (one workgroup per window anchor)
+#define GP_HS 8192     // LDS hash slots (a table closes at GP_HS / 2 keys; + <= 8 * GP_CHUNK per batch: load <= 0.75)
+#define GP_NONE 0xFFFFFFFFu
+
+// Lanes are consecutive WEAK pixels in tile order, whose anchor k is often the same STRONG point: per
+// slot k the runs of equal anchors among neighbouring lanes take one atomic (run head).
+__device__ __forceinline__ void gp_run(bool ok, int q, int &head_lane, int &rank, int &len) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int qp = __shfl_up(q, 1);
+    const bool okp = __shfl_up((int)ok, 1) != 0;
+    const bool head = ok && (lane == 0 || !okp || qp != q);
+    const unsigned long long hb = __ballot(head);
+    // run head of this lane: the highest head at or below it
+    const unsigned long long below = hb & ((lane == 63) ? ~0ull : ((2ull << lane) - 1ull));
+    head_lane = below ? 63 - __builtin_clzll(below) : 0;
+    rank = lane - head_lane;
+    // run length (heads only): distance to the next head or to the end of the run
+    const unsigned long long okb = __ballot(ok);
+    const unsigned long long above = (lane == 63) ? 0ull : (hb | ~okb) & ~((2ull << lane) - 1ull);
+    const int end = above ? __builtin_ctzll(above) : 64;
+    len = end - lane;
+}
+// references per window anchor (cnt) and each WEAK pixel's candidate bits (cbw: anchor h+1 valid and STRONG)
+__global__ __launch_bounds__(BLOCK) void k_gp_count(Args a, const int *__restrict__ list, int count, int *__restrict__ cnt,
+                                                    uint8_t *__restrict__ cbw) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < count;
+    const int wi = a.amap[list[act ? i : count - 1]];
+    const APD_G short2 *anc = a.anchors + (size_t)wi * 9;
+    uint32_t cb = 0;
+#pragma unroll 1
+    for (int k = 1; k < 9; ++k) {
+        const short2 ap = anc[k];
+        const bool ok = act && !(ap.x == -1 || ap.y == -1);
+        const int q = ok ? ap.x + ap.y * a.W : -1;
+        if (ok && a.weak[q] == APD_STRONG) cb |= 1u << (k - 1);
+        int hl, rk, len;
+        gp_run(ok, q, hl, rk, len);
+        if (ok && rk == 0) atomicAdd(&cnt[q], len);
+    }
+    if (act) cbw[wi] = (uint8_t)cb;
+}
+// references (WEAK index * 8 + window slot k - 1) into their window anchor's segment
+__global__ __launch_bounds__(BLOCK) void k_gp_fill(Args a, const int *__restrict__ list, int count, int *__restrict__ cur,
+                                                   uint32_t *__restrict__ refs) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < count;
+    const uint32_t wi = (uint32_t)a.amap[list[act ? i : count - 1]];
+    const APD_G short2 *anc = a.anchors + (size_t)wi * 9;
+#pragma unroll 1
+    for (int k = 1; k < 9; ++k) {
+        const short2 ap = anc[k];
+        const bool ok = act && !(ap.x == -1 || ap.y == -1);
+        const int q = ok ? ap.x + ap.y * a.W : -1;
+        int hl, rk, len;
+        gp_run(ok, q, hl, rk, len);
+        int pos = 0;
+        if (ok && rk == 0) pos = atomicAdd(&cur[q], len);
+        pos = __shfl(pos, hl) + rk;
+        if (ok) refs[pos] = wi * 8u + (uint32_t)(k - 1);
+    }
+}
+// the window anchors that have references, in raster order (task list for k_gp_dedup): flags, then
+// (after an exclusive scan into pos) a scatter
+__global__ __launch_bounds__(BLOCK) void k_gp_flags(const int *__restrict__ off, int HW, int *__restrict__ flag) {
+    const int q = blockIdx.x * BLOCK + threadIdx.x;
+    if (q <= HW) flag[q] = (q < HW && off[q + 1] > off[q]) ? 1 : 0;
+}
+__global__ __launch_bounds__(BLOCK) void k_gp_tasks(const int *__restrict__ off, const int *__restrict__ pos, int HW,
+                                                    int *__restrict__ tasks) {
+    const int q = blockIdx.x * BLOCK + threadIdx.x;
+    if (q < HW && off[q + 1] > off[q]) tasks[pos[q]] = q;
+}
+// One workgroup per window anchor q (tasks[]): its references, in batches of GP_CHUNK, insert their
+// candidate anchors into an LDS hash (keys qh + 1), sized from the reference count; a table that
+// reaches GP_HS / 2 keys after a batch is closed (a new run of pairs for q starts, so an anchor with
+// more than ~4 k distinct candidates repeats a few pairs). Pass 0 counts the distinct pairs per
+// anchor (acnt); pass 1, from the scanned bases, writes each closed table's pairs (plist, slot order)
+// and then every (pixel, candidate, window) slot of the table's references (pidx).
+template <int PASS>
+__global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__restrict__ tasks, const int *__restrict__ off,
+                                                       const uint32_t *__restrict__ refs, const uint8_t *__restrict__ cbw,
+                                                       int *__restrict__ acnt,
+                                                       const int *__restrict__ abase, int2 *__restrict__ plist,
+                                                       uint32_t *__restrict__ pidx) {
+    __shared__ uint32_t hs[GP_HS];
+    __shared__ uint16_t sid[GP_HS];
+    __shared__ int scan_w[GP_CHUNK / WAVE + 1];
+    __shared__ int nfresh;
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid >> 6;
+    const int q = tasks[blockIdx.x];
+    const int r0 = off[q], n = off[q + 1] - r0;
+    const int qx = q % a.W, qy = q / a.W;
+    int cap = 256, lg = 8;
+    while (cap < GP_HS && cap < n * 16) { cap <<= 1; ++lg; }
+    const uint32_t msk = (uint32_t)cap - 1u;
+    auto slot_of = [&](uint32_t key) { return (key * 0x9E3779B1u) >> (32 - lg); };
+    // candidates (valid, STRONG anchors 1..8) of reference r: bits + positions
+    auto cands = [&](int r, uint32_t &wi, uint32_t &k, uint32_t (&qh)[8]) {
+        const uint32_t ref = refs[r];
+        wi = ref >> 3;
+        k = ref & 7u;
+        const APD_G short2 *anc = a.anchors + (size_t)wi * 9;
+        const uint32_t cb = cbw[wi];
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            const short2 ap = anc[h + 1];
+            qh[h] = (uint32_t)(ap.x + ap.y * a.W);  // (used only where cb has the bit: a valid anchor)
+        }
+        return cb;
+    };
+    for (int i = tid; i < cap; i += GP_CHUNK) hs[i] = 0u;
+    if (tid == 0) nfresh = 0;
+    __syncthreads();
+    int base = PASS ? abase[blockIdx.x] : 0, total = 0;
+    int run0 = 0;  // first reference of the open table
+    for (int b0 = 0; b0 < n; b0 += GP_CHUNK) {
+        const int r = b0 + tid;
+        if (r < n) {
+            uint32_t wi, k, qh[8];
+            const uint32_t cb = cands(r0 + r, wi, k, qh);
+            int fresh = 0;
+#pragma unroll
+            for (int h = 0; h < 8; ++h) {
+                if (!((cb >> h) & 1u)) continue;
+                const uint32_t key = qh[h] + 1u;
+                uint32_t sl = slot_of(key);
+                for (;;) {
+                    const uint32_t old = atomicCAS(&hs[sl], 0u, key);
+                    if (old == 0u) { ++fresh; break; }
+                    if (old == key) break;
+                    sl = (sl + 1) & msk;
+                }
+            }
+            if (fresh) atomicAdd(&nfresh, fresh);
+        }
+        __syncthreads();
+        const int nd = nfresh;
+        const bool close = nd >= GP_HS / 2 || b0 + GP_CHUNK >= n;
+        if (!close) continue;  // (uniform)
+        if (PASS == 1) {
+            // plist[base + id] = (window anchor, candidate anchor)
+            const int per = cap / GP_CHUNK;  // slots per thread (cap >= GP_CHUNK)
+            const int s0 = tid * per, s1 = s0 + per;
+            int c = 0;
+            for (int sl = s0; sl < s1; ++sl) c += hs[sl] != 0u;
+            int x = c;
+#pragma unroll
+            for (int o = 1; o < WAVE; o <<= 1) {
+                const int y = __shfl_up(x, o);
+                if (lane >= o) x += y;
+            }
+            if (lane == WAVE - 1) scan_w[wave] = x;
+            __syncthreads();
+            int next = x - c;
+            for (int w = 0; w < wave; ++w) next += scan_w[w];
+            // ids in slot order (ranking the candidates by raster position, so that a group's pixels
+            // read neighbouring rows of pcost, measured: k_weak_cand_g -1 %, this pass +93 %)
+            for (int sl = s0; sl < s1; ++sl) {
+                const uint32_t key = hs[sl];
+                if (!key) continue;
+                plist[base + next] = make_int2(qx | (qy << 16), (int)(key - 1u));
+                sid[sl] = (uint16_t)next;
+                ++next;
+            }
+            __syncthreads();
+            // the table's references: pair ids of their (candidate, window) slots
+            for (int rr = run0 + tid; rr < min(n, b0 + GP_CHUNK); rr += GP_CHUNK) {
+                uint32_t wi, k, qh[8], pv[8];
+                const uint32_t cb = cands(r0 + rr, wi, k, qh);
+#pragma unroll
+                for (int h = 0; h < 8; ++h) {
+                    pv[h] = GP_NONE;
+                    if (!((cb >> h) & 1u)) continue;
+                    const uint32_t key = qh[h] + 1u;
+                    uint32_t sl = slot_of(key);
+                    while (hs[sl] != key) sl = (sl + 1) & msk;
+                    pv[h] = (uint32_t)(base + sid[sl]);
+                }
+                uint4 *dst = reinterpret_cast<uint4 *>(pidx + ((size_t)wi * 8 + k) * 8);  // [WEAK index][window k][candidate h]
+                dst[0] = make_uint4(pv[0], pv[1], pv[2], pv[3]);
+                dst[1] = make_uint4(pv[4], pv[5], pv[6], pv[7]);
+            }
+            __syncthreads();
+        }
+        base += nd;
+        total += nd;
+        run0 = b0 + GP_CHUNK;
+        for (int i = tid; i < cap; i += GP_CHUNK) hs[i] = 0u;
+        __syncthreads();
+        if (tid == 0) nfresh = 0;
+        __syncthreads();
+    }
+    if (PASS == 0 && tid == 0) acnt[blockIdx.x] = total;
+}
+
+// every pair in every view: ComputeBilateralNCCNew's k >= 1 window (APD.cu:500-575), the same
+// statements as k_weak_cand_vm's pair windows; pcost[pair][v] rows padded to a multiple of 4 views
+// (< 0: window absent)
+template <bool F16>
+__global__ __launch_bounds__(BLOCK) void k_gp_cost(Args a, const int2 *__restrict__ plist, int np, float *__restrict__ pcost) {
+    using RT = typename std::conditional<F16, _Float16, float>::type;
+    __shared__ RT rref[9 * BLOCK];
+    const int N = a.N, W = a.W, H = a.H;
+    const int i = xcd_remap(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+    const bool act = i < np;
+    const int2 pr = plist[act ? i : np - 1];
+    const int ax = pr.x & 0xFFFF, ay = pr.x >> 16;
+    const float4 pl = a.plane[pr.y];
+    float sr = 0.0f, srr = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        const int ii = t / 3, jj = t - 3 * (t / 3);
+        const float r = tex_ref(a, ax - 5 + 5 * ii, ay - 5 + 5 * jj);
+        rref[t * BLOCK + threadIdx.x] = (RT)r;
+        sr += r;
+        srr = fmaf(r, r, srr);
+    }
+    const uint32_t selk = a.sel[ax + ay * W];
+    for (int v = 0; v < N; ++v) {
+        const int s = v + 1;
+        const FastTex<F16, true> T(a, s);
+        const SrcTex<F16> Q(a, s);
+        const Hom Hm = homography(a, s, pl);
+        float asx, asy;
+        project(Hm, (float)ax, (float)ay, asx, asy);
+        bool live = act;
+        float res = -1.0f;  // absent
+        if (act && (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H)) {
+            live = false;
+            if ((selk >> (s - 1)) & 1u) res = APD_COST_MAX;
+        }
+        if (__ballot(live)) {
+            const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
+            float ss = 0.0f, sss = 0.0f, srs = 0.0f;
+            ncc_new_window<F16, 3, 5>(a, &rref[threadIdx.x], BLOCK, 0x1FFull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            if (live) res = ncc_finalize(sr, srr, ss, sss, srs, 9.0f);
+        }
+        if (act) pcost[(size_t)i * ((N + 3) & ~3) + v] = res;
+    }
+}
+
+// the anchor candidates' costs from the pair costs: centre windows + focal combination (as
+// k_weak_cand_vm's phase D, without SA masks); lane = pixel, wave = candidate h.
+//   A  per view (the waves take the views together: one source image, the CU's L1): the centre
+//      window of (pixel, h) -> LDS ccost[v][h][p] (-1: dead, the pixel or its anchor 0 out of frame)
+//   B  per (pixel, h): the 8 windows' pair costs, 4 views per 16-byte load, and the focal
+//      combination of each view
+template <bool F16>
+__global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__restrict__ list, int count,
+                                                          const uint8_t *__restrict__ cbw, const uint32_t *__restrict__ pidx,
+                                                          const float *__restrict__ pcost,
+                                                          float *__restrict__ out, uint8_t *__restrict__ done, int wc) {
+    using RT = typename std::conditional<F16, _Float16, float>::type;
+    __shared__ RT cref[36 * VM_P];
+    __shared__ float csr[VM_P], csrr[VM_P];
+    __shared__ uint8_t cws[VM_P], cbits[VM_P];
+    __shared__ int anc0[VM_P];
+    extern __shared__ float ccost[];  // [N][8][64]
+    const int N = a.N, W = a.W, H = a.H;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int first = blk * VM_P;
+    const int np = min(VM_P, count - first);
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
+    const int p1 = lane;
+    const bool pv1 = p1 < np;
+    const int c1 = list[first + min(p1, np - 1)];
+    const int py1 = c1 / W, px1 = c1 - py1 * W;
+    const int wi1 = a.amap[c1];
+    const APD_G short2 *anc1 = a.anchors + (size_t)wi1 * 9;
+    if (wave == 0) {
+        int a0 = -1;
+        uint32_t cb = 0;
+        if (pv1) {
+            const short2 z = anc1[0];
+            a0 = (z.x == -1 || z.y == -1) ? -1 : ((int)(uint16_t)z.x | ((int)z.y << 16));
+            cb = cbw[wi1];
+            done[wi1] = 1;
+        }
+        anc0[p1] = a0;
+        cbits[p1] = (uint8_t)cb;
+    }
+    __syncthreads();
+    if (pv1 && anc0[p1] >= 0) {  // centre window reference taps, fetched by all waves
+        const int pk = anc0[p1];
+        const int ax = pk & 0xFFFF, ay = pk >> 16;
+        for (int t = wave; t < 36; t += PK_WAVES) {
+            const int i = t / 6, j = t - 6 * i;
+            cref[t * VM_P + p1] = (RT)tex_ref(a, ax - 5 + 2 * i, ay - 5 + 2 * j);
+        }
+    }
+    __syncthreads();
+    if (wave == 1) {  // moments in wv_build_windows's tap order
+        float sr = 0.0f, srr = 0.0f, ws = 0.0f;
+        if (pv1 && anc0[p1] >= 0) {
+            for (int t = 0; t < 36; ++t) {
+                const float r = (float)cref[t * VM_P + p1];
+                sr += r;
+                srr = fmaf(r, r, srr);
+                ws += 1.0f;
+            }
+        }
+        csr[p1] = sr;
+        csrr[p1] = srr;
+        cws[p1] = (uint8_t)ws;
+    }
+    __syncthreads();
+    const int h = wave;  // PK_WAVES == 8 candidates
+    const uint32_t cb = cbits[p1];
+    const bool want = pv1 && ((cb >> h) & 1u);
+    float4 pl = make_float4(0.0f, 0.0f, 1.0f, 1.0f);
+    if (want) {
+        const short2 ap = anc1[h + 1];
+        pl = a.plane[ap.x + ap.y * W];
+    }
+    // ---- A: centre windows
+    const int pk0 = anc0[p1];
+    for (int v = 0; v < N; ++v) {
+        const int s = v + 1;
+        const FastTex<F16, true> T(a, s);
+        const SrcTex<F16> Q(a, s);
+        const Hom Hm = homography(a, s, pl);
+        float ptx, pty;
+        project(Hm, (float)px1, (float)py1, ptx, pty);
+        const bool alive = want && !(ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f);
+        const bool has = alive && pk0 >= 0;
+        const int ax = has ? (pk0 & 0xFFFF) : px1, ay = has ? (pk0 >> 16) : py1;
+        bool live = has, dead = !alive;
+        if (has) {
+            float asx, asy;
+            project(Hm, (float)ax, (float)ay, asx, asy);
+            if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) { live = false; dead = true; }
+        }
+        float center_cost = 0.0f;
+#ifdef GP_ABLATE_A  // timing-only (wrong values): no centre-window taps
+        live = false;
+#endif
+        if (__ballot(live)) {
+            const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
+            float ss = 0.0f, sss = 0.0f, srs = 0.0f;
+            ncc_new_window<F16, 6, 2>(a, &cref[p1], VM_P, ~0ull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            if (live) {
+                const float wsum = (float)cws[p1];
+                if (wsum != 0.0f) center_cost = ncc_finalize(csr[p1], csrr[p1], ss, sss, srs, wsum);
+            }
+        }
+        ccost[(v * 8 + h) * VM_P + p1] = dead ? -1.0f : center_cost;
+#ifdef GP_VIEW_SYNC  // (measured: keeping the waves on one view costs more than the shared L1 gains)
+        __syncthreads();
+#endif
+    }
+    if (!want) return;  // (each lane reads back only its own entries: no barrier needed)
+    // ---- B: focal combination (APD.cu:576-593, Softmax 431-446) per view
+    const int Np = (N + 3) & ~3;
+    const float4 *pc4[8];
+    uint32_t pm0 = 0;  // windows whose pair exists (anchor k+1 valid)
+    {
+        const uint32_t *pp = pidx + (size_t)wi1 * 64 + h;  // [window k][candidate h]
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const short2 ak = anc1[k + 1];
+            const uint32_t id = pp[k * 8];
+            const bool ok = !(ak.x == -1 || ak.y == -1) && id != GP_NONE;
+            pc4[k] = reinterpret_cast<const float4 *>(pcost + (size_t)(ok ? id : 0u) * Np);
+            pm0 |= (uint32_t)ok << k;
+        }
+    }
+    for (int v0 = 0; v0 < N; v0 += 4) {
+        float4 q[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[k] = ((pm0 >> k) & 1u) ? pc4[k][v0 >> 2] : make_float4(-1.0f, -1.0f, -1.0f, -1.0f);
+#ifdef GP_ABLATE_B  // timing-only (wrong values): no pair-cost loads
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[k] = make_float4(0.5f, 0.5f, 0.5f, (float)k);
+#endif
+#pragma unroll
+        for (int dv = 0; dv < 4; ++dv) {
+            const int v = v0 + dv;
+            if (v >= N) break;
+            const float cc = ccost[(v * 8 + h) * VM_P + p1];
+            float cost;
+            if (cc < 0.0f) {
+                cost = APD_COST_MAX;
+            } else {
+                const float center_cost = cc;
+                float sc[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) sc[k] = dv == 0 ? q[k].x : dv == 1 ? q[k].y : dv == 2 ? q[k].z : q[k].w;
+                uint32_t pm = 0;
+                float strong_weight = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (sc[k] >= 0.0f) { pm |= 1u << k; strong_weight += 1.0f; }
+                if (strong_weight <= 1e-6f) {
+                    cost = center_cost;
+                } else {
+                    float mx = -1e10f;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) if (((pm >> k) & 1u) && sc[k] > mx) mx = sc[k];
+                    float e[8];
+                    float sum = 0.0f;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        e[k] = 0.0f;
+                        if ((pm >> k) & 1u) { e[k] = d_expf(sc[k] - mx); sum += e[k]; }
+                    }
+                    float acc = 0.0f;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if ((pm >> k) & 1u) { const float w = e[k] / sum; acc = fmaf(w, sc[k], acc); }
+                    acc = (acc > APD_COST_MAX) ? APD_COST_MAX : acc;
+                    cost = (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
+                }
+            }
+            out[((size_t)v * 8 + h) * (size_t)wc + wi1] = cost;
+        }
+    }
+}
+static inline size_t gp_cand_lds_bytes(int N) { return (size_t)N * 8 * VM_P * sizeof(float); }
 
 // ---------------------------------------------------------------------------------------------
 // CheckerboardPropagationWeak + PlaneHypothesisRefinementWeak (APD.cu:1442-1615, 1008-1096)
@@ -3907,7 +4352,7 @@ struct apd_ctx {
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
         fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, wdone, lrs, wcur,
-        wlist;
+        wlist, gp_cb, gp_cnt, gp_cur, gp_refs, gp_ccnt, gp_cbase, gp_plist, gp_pidx, gp_pcost, gp_tmp;
     int n_near = 0;
     int host_stat[4] = {0, 0, 0, 0};  // apd_set_problem's read-back (see there)
     int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
@@ -3917,6 +4362,9 @@ struct apd_ctx {
     int dw_tile_w = 8;             // DepthToWeak pixel tile width (64 / tile height); APD_DW_TILE_W
     int tile_w = 8;                // sweep list tile width (tile = tile_w x 256/tile_w positions); APD_TILE_W
     bool cand_pairs = true;        // Weak sweep candidates through k_weak_cand_vm; APD_NO_CAND_PAIRS=1 disables
+    bool cand_global = true;       // ... through the image-wide pair table (no SA); APD_NO_GLOBAL_PAIRS=1 disables
+    bool gp_on = false;            // the pair table of the prepared problem is built (apd_stage_prepare)
+    int gp_np = 0;                 // its distinct pairs
     bool lr_handover = true;       // LocalRefine reads DepthToWeak's samples; APD_NO_LR_HANDOVER=1 disables
     bool wcur_on = true;           // RandomInit keeps WEAK current-plane costs for iteration 0; APD_NO_WCUR=1 disables
     bool wcur_fresh = false;       // they belong to the current planes (set by prepare, cleared by iteration)
@@ -4118,6 +4566,7 @@ apd_ctx *apd_create(int32_t device) {
     for (auto &e : ctx->ev) (void)hipEventCreate(&e);
     ctx->sweep_vm = getenv("APD_SWEEP_LANES") == nullptr;
     ctx->cand_pairs = getenv("APD_NO_CAND_PAIRS") == nullptr;
+    ctx->cand_global = getenv("APD_NO_GLOBAL_PAIRS") == nullptr;
     ctx->lr_handover = getenv("APD_NO_LR_HANDOVER") == nullptr;
     ctx->wcur_on = getenv("APD_NO_WCUR") == nullptr;
     // tile_pix needs the tile width to divide the 64-pixel tile (otherwise two workgroups share pixels)
@@ -4155,7 +4604,8 @@ void apd_destroy(apd_ctx *ctx) {
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
                       &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand, &ctx->wdone,
-                      &ctx->lrs, &ctx->wcur, &ctx->wlist};
+                      &ctx->lrs, &ctx->wcur, &ctx->wlist, &ctx->gp_cb, &ctx->gp_cnt, &ctx->gp_cur, &ctx->gp_refs, &ctx->gp_ccnt,
+                      &ctx->gp_cbase, &ctx->gp_plist, &ctx->gp_pidx, &ctx->gp_pcost, &ctx->gp_tmp};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
@@ -4430,6 +4880,82 @@ static int *list_ptr(apd_ctx *ctx, int which) {
     return base + off;
 }
 
+// ensure() for optional buffers: a failed allocation leaves no error behind (the caller falls back)
+static bool try_ensure(apd_ctx *ctx, DevBuf &b, size_t bytes) {
+    if (ensure(ctx, b, bytes) == APD_OK) return true;
+    (void)hipGetLastError();
+    ctx->err.clear();
+    return false;
+}
+
+// exclusive prefix sum of n ints (rocPRIM) on the ctx stream
+static int exclusive_scan_int(apd_ctx *ctx, const int *in, int *out, size_t n) {
+    size_t tb = 0;
+    HIP_OK(ctx, rocprim::exclusive_scan(nullptr, tb, in, out, 0, n, rocprim::plus<int>(), ctx->stream));
+    if (!try_ensure(ctx, ctx->gp_tmp, tb)) return APD_ENOMEM;
+    HIP_OK(ctx, rocprim::exclusive_scan(ctx->gp_tmp.p, tb, in, out, 0, n, rocprim::plus<int>(), ctx->stream));
+    return APD_OK;
+}
+
+// The image-wide (window anchor, candidate anchor) pair table of the prepared problem (see
+// k_gp_dedup); ctx->gp_on stays false (k_weak_cand_vm's per-group pairs) when a buffer does not fit.
+static int build_global_pairs(apd_ctx *ctx, int nw) {
+    Args &a = ctx->args;
+    hipStream_t s = ctx->stream;
+    const size_t HW = (size_t)a.HW, wc = (size_t)std::max(ctx->weak_count, 1);
+    ctx->gp_on = false;
+    ctx->gp_np = 0;
+    if (!try_ensure(ctx, ctx->gp_cnt, (HW + 1) * sizeof(int)) || !try_ensure(ctx, ctx->gp_cur, (HW + 1) * sizeof(int)) ||
+        !try_ensure(ctx, ctx->gp_refs, (size_t)nw * 8 * sizeof(uint32_t)) ||
+        !try_ensure(ctx, ctx->gp_pidx, wc * 64 * sizeof(uint32_t)) || !try_ensure(ctx, ctx->gp_cb, wc))
+        return APD_OK;
+    int *cnt = (int *)ctx->gp_cnt.p, *cur = (int *)ctx->gp_cur.p;
+    HIP_OK(ctx, hipMemsetAsync(cnt, 0, (HW + 1) * sizeof(int), s));
+    hipLaunchKernelGGL(k_gp_count, dim3(blocks_for((size_t)nw, BLOCK)), dim3(BLOCK), 0, s, a, (const int *)ctx->wlist.p, nw, cnt,
+                       (uint8_t *)ctx->gp_cb.p);
+    int st;
+    if ((st = exclusive_scan_int(ctx, cnt, cur, HW + 1))) return st == APD_ENOMEM ? APD_OK : st;
+    int nrefs = 0;
+    HIP_OK(ctx, hipMemcpyAsync(&nrefs, cur + HW, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_OK(ctx, hipMemcpyAsync(cnt, cur, HW * sizeof(int), hipMemcpyDeviceToDevice, s));  // fill cursors
+    hipLaunchKernelGGL(k_gp_fill, dim3(blocks_for((size_t)nw, BLOCK)), dim3(BLOCK), 0, s, a, (const int *)ctx->wlist.p, nw, cnt,
+                       (uint32_t *)ctx->gp_refs.p);
+    HIP_OK(ctx, hipStreamSynchronize(s));
+    if (nrefs <= 0) { ctx->gp_on = true; return check_launch(ctx, "pair table"); }
+    // window anchors with references -> one dedup workgroup each
+    if (!try_ensure(ctx, ctx->gp_ccnt, (HW + 1) * sizeof(int)) || !try_ensure(ctx, ctx->gp_cbase, 2 * (HW + 1) * sizeof(int)))
+        return APD_OK;
+    int *tpos = (int *)ctx->gp_ccnt.p, *tasks = cnt;  // (the fill cursors are done with)
+    hipLaunchKernelGGL(k_gp_flags, dim3(blocks_for(HW + 1, BLOCK)), dim3(BLOCK), 0, s, (const int *)cur, (int)HW, cnt);
+    if ((st = exclusive_scan_int(ctx, cnt, tpos, HW + 1))) return st == APD_ENOMEM ? APD_OK : st;
+    hipLaunchKernelGGL(k_gp_tasks, dim3(blocks_for(HW, BLOCK)), dim3(BLOCK), 0, s, (const int *)cur, (const int *)tpos, (int)HW, tasks);
+    int ntask = 0;
+    HIP_OK(ctx, hipMemcpyAsync(&ntask, tpos + HW, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_OK(ctx, hipStreamSynchronize(s));
+    int *acnt = (int *)ctx->gp_cbase.p, *abase = acnt + (HW + 1);
+    HIP_OK(ctx, hipMemsetAsync(acnt + ntask, 0, sizeof(int), s));
+    if (ntask > 0)
+        hipLaunchKernelGGL((k_gp_dedup<0>), dim3(ntask), dim3(GP_CHUNK), 0, s, a, (const int *)tasks, (const int *)cur,
+                           (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, acnt, (const int *)nullptr,
+                           (int2 *)nullptr, (uint32_t *)nullptr);
+    if ((st = exclusive_scan_int(ctx, acnt, abase, (size_t)ntask + 1))) return st == APD_ENOMEM ? APD_OK : st;
+    int npairs = 0;
+    HIP_OK(ctx, hipMemcpyAsync(&npairs, abase + ntask, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_OK(ctx, hipStreamSynchronize(s));
+    if (npairs > 0 && (!try_ensure(ctx, ctx->gp_plist, (size_t)npairs * sizeof(int2)) ||
+                       !try_ensure(ctx, ctx->gp_pcost, (size_t)npairs * ((a.N + 3) & ~3) * sizeof(float))))
+        return APD_OK;
+    if (npairs > 0)
+        hipLaunchKernelGGL((k_gp_dedup<1>), dim3(ntask), dim3(GP_CHUNK), 0, s, a, (const int *)tasks, (const int *)cur,
+                           (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, (int *)nullptr, (const int *)abase,
+                           (int2 *)ctx->gp_plist.p,
+                           (uint32_t *)ctx->gp_pidx.p);
+    if ((st = check_launch(ctx, "pair table"))) return st;
+    ctx->gp_np = npairs;
+    ctx->gp_on = true;
+    return APD_OK;
+}
+
 int32_t apd_stage_prepare(apd_ctx *ctx) {
     if (!ctx || !ctx->loaded) return APD_ESTATE;
     (void)hipSetDevice(ctx->device);
@@ -4437,6 +4963,7 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
     hipStream_t s = ctx->stream;
     const unsigned gpx = blocks_for((size_t)a.HW, BLOCK);
     int st;
+    ctx->gp_on = false;
     (void)hipEventRecord(ctx->ev[0], s);
     if (a.use_apd) {
         // anchors_map from the input WEAK mask (APD.cpp:627-640)
@@ -4476,6 +5003,9 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
             if ((st = ensure(ctx, ctx->wdone, wc))) return st;
             if ((st = ensure(ctx, ctx->wlist, (size_t)(ctx->cnt[2] + ctx->cnt[3]) * sizeof(int)))) return st;
             if ((st = build_tile_list(ctx, 1, 2, (int *)ctx->wlist.p, tot + 5))) return st;
+            if (ctx->cand_global && !a.sa_any && (size_t)a.HW < (1u << 25) &&
+                (st = build_global_pairs(ctx, ctx->cnt[2] + ctx->cnt[3])))
+                return st;
         }
     }
     (void)hipEventRecord(ctx->ev[2], s);
@@ -4566,9 +5096,18 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             e0 = prof_begin(ctx);
             Args ac = a;
             ac.evals = evals;  // (only instrumented builds write it)
-            LAUNCH_TEX(k_weak_cand_vm, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK),
-                       (ctx->args.tex_f16 ? pk_lds_bytes<true>() : pk_lds_bytes<false>()), s, ac,
-                       (const int *)ctx->wlist.p, nw, (float *)ctx->wcand.p, (uint8_t *)ctx->wdone.p, wc);
+            if (ctx->gp_on) {
+                if (ctx->gp_np > 0)
+                    LAUNCH_TEX(k_gp_cost, dim3(blocks_for((size_t)ctx->gp_np, BLOCK)), dim3(BLOCK), 0, s, ac,
+                               (const int2 *)ctx->gp_plist.p, ctx->gp_np, (float *)ctx->gp_pcost.p);
+                LAUNCH_TEX(k_weak_cand_g, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), gp_cand_lds_bytes(a.N), s, ac, (const int *)ctx->wlist.p, nw,
+                           (const uint8_t *)ctx->gp_cb.p, (const uint32_t *)ctx->gp_pidx.p, (const float *)ctx->gp_pcost.p, (float *)ctx->wcand.p,
+                           (uint8_t *)ctx->wdone.p, wc);
+            } else {
+                LAUNCH_TEX(k_weak_cand_vm, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK),
+                           (ctx->args.tex_f16 ? pk_lds_bytes<true>() : pk_lds_bytes<false>()), s, ac,
+                           (const int *)ctx->wlist.p, nw, (float *)ctx->wcand.p, (uint8_t *)ctx->wdone.p, wc);
+            }
             prof_end(ctx, e0, APD_PROF_WEAK_CAND, nw);
             cand = (const float *)ctx->wcand.p;
         }

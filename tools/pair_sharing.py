@@ -60,3 +60,13 @@ for y0 in (H // 4, H // 2):
     k = pairs_of(sel)
     print(f"band rows {y0}..{y0 + band_rows} ({sel.size} px): evaluations {k.size}, distinct {np.unique(k).size}, "
           f"sharing {k.size / max(np.unique(k).size, 1):.2f}x", flush=True)
+if os.environ.get("GLOBAL") == "1":  # the whole image (sorts ~1.4 G keys: minutes)
+    k = np.unique(pairs_of(np.arange(nw)))
+    qk = k // (W * H)
+    _, cnt = np.unique(qk, return_counts=True)
+    tot = int(win.sum(1) @ np.ones(1) * 0) if False else int((win[:, :, None] & cand[:, None, :]).sum())
+    print(f"whole image: evaluations {tot}, distinct {k.size}, sharing {tot / max(k.size, 1):.2f}x; "
+          f"{cnt.size} distinct window anchors, candidates per window anchor mean {cnt.mean():.1f} "
+          f"p50 {np.percentile(cnt, 50):.0f} p99 {np.percentile(cnt, 99):.0f} max {cnt.max()}", flush=True)
+    ca = np.unique(q[:, 1:][cand])
+    print(f"distinct candidate anchors {ca.size}", flush=True)
