@@ -855,6 +855,83 @@ static void k_sweep_strong(octx *o, int px, int py, int iter) {
     for (int i = 0; i < N; ++i) WR(o, vw, (size_t)i * o->HW + c) = vw[i];
 }
 
+#ifdef ORACLE_WEAK_STATS
+/* Measurement build only (tools/weak_bound_stats.py): how many Weak-refinement evaluations lower
+ * bounds could reject before the anchor windows. NCC-New = COST_MAX when the centre or its anchor
+ * projects out of the source, else (float)(0.25 * cc + 0.75 * acc) with acc >= 0, so
+ * lb = (float)(0.25 * (double)cc) (or COST_MAX) never exceeds it; fmaf(gf, geom, .) and the weighted
+ * fmaf chain are monotone. */
+static float o_ncc_new_centre_lb(const octx *o, int px, int py, int s, f4 pl) {
+    const int W = o->W, H = o->H;
+    const int center = px + py * W;
+    float Hm[9];
+    homography(o, s, pl, Hm);
+    float ptx, pty;
+    project(Hm, (float)px, (float)py, &ptx, &pty);
+    if (ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f) return COST_MAX;
+    int ax = anchor_x(o, center, 0), ay = anchor_y(o, center, 0);
+    if (ax == -1 || ay == -1) return 0.0f;
+    float asx, asy;
+    project(Hm, (float)ax, (float)ay, &asx, &asy);
+    if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) return COST_MAX;
+    float sr = 0.0f, srr = 0.0f, ss = 0.0f, sss = 0.0f, srs = 0.0f, wsum = 0.0f;
+    for (int i = -5; i <= 5; i += 2)
+        for (int j = -5; j <= 5; j += 2) {
+            float r = tex_ref(o, ax + i, ay + j);
+            float sx, sy;
+            project(Hm, (float)(ax + i), (float)(ay + j), &sx, &sy);
+            float v = tex_bilinear(o, s, sx, sy);
+            sr += r; srr = fmaf(r, r, srr); ss += v; sss = fmaf(v, v, sss); srs = fmaf(r, v, srs); wsum += 1.0f;
+        }
+    return (float)(0.25 * (double)ncc_finalize(sr, srr, ss, sss, srs, wsum));
+}
+/* [0] candidates (fit + refinement), [1] weighted-view evaluations, [2] with the per-view prefix exit,
+ * [3] rejected by the geometric bound, [4] by the centre + geometric bound, [5] anchor-window
+ * evaluations left with the centre + geometric bound then the prefix exit, [6] candidates accepted */
+static long long g_wstats[8];
+long long oracle_weak_stats(int i) { return (i >= 0 && i < 8) ? g_wstats[i] : -1; }
+void oracle_weak_stats_reset(void) { memset(g_wstats, 0, sizeof(g_wstats)); }
+static void weak_stats(const octx *o, int px, int py, f4 t, const uint8_t *vw, float wn, float thr) {
+    const int N = o->N, geom = o->P.geom_consistency;
+    const float gf = o->P.geom_factor;
+    long long st[8] = {0};
+    float full[32], lbg[32], lbc[32];
+    st[0] = 1;
+    for (int i = 0; i < N; ++i) {
+        if (!vw[i]) continue;
+        const float g = geom ? o_geom_cost(o, px, py, i + 1, t) : 0.0f;
+        const float nn = o_ncc_new(o, px, py, i + 1, t);
+        full[i] = geom ? fmaf(gf, g, nn) : nn;
+        lbg[i] = geom ? fmaf(gf, g, 0.0f) : 0.0f;
+        const float lc = o_ncc_new_centre_lb(o, px, py, i + 1, t);
+        lbc[i] = geom ? fmaf(gf, g, lc) : lc;
+        st[1]++;
+    }
+    float P = 0.0f, Pg = 0.0f, Pc = 0.0f;
+    int stop = 0;
+    for (int i = 0; i < N; ++i) {
+        if (!vw[i]) continue;
+        if (!stop) { st[2]++; P = fmaf((float)vw[i], full[i], P); if (P / wn >= thr) stop = 1; }
+        Pg = fmaf((float)vw[i], lbg[i], Pg);
+        Pc = fmaf((float)vw[i], lbc[i], Pc);
+    }
+    if (Pg / wn >= thr) st[3] = 1;
+    if (Pc / wn >= thr) st[4] = 1;
+    else {  /* survivors: anchor windows with the prefix exit */
+        float Q = 0.0f;
+        for (int i = 0; i < N; ++i) {
+            if (!vw[i]) continue;
+            st[5]++;
+            Q = fmaf((float)vw[i], full[i], Q);
+            if (Q / wn >= thr) break;
+        }
+    }
+    if (!stop) st[6] = 1;
+#pragma omp critical
+    for (int i = 0; i < 8; ++i) g_wstats[i] += st[i];
+}
+#endif
+
 /* CheckerboardPropagationWeak + PlaneHypothesisRefinementWeak, APD.cu:1442-1615, 1008-1096 */
 static void k_sweep_weak(octx *o, int px, int py, int iter) {
     const int W = o->W, N = o->N;
@@ -923,6 +1000,9 @@ static void k_sweep_weak(octx *o, int px, int py, int iter) {
     /* PlaneHypothesisRefinementWeak, APD.cu:1008-1096 */
     f4 fit = RD(o, fit, c);
     if (!(fit.x == 0 && fit.y == 0 && fit.z == 0)) {
+#ifdef ORACLE_WEAK_STATS
+        weak_stats(o, px, py, fit, vw, wn, cost_now);
+#endif
         {
             float tc = 0.0f;
             for (int i = 0; i < N; ++i) {
@@ -939,9 +1019,15 @@ static void k_sweep_weak(octx *o, int px, int py, int iter) {
         float dc[5];
         f4 nc[5];
         refine_candidates(o, px, py, &g, pnow, depth_now, dc, nc);
+#ifdef ORACLE_WEAK_STATS
+        const float thr5 = cost_now;  /* the GPU's exit threshold: the cost after the fit plane */
+#endif
         for (int k = 0; k < 5; ++k) {
             f4 t = nc[k];
             t.w = dist2origin(cam, px, py, dc[k], t);
+#ifdef ORACLE_WEAK_STATS
+            weak_stats(o, px, py, t, vw, wn, thr5);
+#endif
             float tc = 0.0f;
             for (int i = 0; i < N; ++i) {
                 if (vw[i] > 0) {
