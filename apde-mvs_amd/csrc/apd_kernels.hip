@@ -3089,6 +3089,36 @@ __global__ __launch_bounds__(BLOCK) void k_gp_cost(Args a, const int2 *__restric
     }
 }
 
+// the focal combination (APD.cu:576-593, Softmax 431-446) of one (pixel, candidate, view): centre
+// cost cc (< 0: dead -> COST_MAX) and the 8 windows' pair costs sc[k] (< 0: window absent), in anchor
+// order -- ncc_new_vm's statements
+__device__ __forceinline__ float gp_combine(float cc, const float (&sc)[8]) {
+    if (cc < 0.0f) return APD_COST_MAX;
+    const float center_cost = cc;
+    uint32_t pm = 0;
+    float strong_weight = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (sc[k] >= 0.0f) { pm |= 1u << k; strong_weight += 1.0f; }
+    if (strong_weight <= 1e-6f) return center_cost;
+    float mx = -1e10f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) if (((pm >> k) & 1u) && sc[k] > mx) mx = sc[k];
+    float e[8];
+    float sum = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        e[k] = 0.0f;
+        if ((pm >> k) & 1u) { e[k] = d_expf(sc[k] - mx); sum += e[k]; }
+    }
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if ((pm >> k) & 1u) { const float w = e[k] / sum; acc = fmaf(w, sc[k], acc); }
+    acc = (acc > APD_COST_MAX) ? APD_COST_MAX : acc;
+    return (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
+}
+
 // the anchor candidates' costs from the pair costs: centre windows + focal combination (as
 // k_weak_cand_vm's phase D, without SA masks); lane = pixel, wave = candidate h.
 //   A  per view (the waves take the views together: one source image, the CU's L1): the centre
@@ -3194,11 +3224,19 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
                 if (wsum != 0.0f) center_cost = ncc_finalize(csr[p1], csrr[p1], ss, sss, srs, wsum);
             }
         }
+#ifdef GP_FUSED
         ccost[(v * 8 + h) * VM_P + p1] = dead ? -1.0f : center_cost;
+#else
+        // (k_weak_cand_comb reads it back and writes the candidate's cost in its place)
+        if (want) out[((size_t)v * 8 + h) * (size_t)wc + wi1] = dead ? -1.0f : center_cost;
+#endif
 #ifdef GP_VIEW_SYNC  // (measured: keeping the waves on one view costs more than the shared L1 gains)
         __syncthreads();
 #endif
     }
+#ifndef GP_FUSED
+    return;
+#endif
     if (!want) return;  // (each lane reads back only its own entries: no barrier needed)
     // ---- B: focal combination (APD.cu:576-593, Softmax 431-446) per view
     const int Np = (N + 3) & ~3;
@@ -3227,46 +3265,64 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
         for (int dv = 0; dv < 4; ++dv) {
             const int v = v0 + dv;
             if (v >= N) break;
-            const float cc = ccost[(v * 8 + h) * VM_P + p1];
-            float cost;
-            if (cc < 0.0f) {
-                cost = APD_COST_MAX;
-            } else {
-                const float center_cost = cc;
-                float sc[8];
+            float sc[8];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) sc[k] = dv == 0 ? q[k].x : dv == 1 ? q[k].y : dv == 2 ? q[k].z : q[k].w;
-                uint32_t pm = 0;
-                float strong_weight = 0.0f;
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    if (sc[k] >= 0.0f) { pm |= 1u << k; strong_weight += 1.0f; }
-                if (strong_weight <= 1e-6f) {
-                    cost = center_cost;
-                } else {
-                    float mx = -1e10f;
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) if (((pm >> k) & 1u) && sc[k] > mx) mx = sc[k];
-                    float e[8];
-                    float sum = 0.0f;
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        e[k] = 0.0f;
-                        if ((pm >> k) & 1u) { e[k] = d_expf(sc[k] - mx); sum += e[k]; }
-                    }
-                    float acc = 0.0f;
-#pragma unroll
-                    for (int k = 0; k < 8; ++k)
-                        if ((pm >> k) & 1u) { const float w = e[k] / sum; acc = fmaf(w, sc[k], acc); }
-                    acc = (acc > APD_COST_MAX) ? APD_COST_MAX : acc;
-                    cost = (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
-                }
-            }
+            for (int k = 0; k < 8; ++k) sc[k] = dv == 0 ? q[k].x : dv == 1 ? q[k].y : dv == 2 ? q[k].z : q[k].w;
+            const float cost = gp_combine(ccost[(v * 8 + h) * VM_P + p1], sc);
             out[((size_t)v * 8 + h) * (size_t)wc + wi1] = cost;
         }
     }
 }
-static inline size_t gp_cand_lds_bytes(int N) { return (size_t)N * 8 * VM_P * sizeof(float); }
+static inline size_t gp_cand_lds_bytes(int N) {
+#ifdef GP_FUSED
+    return (size_t)N * 8 * VM_P * sizeof(float);
+#else
+    (void)N;
+    return 0;
+#endif
+}
+// Phase B of k_weak_cand_g as its own kernel (the default): a thread per (WEAK pixel, candidate),
+// few registers and many waves in flight for the pair-cost gathers (a timing study of the fused
+// kernel put ~40 ms per C3 iteration on those loads); `out` holds the centre cost (< 0: dead) and
+// receives the candidate's cost in its place. Block = 4 candidates x 64 pixels of one group.
+__global__ __launch_bounds__(BLOCK) void k_weak_cand_comb(Args a, const int *__restrict__ list, int count,
+                                                          const uint8_t *__restrict__ cbw, const uint32_t *__restrict__ pidx,
+                                                          const float *__restrict__ pcost, float *__restrict__ out, int wc) {
+    const int b = xcd_remap(blockIdx.x, gridDim.x);
+    const int h = ((b & 1) << 2) + (threadIdx.x >> 6);
+    const int i = (b >> 1) * VM_P + (threadIdx.x & (WAVE - 1));
+    if (i >= count) return;
+    const int wi = a.amap[list[i]];
+    if (!((cbw[wi] >> h) & 1u)) return;
+    const int N = a.N, Np = (N + 3) & ~3;
+    const APD_G short2 *anc = a.anchors + (size_t)wi * 9;
+    const uint32_t *pp = pidx + (size_t)wi * 64 + h;  // [window k][candidate h]
+    const float4 *pc4[8];
+    uint32_t pm0 = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const short2 ak = anc[k + 1];
+        const uint32_t id = pp[k * 8];
+        const bool ok = !(ak.x == -1 || ak.y == -1) && id != GP_NONE;
+        pc4[k] = reinterpret_cast<const float4 *>(pcost + (size_t)(ok ? id : 0u) * Np);
+        pm0 |= (uint32_t)ok << k;
+    }
+    for (int v0 = 0; v0 < N; v0 += 4) {
+        float4 q[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[k] = ((pm0 >> k) & 1u) ? pc4[k][v0 >> 2] : make_float4(-1.0f, -1.0f, -1.0f, -1.0f);
+#pragma unroll
+        for (int dv = 0; dv < 4; ++dv) {
+            const int v = v0 + dv;
+            if (v >= N) break;
+            float sc[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sc[k] = dv == 0 ? q[k].x : dv == 1 ? q[k].y : dv == 2 ? q[k].z : q[k].w;
+            float *o = out + ((size_t)v * 8 + h) * (size_t)wc + wi;
+            *o = gp_combine(*o, sc);
+        }
+    }
+}
 
 // ---------------------------------------------------------------------------------------------
 // CheckerboardPropagationWeak + PlaneHypothesisRefinementWeak (APD.cu:1442-1615, 1008-1096)
@@ -5103,6 +5159,11 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
                 LAUNCH_TEX(k_weak_cand_g, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), gp_cand_lds_bytes(a.N), s, ac, (const int *)ctx->wlist.p, nw,
                            (const uint8_t *)ctx->gp_cb.p, (const uint32_t *)ctx->gp_pidx.p, (const float *)ctx->gp_pcost.p, (float *)ctx->wcand.p,
                            (uint8_t *)ctx->wdone.p, wc);
+#ifndef GP_FUSED
+                hipLaunchKernelGGL(k_weak_cand_comb, dim3(2 * blocks_for((size_t)nw, VM_P)), dim3(BLOCK), 0, s, ac,
+                                   (const int *)ctx->wlist.p, nw, (const uint8_t *)ctx->gp_cb.p, (const uint32_t *)ctx->gp_pidx.p,
+                                   (const float *)ctx->gp_pcost.p, (float *)ctx->wcand.p, wc);
+#endif
             } else {
                 LAUNCH_TEX(k_weak_cand_vm, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK),
                            (ctx->args.tex_f16 ? pk_lds_bytes<true>() : pk_lds_bytes<false>()), s, ac,

@@ -1,5 +1,5 @@
 """Per-kernel HIP-event times of the bench's headline pass (or AB_W x AB_H, AB_N) for several library
-builds, one process: python tools/ab_kernels.py libA.so libB.so ..."""
+builds, one process: python tools/ab_kernels.py libA.so libB.so[:ENV=VAL,...] ..."""
 import os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "apde-mvs_amd"), os.path.join(REPO, "tests")]
@@ -8,7 +8,17 @@ import apd_abi as A
 
 W, H, N = int(os.environ.get("AB_W", 6048)), int(os.environ.get("AB_H", 4032)), int(os.environ.get("AB_N", 10))
 sc = bench.make_scene(W, H, N, 1, os.environ.get("AB_TEXTURE", "smooth"))
-engs = [(os.path.basename(p), A.Engine(0, A.load_library(p))) for p in sys.argv[1:]]
+def make_engine(spec):  # lib.so[:ENV=VAL,...] (env read by apd_create)
+    path, _, opt = spec.partition(":")
+    envs = dict(kv.split("=", 1) for kv in opt.split(",")) if opt else {}
+    os.environ.update(envs)
+    e = A.Engine(0, A.load_library(path))
+    for k in envs:
+        os.environ.pop(k, None)
+    return os.path.basename(path) + (":" + opt if opt else ""), e
+
+
+engs = [make_engine(p) for p in sys.argv[1:]]
 ids = [0] + [j for j, _ in sc.pairs[0]][:N]
 priors = bench.first_init_priors(engs[0][1], sc, ids, N)
 arr = bench.final_round_problem(sc, priors, 0, N)
