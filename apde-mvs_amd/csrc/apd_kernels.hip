@@ -468,6 +468,30 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
             odi++;
             for (int ri = 0; ri < rt; ++ri) {
                 const int di = odi * 4 + ri;
+                if (a.anc_shift == 1) {
+                    // rotate_time >= 3 (main.cpp's rounds 2 and 3): shift = max((int)(tan(angle / 2) * 20), 1)
+                    // is 1, so every draw's offset is x % 1 = 0 and the 4 attempts of a radius sample the
+                    // same point -- the same lookup and verdict. The draws only advance the stream: by 4
+                    // (attempt 1 succeeds) or 16 (all fail), exactly as the general search below.
+                    float ddx = dx * 20 + (float)0, ddy = dy * 20 + (float)0;
+                    normalize2(ddx, ddy);
+                    for (int radius = 2; radius <= APD_MAX_SEARCH_RADIUS; radius = min(radius * 2, radius + 25)) {
+                        float tx = (float)px + dx * (float)radius, ty = (float)py + dy * (float)radius;
+                        if (tx < 0 || ty < 0 || tx >= (float)W || ty >= (float)H) break;
+                        const int ax = (int16_t)(int)((float)px + ddx * (float)radius);
+                        const int ay = (int16_t)(int)((float)py + ddy * (float)radius);
+                        bool ok = !(ax < margin || ay < margin || ax >= W - margin || ay >= H - margin);
+                        const short2 nn = ok ? a.nearest[ax + ay * W] : make_short2(-1, -1);
+                        ok = ok && !(nn.x == -1 || nn.y == -1);
+                        if (ok) {
+                            float tdx = (float)(nn.x - px), tdy = (float)(nn.y - py);
+                            normalize2(tdx, tdy);
+                            ok = tdx * dx + tdy * dy > a.anc_thr;
+                        }
+                        g.n += ok ? 4u : 16u;
+                        if (ok) { sp[di] = nn; dvalid |= 1u << di; nsp++; break; }
+                    }
+                } else
                 for (int radius = 2; radius <= APD_MAX_SEARCH_RADIUS; radius = min(radius * 2, radius + 25)) {
                     float tx = (float)px + dx * (float)radius, ty = (float)py + dy * (float)radius;
                     if (tx < 0 || ty < 0 || tx >= (float)W || ty >= (float)H) break;
@@ -499,6 +523,12 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
                         float ca = tdx * dx + tdy * dy;
                         if (ca > a.anc_thr) { sp[di] = nn[t]; dvalid |= 1u << di; nsp++; used = t + 1; }
                     }
+#ifdef APD_ANCHOR_STATS  // measurement build: steps, the attempt that succeeded, wave-level steps
+                    if (a.evals) {
+                        atomicAdd(a.evals + 20 + (used == 4 && !((dvalid >> di) & 1u) ? 4 : used - 1), 1ull);
+                        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(true))) atomicAdd(a.evals + 25, 1ull);
+                    }
+#endif
                     g.n = n0 + 4u * (uint32_t)used;
                     if ((dvalid >> di) & 1u) break;
                 }
@@ -1990,6 +2020,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     }
     __syncthreads();
 
+    PHASE_STAMP(22);  // (instrumented builds: P2a apart from P1b + P1c)
     // ---- P1b: current-plane tasks, lane = pixel, for the views with weight > 0
     const int cur_row = direct ? 0 : 8 * N;
     for (int v = wave; v < N; v += WV_WAVES) {
@@ -5032,7 +5063,11 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         } else {
             hipLaunchKernelGGL(k_find_nearest, dim3(gpx), dim3(BLOCK), 0, s, a, ctx->n_near);
         }
-        hipLaunchKernelGGL(k_gen_anchors, dim3(gpx), dim3(BLOCK), 0, s, a);
+        {
+            Args ag = a;  // (profiling counters: instrumented builds of k_gen_anchors only)
+            ag.evals = (ctx->prof && ctx->evals.p) ? (APD_G unsigned long long *)ctx->evals.p : nullptr;
+            hipLaunchKernelGGL(k_gen_anchors, dim3(gpx), dim3(BLOCK), 0, s, ag);
+        }
         hipLaunchKernelGGL(k_neighbour_update, dim3(gpx), dim3(BLOCK), 0, s, a);
         if ((st = check_launch(ctx, "anchors"))) return st;
     }

@@ -25,12 +25,13 @@ names = {8: "cand setup (hash, windows)", 9: "cand pair windows", 10: "cand cent
          0: "sweep P0 anchors/windows", 1: "sweep P1 current plane", 2: "sweep P2 view selection+geom",
          3: "sweep P3 fit plane", 4: "sweep P4 candidates", 5: "sweep P5 refinement", 6: "sweep P6 acceptance"}
 for lo, hi, title in ((8, 12, "k_weak_cand_vm"), (0, 7, "k_sweep_weak_vm")):
-    tot = sum(c[8 + i] for i in range(lo, hi)) or 1
+    tot = (sum(c[8 + i] for i in range(lo, hi)) + (c[30] if lo == 0 else 0)) or 1
     print(title)
     for i in range(lo, hi):
         print(f"  {names[i]:32s} {100.0 * c[8 + i] / tot:6.1f} %")
     if lo == 0:
-        print(f"  (of P2: geometric terms, thread 0's own time {100.0 * c[15] / max(c[10], 1):5.1f} %)")
+        print(f"  {'sweep P2a (before P1b)':32s} {100.0 * c[30] / tot:6.1f} %   (P2 above = P1b + P1c when stamped)")
+        print(f"  (of P2a: geometric terms, thread 0's own time {100.0 * c[15] / max(c[30] or c[10], 1):5.1f} %)")
 t = eng.timing()
 print(f"iteration ms {list(t.iter_ms)[:t.iterations]}")
 for slot, what in ((20, "sweep P5 refinement tasks"), (22, "sweep P3 fit-plane tasks"), (24, "sweep P1b current-plane tasks"),
