@@ -615,24 +615,27 @@ __global__ __launch_bounds__(BLOCK) void k_neighbour_update(Args a) {
     if (a.weak[c] == APD_WEAK && a.reliable[c] != 1) a.weak[c] = APD_UNKNOWN;
 }
 
-// RANSACToGetFitPlane (APD.cu:2486-2598)
+// RANSACToGetFitPlane (APD.cu:2486-2598). The anchor points live in LDS (one float4 per point and
+// thread: X, Y, Z and the packed pixel position), so the draws' dynamically indexed reads are three
+// 16-byte LDS loads instead of select chains over a register array.
 __global__ __launch_bounds__(BLOCK) void k_ransac_fit(Args a, int iter) {
+    __shared__ float4 pts[8][BLOCK];
     const int c = blockIdx.x * BLOCK + threadIdx.x;
+    const int tid = threadIdx.x;
     if (c >= a.HW) return;
     if (a.weak[c] != APD_WEAK) { a.fit[c] = a.plane[c]; return; }
     const int W = a.W;
     const int py = c / W, px = c - py * W;
     const APD_C Cam &cam = a.cams[0];
     const APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
-    int sx[8], sy[8], cnt = 0;
-    float s3[8][3], X[3];
+    int cnt = 0;
+    float X[3];
     for (int i = 1; i < 9; ++i) {
         short2 t = anc[i];
         if (t.x == -1 || t.y == -1) continue;
-        sx[cnt] = t.x; sy[cnt] = t.y;
         float d = depth_from_plane(cam, a.plane[t.x + t.y * W], t.x, t.y);
         get3d(cam, (float)t.x, (float)t.y, d, X);
-        s3[cnt][0] = X[0]; s3[cnt][1] = X[1]; s3[cnt][2] = X[2];
+        pts[cnt][tid] = make_float4(X[0], X[1], X[2], __int_as_float((int)(uint16_t)t.x | ((int)t.y << 16)));
         cnt++;
     }
     if (cnt < 3) { a.fit[c] = a.plane[c]; return; }
@@ -646,18 +649,20 @@ __global__ __launch_bounds__(BLOCK) void k_ransac_fit(Args a, int iter) {
         int ib = (int)fm.mod(g.u32());
         int ic = (int)fm.mod(g.u32());
         if (ia == ib || ib == ic || ia == ic) continue;
-        if (!point_in_triangle(sx[ia], sy[ia], sx[ib], sy[ib], sx[ic], sy[ic], px, py)) continue;
-        const float *A = s3[ia], *B = s3[ib], *C = s3[ic];
-        float ACx = A[0] - C[0], ACy = A[1] - C[1], ACz = A[2] - C[2];
-        float BCx = B[0] - C[0], BCy = B[1] - C[1], BCz = B[2] - C[2];
+        const float4 A = pts[ia][tid], B = pts[ib][tid], C = pts[ic][tid];
+        const int pa = __float_as_int(A.w), pb = __float_as_int(B.w), pc = __float_as_int(C.w);
+        if (!point_in_triangle(pa & 0xFFFF, pa >> 16, pb & 0xFFFF, pb >> 16, pc & 0xFFFF, pc >> 16, px, py)) continue;
+        float ACx = A.x - C.x, ACy = A.y - C.y, ACz = A.z - C.z;
+        float BCx = B.x - C.x, BCy = B.y - C.y, BCz = B.z - C.z;
         float4 cr = make_float4(ACy * BCz - BCy * ACz, -(ACx * BCz - BCx * ACz), ACx * BCy - BCx * ACy, 0.0f);
         if ((cr.x == 0 && cr.y == 0 && cr.z == 0) || isnan(cr.x) || isnan(cr.y) || isnan(cr.z)) continue;
         normalize3(cr);
-        cr.w = -(cr.x * A[0] + cr.y * A[1] + cr.z * A[2]);
+        cr.w = -(cr.x * A.x + cr.y * A.y + cr.z * A.z);
         float tc = 0.0f;
         for (int k = 0; k < cnt; ++k) {
             if (k == ia || k == ib || k == ic) continue;
-            tc += fabsf(cr.x * s3[k][0] + cr.y * s3[k][1] + cr.z * s3[k][2] + cr.w);
+            const float4 P = pts[k][tid];
+            tc += fabsf(cr.x * P.x + cr.y * P.y + cr.z * P.z + cr.w);
         }
         if (tc < min_cost) { min_cost = tc; best = cr; has = true; }
         if (min_cost == 0) break;
