@@ -7,7 +7,7 @@ geometric consistency, impetus, rotate_time 4, ransac_threshold 0.00625). Its pr
 normals, pixel states, confidence of every view) come from FIRST_INIT runs of the scan's views at the
 same resolution. A "step" is one iteration of the loop body APD.cu:2699-2708 over the whole
 reference view: Strong sweep black + red, RANSACToGetFitPlane, and the Weak sweep black + red
-(anchor candidates through the image-wide pair table: k_gp_cost + k_weak_cand_g, then
+(anchor candidates through the image-wide pair table: k_gp_cost + k_weak_cand_g + k_weak_cand_comb, then
 k_sweep_weak_vm). Steps are iterations 0, 1, 2 of FRESH runs (the
 median over a fresh run's iterations): before every block of (up to) 3 steps the problem is
 re-uploaded and re-initialised (apd_set_problem + apd_stage_prepare, outside the timed region), so
@@ -22,7 +22,7 @@ timing barriers and a max-reduction of the elapsed time (no data-path collective
 
 Besides the headline the JSON line carries:
   roofline      the dominant kernels of the step, the Weak sweep (the anchor candidates -- k_gp_cost +
-                k_weak_cand_g, or k_weak_cand_vm with SA masks -- + 2 x k_sweep_weak_vm per iteration,
+                k_weak_cand_g + k_weak_cand_comb, or k_weak_cand_vm with SA masks -- + 2 x k_sweep_weak_vm,
                 95 % of it at C3): algorithmic FP32 flops = NCC-New evaluations x 4038 +
                 geometric terms x 80, both counted on the device for the evaluations
                 CheckerboardPropagationWeak uses (apd_profile_counters), / their summed launch time from
@@ -178,18 +178,18 @@ def weak_roofline(eng, steps, W, N):
     return {
         "bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-        "kernel": "k_sweep_weak_vm (+ k_gp_cost + k_weak_cand_g): CheckerboardPropagationWeak, APD.cu:1442-1615",
+        "kernel": "k_sweep_weak_vm (+ k_gp_cost + k_weak_cand_g + k_weak_cand_comb): CheckerboardPropagationWeak, APD.cu:1442-1615",
         "note": "VALU-FP32 gather/stencil kernels (no matrix work, SURVEY.md §8d); one Weak sweep "
-                "iteration = the anchor-candidate kernels (k_gp_cost + k_weak_cand_g) + 2 k_sweep_weak_vm launches; flops = device-counted "
+                "iteration = the anchor-candidate kernels (k_gp_cost + k_weak_cand_g + k_weak_cand_comb) + 2 k_sweep_weak_vm launches; flops = device-counted "
                 "NCC-New x 4038 + geometric terms x 80, over their summed HIP-event time; traffic = "
                 "HBM bytes per k_sweep_weak_vm launch (PMC, profiles/)",
         "ms_per_iteration": round(ms / max(steps, 1), 3),
         "flop_per_iteration": flop / max(steps, 1),
         "ncc_new_per_iteration": round(cnt[1] / max(steps, 1)),
         "geom_terms_per_iteration": round(cnt[2] / max(steps, 1)),
-        "launch_avg_ms": {"k_gp_cost+k_weak_cand_g": cand["avg_ms"], "k_sweep_weak_vm": sweep["avg_ms"],
+        "launch_avg_ms": {"k_gp_cost+k_weak_cand_g+k_weak_cand_comb": cand["avg_ms"], "k_sweep_weak_vm": sweep["avg_ms"],
                           "k_sweep_strong_vm": strong["avg_ms"], "k_ransac_fit": ransac["avg_ms"]},
-        "launches": {"k_gp_cost+k_weak_cand_g": cand["launches"], "k_sweep_weak_vm": sweep["launches"],
+        "launches": {"k_gp_cost+k_weak_cand_g+k_weak_cand_comb": cand["launches"], "k_sweep_weak_vm": sweep["launches"],
                      "k_sweep_strong_vm": strong["launches"], "k_ransac_fit": ransac["launches"]},
         "pmc_file": pmc.get("_file") if pmc else None,
     }
