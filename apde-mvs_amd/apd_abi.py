@@ -24,7 +24,11 @@ WEAK, STRONG, UNKNOWN = 0, 1, 2
 
 # apd_profile_kernel kinds and apd_profile_counters slots (include/apd_hip.h)
 PROF_STRONG_SWEEP, PROF_RANSAC_FIT, PROF_WEAK_CAND, PROF_WEAK_SWEEP = 0, 1, 2, 3
-PROF_COUNTERS = 4  # [NCC-Old (Strong sweep), NCC-New (Weak sweep), geometric terms (Weak sweep), reserved]
+PROF_DEPTH_TO_WEAK, PROF_GP_COST, PROF_WEAK_CAND_G, PROF_WEAK_CAND_COMB = 4, 5, 6, 7
+# apd_hip.h's counters: [0] NCC-Old (Strong sweep), [1] NCC-New (Weak sweep, algorithmic), [2] geometric
+# terms (Weak sweep), [3] NCC-Old (DepthToWeak), [4] geometric terms (DepthToWeak), [5] pair windows
+# (k_gp_cost), [6] centre windows (k_weak_cand_g), [7] centre / [8] anchor windows (k_sweep_weak_vm)
+PROF_COUNTERS = 9
 
 STATUS = {0: "APD_OK", -1: "APD_EINVAL", -2: "APD_ENOMEM", -3: "APD_EDEVICE", -4: "APD_ETOOMANYVIEWS",
           -5: "APD_ESTATE"}
@@ -72,7 +76,7 @@ class ApdOutputs(C.Structure):
 class ApdTiming(C.Structure):
     _fields_ = [("total_ms", C.c_float), ("init_ms", C.c_float), ("anchors_ms", C.c_float),
                 ("sweep_ms", C.c_float), ("post_ms", C.c_float), ("iter_ms", C.c_float * 8),
-                ("iterations", C.c_int32)]
+                ("iterations", C.c_int32), ("lists_ms", C.c_float), ("pairs_ms", C.c_float)]
 
 
 def default_params(num_images: int, depth_min: float, depth_max: float, **kw) -> ApdParams:
@@ -97,6 +101,24 @@ def _ptr(a, ctype):
 
 
 _TORCH_DTYPES = {np.dtype(np.float32): "float32", np.dtype(np.uint8): "uint8"}
+
+
+def _torch_device_sync(*objs):
+    """Wait for torch's current stream on the device of every CUDA tensor in `objs` (lists/tuples
+    are searched one level deep). The library works on its own non-blocking HIP stream, which does
+    not wait for torch's stream or for RCCL's: a tensor torch (an index_select, a .to(), a cat, an
+    all_gather) has just produced may still be in flight when the library reads it, and a fresh
+    torch.empty may reuse memory a pending torch kernel still touches."""
+    seen = set()
+    for o in objs:
+        for t in (o if isinstance(o, (list, tuple)) else (o,)):
+            if t is None or not hasattr(t, "is_cuda") or not t.is_cuda:
+                continue
+            if t.device.index in seen:
+                continue
+            seen.add(t.device.index)
+            import torch
+            torch.cuda.current_stream(t.device).synchronize()
 
 
 def _keep(a, dtype):
@@ -370,6 +392,9 @@ class Engine:
     def set_problem(self, arrays: ProblemArrays):
         pb = arrays.build()
         self._arrays = arrays
+        # device-resident inputs (scan_runner.py) may be fresh outputs of torch / RCCL kernels
+        _torch_device_sync(arrays._imgs, getattr(arrays, "_deps", None), arrays._planes, arrays._weak,
+                           arrays._conf, arrays._sa)
         self._check(self.lib.apd_set_problem(self.ctx, C.byref(pb)), "apd_set_problem")
 
     def run(self):
@@ -404,6 +429,7 @@ class Engine:
         s.planes = _ptr(o.planes, C.c_float)
         s.weak_info = _ptr(o.weak_info, C.c_uint8)
         s.confidence = _ptr(o.confidence, C.c_uint8)
+        _torch_device_sync(o.planes)
         self._check(self.lib.apd_get_results(self.ctx, C.byref(s)), "apd_get_results")
         return o
 
@@ -414,6 +440,7 @@ class Engine:
         sh, sw = src.shape[:2]
         dst = torch.empty((dh, dw) + tuple(src.shape[2:]), dtype=src.dtype, device=src.device)
         elem = src.element_size() * (src[0, 0].numel() if src.dim() > 2 else 1)
+        _torch_device_sync(src, dst)
         self._check(self.lib.apd_device_resize_nearest(self.ctx, src.data_ptr(), sw, sh, dst.data_ptr(), dw, dh, elem),
                     "apd_device_resize_nearest")
         return dst
@@ -423,6 +450,7 @@ class Engine:
         import torch
         depth = torch.empty((height, width), dtype=torch.float32, device=device)
         planes = torch.empty((height, width, 4), dtype=torch.float32, device=device)
+        _torch_device_sync(depth, planes)
         self._check(self.lib.apd_result_device(self.ctx, depth.data_ptr(), planes.data_ptr()), "apd_result_device")
         return depth, planes
 

@@ -667,6 +667,28 @@ struct FastTex {
         }
     }
     __device__ __forceinline__ float sample(const Tap &t) const { return finish(t, load(t)); }
+    // Compact tap (2 VGPRs instead of 3, for windows kept in flight together): the fixed-point
+    // fractions (qx & 255, qy & 255) packed in one register and converted at finish -- the same
+    // values as Tap::f ((float)(q & 255) * 2^-8 is exact either way).
+    struct CTap { uint32_t off; uint32_t fq; };
+    __device__ __forceinline__ CTap ctap(apd_f2 XY, float iz) const {
+        apd_f2 p = XY * iz;
+        p.x = __builtin_amdgcn_fmed3f(p.x, -1.0f, Wm1);
+        p.y = __builtin_amdgcn_fmed3f(p.y, -1.0f, Hm1);
+        const apd_f2 q = pk_fma(p, (apd_f2){256.0f, 256.0f}, (apd_f2){512.5f, 512.5f});
+        const int qx = (int)q.x, qy = (int)q.y;
+        CTap t;
+        t.off = ((__umul24((uint32_t)qy >> 8, W1) + ((uint32_t)qx >> 8)) << SHIFT) + vbase;
+        t.fq = ((uint32_t)qx & 255u) | (((uint32_t)qy & 255u) << 16);
+        return t;
+    }
+    __device__ __forceinline__ Raw cload(const CTap &t) const { return *(const APD_G Raw *)(base + t.off); }
+    __device__ __forceinline__ float cfinish(const CTap &c, const Raw &v) const {
+        Tap t;
+        t.off = c.off;
+        t.f = (apd_f2){(float)(c.fq & 255u), (float)(c.fq >> 16)} * 0.00390625f;
+        return finish(t, v);
+    }
 };
 
 // The 36 taps of a ComputeBilateralNCCOld window (6x6, step 2) and their moments, for a texel source

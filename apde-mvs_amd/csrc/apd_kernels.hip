@@ -29,16 +29,18 @@ using namespace apd;
 
 #define WAVE 64
 #define BLOCK 256
-// profiling slots: APD_PROF_COUNTERS public counters (apd_hip.h), then per-phase cycle sums of
-// instrumented builds (-DAPD_PHASE_STAMPS: wave 0 of every workgroup adds the clock64() delta of each
-// phase -- barrier to barrier -- to slot 8 + phase; read with apd_profile_counters(ctx, c, 32))
-#define APD_PROF_SLOTS 32
+// profiling slots: APD_PROF_COUNTERS public counters (apd_hip.h) in slots 0..31, then the
+// measurement slots of instrumented builds from APD_INSTR (-DAPD_PHASE_STAMPS: wave 0 of every
+// workgroup adds the clock64() delta of each phase -- barrier to barrier -- to slot APD_INSTR + 8 +
+// phase; LANE_STAT / APD_ANCHOR_STATS at APD_INSTR + their slot; read with apd_profile_counters(ctx, c, 64))
+#define APD_PROF_SLOTS 64
+#define APD_INSTR 32
 #ifdef APD_PHASE_STAMPS
 #define PHASE_STAMP(i)                                                                       \
     do {                                                                                     \
         if (a.evals && threadIdx.x == 0) {                                                   \
             const long long t_ = clock64();                                                  \
-            atomicAdd(a.evals + 8 + (i), (unsigned long long)(t_ - t_phase_));               \
+            atomicAdd(a.evals + APD_INSTR + 8 + (i), (unsigned long long)(t_ - t_phase_));    \
             t_phase_ = t_;                                                                   \
         }                                                                                    \
     } while (0)
@@ -48,8 +50,8 @@ using namespace apd;
     do {                                                                                     \
         const unsigned long long b_ = __ballot(pred);                                        \
         if (a.evals && b_ && (threadIdx.x & 63) == 0) {                                      \
-            atomicAdd(a.evals + (slot), 1ull);                                               \
-            atomicAdd(a.evals + (slot) + 1, (unsigned long long)__builtin_popcountll(b_));   \
+            atomicAdd(a.evals + APD_INSTR + (slot), 1ull);                                   \
+            atomicAdd(a.evals + APD_INSTR + (slot) + 1, (unsigned long long)__builtin_popcountll(b_)); \
         }                                                                                    \
     } while (0)
 #else
@@ -525,8 +527,8 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
                     }
 #ifdef APD_ANCHOR_STATS  // measurement build: steps, the attempt that succeeded, wave-level steps
                     if (a.evals) {
-                        atomicAdd(a.evals + 20 + (used == 4 && !((dvalid >> di) & 1u) ? 4 : used - 1), 1ull);
-                        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(true))) atomicAdd(a.evals + 25, 1ull);
+                        atomicAdd(a.evals + APD_INSTR + 20 + (used == 4 && !((dvalid >> di) & 1u) ? 4 : used - 1), 1ull);
+                        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(true))) atomicAdd(a.evals + APD_INSTR + 25, 1ull);
                     }
 #endif
                     g.n = n0 + 4u * (uint32_t)used;
@@ -1581,6 +1583,35 @@ __device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
 // statement. Every lane of the wave executes the same instruction stream; lanes that do not need
 // this window (`live` false) run on a parked homography and discard the sums.
 // Reference taps: tap tk of the window at rb[tk * rs] (WvRefT: &rref[tap0 * VM_P + p], VM_P).
+// The IEEE statement of an NCC-New window's taps (lanes whose window fails window_rcp_ok).
+template <bool F16, int NW, int INC>
+__device__ __forceinline__ void ncc_new_window_slow(const Args &a, const typename std::conditional<F16, _Float16, float>::type *rb,
+                                                    int rs, uint64_t mask, const Hom &Hm, int ax, int ay, const SrcTex<F16> &Q,
+                                                    float &ss, float &sss, float &srs) {
+    const float Wm1 = (float)(a.W - 1), Hm1 = (float)(a.H - 1);
+    const uint32_t W1 = SrcTex<F16>::pitch(a.W);
+    for (int i = 0; i < NW; ++i) {
+        const float x = (float)(ax - 5 + INC * i);
+        const float cx = fmaf(Hm.h[0], x, Hm.h[2]);
+        const float cy = fmaf(Hm.h[3], x, Hm.h[5]);
+        const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
+        for (int j = 0; j < NW; ++j) {
+            const int tk = i * NW + j;
+            if (!((mask >> tk) & 1ull)) continue;
+            const float y = (float)(ay - 5 + INC * j);
+            const float X = fmaf(Hm.h[1], y, cx);
+            const float Y = fmaf(Hm.h[4], y, cy);
+            const float Z = fmaf(Hm.h[7], y, cz);
+            const float iz = 1.0f / Z;
+            const QuadTap t = quad_tap(Wm1, Hm1, W1, X * iz, Y * iz);
+            const float v = bilerp(Q.fetch(t.idx), t.ax, t.ay);
+            const float r = rb[tk * rs];
+            ss += v;
+            sss = fmaf(v, v, sss);
+            srs = fmaf(r, v, srs);
+        }
+    }
+}
 template <bool F16, int NW, int INC>
 __device__ __forceinline__ void ncc_new_window(const Args &a, const typename std::conditional<F16, _Float16, float>::type *rb,
                                                int rs, uint64_t mask, const Hom &Hm, int ax, int ay, bool live,
@@ -1652,31 +1683,60 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const typename std
             }
         }
     }
-    if (sm && live && !fast) {
-        const float Wm1 = (float)(a.W - 1), Hm1 = (float)(a.H - 1);
-        const uint32_t W1 = SrcTex<F16>::pitch(a.W);
-        for (int i = 0; i < NW; ++i) {
-            const float x = (float)(ax - 5 + INC * i);
-            const float cx = fmaf(Hm.h[0], x, Hm.h[2]);
-            const float cy = fmaf(Hm.h[3], x, Hm.h[5]);
+    if (sm && live && !fast) ncc_new_window_slow<F16, NW, INC>(a, rb, rs, mask, Hm, ax, ay, Q, ss, sss, srs);
+}
+
+// Two 3x3 anchor windows (INC 5) with all 18 gathers in flight before the first is consumed: the
+// fast-tap statements of ncc_new_window<F16, 3, 5> for each window, lanes f0 / f1 only (the rest of
+// each window's lanes take ncc_new_window_slow). Compact taps keep the pair at 72 VGPRs of tap state.
+template <bool F16>
+__device__ __forceinline__ void ncc_new_window_pair(const typename std::conditional<F16, _Float16, float>::type *rb0,
+                                                    const typename std::conditional<F16, _Float16, float>::type *rb1,
+                                                    int rs, uint32_t m0, uint32_t m1, const Hom &Hm, int ax0, int ay0,
+                                                    int ax1, int ay1, bool f0, bool f1, const FastTex<F16, true> &T,
+                                                    float (&s0)[3], float (&s1)[3]) {
+    using TT = FastTex<F16, true>;
+    typename TT::CTap t0[9], t1[9];
+    typename TT::Raw q0[9], q1[9];
+    auto taps = [&](int ax, int ay, typename TT::CTap *t) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const float x = (float)(ax - 5 + 5 * i);
+            const apd_f2 cxy = {fmaf(Hm.h[0], x, Hm.h[2]), fmaf(Hm.h[3], x, Hm.h[5])};
             const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
-            for (int j = 0; j < NW; ++j) {
-                const int tk = i * NW + j;
-                if (!((mask >> tk) & 1ull)) continue;
-                const float y = (float)(ay - 5 + INC * j);
-                const float X = fmaf(Hm.h[1], y, cx);
-                const float Y = fmaf(Hm.h[4], y, cy);
-                const float Z = fmaf(Hm.h[7], y, cz);
-                const float iz = 1.0f / Z;
-                const QuadTap t = quad_tap(Wm1, Hm1, W1, X * iz, Y * iz);
-                const float v = bilerp(Q.fetch(t.idx), t.ax, t.ay);
-                const float r = rb[tk * rs];
-                ss += v;
-                sss = fmaf(v, v, sss);
-                srs = fmaf(r, v, srs);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const float y = (float)(ay - 5 + 5 * j);
+                const apd_f2 XY = pk_fma((apd_f2){Hm.h[1], Hm.h[4]}, (apd_f2){y, y}, cxy);
+                t[i * 3 + j] = T.ctap(XY, rcp_newton(fmaf(Hm.h[7], y, cz)));
             }
         }
+    };
+    auto consume = [&](const typename TT::CTap *t, const typename TT::Raw *q, uint32_t m,
+                       const typename std::conditional<F16, _Float16, float>::type *rb, float (&sa)[3]) {
+#pragma unroll
+        for (int tk = 0; tk < 9; ++tk) {
+            const float v = T.cfinish(t[tk], q[tk]);
+            if ((m >> tk) & 1u) {
+                const float r = rb[tk * rs];
+                sa[0] += v;
+                sa[1] = fmaf(v, v, sa[1]);
+                sa[2] = fmaf(r, v, sa[2]);
+            }
+        }
+    };
+    if (f0) {
+        taps(ax0, ay0, t0);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) q0[k] = T.cload(t0[k]);
     }
+    if (f1) {
+        taps(ax1, ay1, t1);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) q1[k] = T.cload(t1[k]);
+    }
+    if (f0) consume(t0, q0, m0, rb0, s0);
+    if (f1) consume(t1, q1, m1, rb1, s1);
 }
 
 // NCC-New reference side of pixel slot p (APD.cu:448-575): the 9 windows' reference taps, SA tap
@@ -1747,7 +1807,8 @@ __device__ __forceinline__ void wv_build_windows(const Args &a, WvRefT<F16> &L, 
 // of the source image, APD.cu:510-520), the one input the Strong sweep changes between launches.
 template <bool F16>
 __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L, int p, int px, int py, int s, float4 pl,
-                                            bool want, bool *seldep = nullptr) {
+                                            bool want, bool *seldep = nullptr, uint32_t *nwc = nullptr,
+                                            uint32_t *nwa = nullptr) {
     const int W = a.W, H = a.H;
     const Hom Hm = homography(a, s, pl);
     float ptx, pty;
@@ -1760,6 +1821,7 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
     int ns = 0;
     float center_cost = 0.0f, strong_weight = 0.0f;
     bool dead = !alive;  // COST_MAX (centre or centre-anchor projected out of the image)
+#ifndef WV_PAIR_WINDOWS  // (A/B: the anchor windows one at a time / in pairs)
 #pragma unroll 1
     for (int k = 0; k < 9; ++k) {
         const int pk = L.anc[k * VM_P + p];
@@ -1794,6 +1856,7 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
             ncc_new_window<F16, 3, 5>(a, &L.rref[(36 + 9 * (k - 1)) * VM_P + p], VM_P, (uint64_t)L.tmask[(k - 1) * VM_P + p], Hm, ax, ay,
                                       live, fast, T, Q, ss, sss, srs);
         if (!live) continue;
+        if (nwc) { if (k == 0) ++*nwc; else ++*nwa; }  // (profiling: windows evaluated)
         const float wsum = (float)L.wsum[k * VM_P + p];
         if (wsum == 0.0f) continue;
         const float c = ncc_finalize(L.wsr[k * VM_P + p], L.wsrr[k * VM_P + p], ss, sss, srs, wsum);
@@ -1806,6 +1869,90 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
             strong_weight += 1.0f;
         }
     }
+#else
+    // The window states in the reference's k order (APD.cu:488-571): evaluated (livem), an
+    // out-of-frame COST_MAX entry (maxm), or absent. Anchor 0 out of frame kills the pixel first.
+    uint32_t livem = 0, maxm = 0;
+#pragma unroll 1
+    for (int k = 0; k < 9; ++k) {
+        const int pk = L.anc[k * VM_P + p];
+        if (!(alive && pk >= 0 && ((awin >> k) & 1u))) continue;
+        const int ax = pk & 0xFFFF, ay = pk >> 16;
+        float asx, asy;
+        project(Hm, (float)ax, (float)ay, asx, asy);
+        if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) {
+            if (k != 0) {
+                if (seldep) *seldep = true;
+                if ((a.sel[ax + ay * W] >> (s - 1)) & 1u) maxm |= 1u << k;
+            } else {
+                dead = true;
+                alive = false;
+            }
+        } else {
+            livem |= 1u << k;
+        }
+    }
+    const bool live0 = livem & 1u;
+    if (__ballot(live0)) {  // the centre window (6x6, step 2)
+        const int pk = L.anc[p];
+        const int ax = live0 ? (pk & 0xFFFF) : px, ay = live0 ? (pk >> 16) : py;
+        const bool fast = live0 && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
+        float ss = 0.0f, sss = 0.0f, srs = 0.0f;
+        ncc_new_window<F16, 6, 2>(a, &L.rref[p], VM_P, L.tmask0[p], Hm, ax, ay, live0, fast, T, Q, ss, sss, srs);
+        if (live0) {
+            if (nwc) ++*nwc;
+            const float wsum = (float)L.wsum[p];
+            if (wsum != 0.0f) center_cost = ncc_finalize(L.wsr[p], L.wsrr[p], ss, sss, srs, wsum);
+        }
+    }
+    // the anchor windows two at a time (18 gathers in flight), entries appended in k order
+#pragma unroll 1
+    for (int k = 1; k < 9; k += 2) {
+        const bool l0 = (livem >> k) & 1u, l1 = (livem >> (k + 1)) & 1u;
+        float c0 = 0.0f, c1 = 0.0f;
+        bool e0 = false, e1 = false;
+        if (__ballot(l0 || l1)) {
+            const int pk0 = L.anc[k * VM_P + p], pk1 = L.anc[(k + 1) * VM_P + p];
+            const int ax0 = l0 ? (pk0 & 0xFFFF) : px, ay0 = l0 ? (pk0 >> 16) : py;
+            const int ax1 = l1 ? (pk1 & 0xFFFF) : px, ay1 = l1 ? (pk1 >> 16) : py;
+            const bool f0 = l0 && window_rcp_ok(Hm, (float)(ax0 - 5), (float)(ay0 - 5));
+            const bool f1 = l1 && window_rcp_ok(Hm, (float)(ax1 - 5), (float)(ay1 - 5));
+            const auto *rb0 = &L.rref[(36 + 9 * (k - 1)) * VM_P + p], *rb1 = rb0 + 9 * VM_P;
+            const uint32_t m0 = L.tmask[(k - 1) * VM_P + p], m1 = L.tmask[k * VM_P + p];
+            float s0[3] = {0.0f, 0.0f, 0.0f}, s1[3] = {0.0f, 0.0f, 0.0f};
+            ncc_new_window_pair<F16>(rb0, rb1, VM_P, m0, m1, Hm, ax0, ay0, ax1, ay1, f0, f1, T, s0, s1);
+            if (__ballot((l0 && !f0) || (l1 && !f1))) {
+                if (l0 && !f0) ncc_new_window_slow<F16, 3, 5>(a, rb0, VM_P, m0, Hm, ax0, ay0, Q, s0[0], s0[1], s0[2]);
+                if (l1 && !f1) ncc_new_window_slow<F16, 3, 5>(a, rb1, VM_P, m1, Hm, ax1, ay1, Q, s1[0], s1[1], s1[2]);
+            }
+            if (l0) {
+                if (nwa) ++*nwa;
+                const float wsum = (float)L.wsum[k * VM_P + p];
+                if (wsum != 0.0f) { c0 = ncc_finalize(L.wsr[k * VM_P + p], L.wsrr[k * VM_P + p], s0[0], s0[1], s0[2], wsum); e0 = true; }
+            }
+            if (l1) {
+                if (nwa) ++*nwa;
+                const float wsum = (float)L.wsum[(k + 1) * VM_P + p];
+                if (wsum != 0.0f) { c1 = ncc_finalize(L.wsr[(k + 1) * VM_P + p], L.wsrr[(k + 1) * VM_P + p], s1[0], s1[1], s1[2], wsum); e1 = true; }
+            }
+        }
+        const bool x0 = (maxm >> k) & 1u, x1 = (maxm >> (k + 1)) & 1u;
+        if (x0 || e0) {
+            const float c = x0 ? APD_COST_MAX : c0;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) if (t == ns) sc[t] = c;
+            ns++;
+            strong_weight += 1.0f;
+        }
+        if (x1 || e1) {
+            const float c = x1 ? APD_COST_MAX : c1;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) if (t == ns) sc[t] = c;
+            ns++;
+            strong_weight += 1.0f;
+        }
+    }
+#endif
     if (dead) return APD_COST_MAX;
     if (strong_weight <= 1e-6f) return center_cost;
     float mx = -1e10f;
@@ -1844,13 +1991,13 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
 template <bool F16>
 __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
                                                                 int iter, const float *__restrict__ cand,
-                                                                const uint8_t *__restrict__ cand_done, int wc) {
+                                                                const uint8_t *__restrict__ cand_done, int wc, int direct_) {
     const int N = a.N, W = a.W;
     PHASE_BEGIN;
-    // direct: k_weak_cand_vm evaluated every pixel's anchor candidates (no SA masks: no group is left
-    // to the sweep), so P2 reads their costs from `cand` and the table is [N][64] (current plane),
-    // later [5][N][64] (wv_lds_bytes)
-    const bool direct = cand != nullptr && !a.sa_any;
+    // direct: the candidate kernels evaluated every pixel's anchor candidates (the pair table, or
+    // k_weak_cand_vm without SA masks: no group is left to the sweep), so P2 reads their costs from
+    // `cand` and the table is [N][64] (current plane), later [5][N][64] (wv_lds_bytes)
+    const bool direct = cand != nullptr && direct_ != 0;
     WvLdsT<F16> &L = *reinterpret_cast<WvLdsT<F16> *>(apd_dyn_lds);
     float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64] (direct: [N][64]), later [5][N][64]
     uint8_t *wts = reinterpret_cast<uint8_t *>(costL + (direct ? 5 : 9) * N * VM_P);  // [N][64] view weights
@@ -1916,6 +2063,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     // The current plane is evaluated after the view selection (P1b), for the views it weights only:
     // cost_now = sum of fmaf(w_v, c_v) over all views, and a weight-0 view adds fmaf(0, c_v, .) == the
     // sum itself (c_v finite), so its value is never needed.
+    uint32_t nwc = 0, nwa = 0;  // profiling: centre / anchor windows this lane evaluated
     const int wi1 = cand ? a.amap[c1] : 0;
     const bool cand_ok = cand && pv1 && cand_done[wi1];  // per pixel (groups of k_weak_cand_vm span both colours)
     const int ntask = direct ? 0 : 8 * N;
@@ -1929,7 +2077,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             continue;
         }
         const float4 pl = L.hyp[h * VM_P + p1];
-        const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want);
+        const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
         if (want) val = nv;
         costL[t * VM_P + p1] = val;
     }
@@ -1989,7 +2137,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             for (int k = 0; k < 8; ++k) if (j == k) gval[k] = vv;
         }
 #ifdef APD_PHASE_STAMPS
-        if (a.evals && threadIdx.x == 0) atomicAdd(a.evals + 8 + 7, (unsigned long long)(clock64() - tg0_));
+        if (a.evals && threadIdx.x == 0) atomicAdd(a.evals + APD_INSTR + 8 + 7, (unsigned long long)(clock64() - tg0_));
 #endif
         float fc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         float wn = 0.0f;
@@ -2041,7 +2189,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             if (iter == 0 && a.wcur && !__ballot(want && __builtin_isnan(kept)))
                 nv = kept;
             else
-                nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want);
+                nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
             if (want) {
                 val = nv;
                 if (geom) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
@@ -2130,7 +2278,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[p1];
             LANE_STAT(22, want);
             const float4 fit = fit1;
-            const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, fit, want);
+            const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, fit, want, nullptr, &nwc, &nwa);
             if (want) {
                 cv = nv;
                 if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, fit), cv);
@@ -2228,7 +2376,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
                     const int px = pxy & 0xFFFF, py = pxy >> 16;
                     const float4 tp = WV_CAND(L)[k * VM_P + p];
                     LANE_STAT(20, want);
-                    const float nv = ncc_new_vm<F16>(a, L, p, px, py, v + 1, tp, want);
+                    const float nv = ncc_new_vm<F16>(a, L, p, px, py, v + 1, tp, want, nullptr, &nwc, &nwa);
                     if (want) {
                         float cv = nv;
                         if (geom) cv = fmaf(gf, geom_cost(a, px, py, v + 1, tp), cv);
@@ -2270,7 +2418,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[(1 + k) * VM_P + p1];
             LANE_STAT(20, want);
             const float4 tp = WV_CAND(L)[k * VM_P + p1];
-            const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, tp, want);
+            const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, tp, want, nullptr, &nwc, &nwa);
             if (want) {
                 cv = nv;
                 if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
@@ -2303,10 +2451,16 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         if (lane == 0) { atomicAdd(a.evals + 1, (unsigned long long)nn); atomicAdd(a.evals + 2, (unsigned long long)ng); }
     }
     if (a.evals) {  // ... plus the fit-plane and refinement evaluations every wave issued (P3, P5)
-        uint32_t nn = issued_nn, ng = issued_g;
+        uint32_t nn = issued_nn, ng = issued_g, wc0 = nwc, wa0 = nwa;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) { nn += __shfl_xor(nn, o); ng += __shfl_xor(ng, o); }
-        if (lane == 0) { atomicAdd(a.evals + 1, (unsigned long long)nn); atomicAdd(a.evals + 2, (unsigned long long)ng); }
+        for (int o = 32; o > 0; o >>= 1) {
+            nn += __shfl_xor(nn, o); ng += __shfl_xor(ng, o);
+            wc0 += __shfl_xor(wc0, o); wa0 += __shfl_xor(wa0, o);
+        }
+        if (lane == 0) {
+            atomicAdd(a.evals + 1, (unsigned long long)nn); atomicAdd(a.evals + 2, (unsigned long long)ng);
+            atomicAdd(a.evals + 7, (unsigned long long)wc0); atomicAdd(a.evals + 8, (unsigned long long)wa0);
+        }
     }
 
     // ---- P6: acceptance, writes
@@ -2887,6 +3041,12 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
 #define GP_HS 8192     // LDS hash slots (a table closes at GP_HS / 2 keys; + <= 8 * GP_CHUNK per batch: load <= 0.75)
 #define GP_NONE 0xFFFFFFFFu
 
+// profiling: a wave's sum of the lanes' counts, one atomic per wave
+__device__ __forceinline__ void wave_count(unsigned long long *slot, uint32_t n) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+    if ((threadIdx.x & (WAVE - 1)) == 0 && n) atomicAdd(slot, (unsigned long long)n);
+}
 // Lanes are consecutive WEAK pixels in tile order, whose anchor k is often the same STRONG point: per
 // slot k the runs of equal anchors among neighbouring lanes take one atomic (run head).
 __device__ __forceinline__ void gp_run(bool ok, int q, int &head_lane, int &rank, int &len) {
@@ -2905,44 +3065,61 @@ __device__ __forceinline__ void gp_run(bool ok, int q, int &head_lane, int &rank
     const int end = above ? __builtin_ctzll(above) : 64;
     len = end - lane;
 }
-// references per window anchor (cnt) and each WEAK pixel's candidate bits (cbw: anchor h+1 valid and STRONG)
+// SA masks (APD.cu:464-465, 493-497, 526-530): with a non-zero label at the pixel, an anchor window is
+// used only when the anchor carries the same label, and its taps are then filtered by that label --
+// the anchor's own. With label 0 nothing is filtered. So a window's cost depends on (window anchor,
+// filtered, candidate plane, view) only: the table keys windows by (anchor, filtered) and each pixel's
+// used windows (wmw) replace the anchors' validity.
+__device__ __forceinline__ bool gp_window_used(const Args &a, int cid, int q) { return cid == 0 || (int)a.sa[q] == cid; }
+// references per window anchor (cnt), each WEAK pixel's candidate bits (cbw: anchor h+1 valid and
+// STRONG) and used windows (wmw: anchor k valid and, with an SA label, carrying it; bit k - 1)
 __global__ __launch_bounds__(BLOCK) void k_gp_count(Args a, const int *__restrict__ list, int count, int *__restrict__ cnt,
-                                                    uint8_t *__restrict__ cbw) {
+                                                    uint8_t *__restrict__ cbw, uint8_t *__restrict__ wmw) {
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     const bool act = i < count;
-    const int wi = a.amap[list[act ? i : count - 1]];
+    const int c = list[act ? i : count - 1];
+    const int wi = a.amap[c];
+    const int cid = a.sa_any ? (int)a.sa[c] : 0;
     const APD_G short2 *anc = a.anchors + (size_t)wi * 9;
-    uint32_t cb = 0;
+    uint32_t cb = 0, wm = 0;
 #pragma unroll 1
     for (int k = 1; k < 9; ++k) {
         const short2 ap = anc[k];
-        const bool ok = act && !(ap.x == -1 || ap.y == -1);
-        const int q = ok ? ap.x + ap.y * a.W : -1;
-        if (ok && a.weak[q] == APD_STRONG) cb |= 1u << (k - 1);
+        const bool valid = act && !(ap.x == -1 || ap.y == -1);
+        const int q = valid ? ap.x + ap.y * a.W : -1;
+        if (valid && a.weak[q] == APD_STRONG) cb |= 1u << (k - 1);
+        const bool ok = valid && gp_window_used(a, cid, q);
+        if (ok) wm |= 1u << (k - 1);
         int hl, rk, len;
         gp_run(ok, q, hl, rk, len);
         if (ok && rk == 0) atomicAdd(&cnt[q], len);
     }
-    if (act) cbw[wi] = (uint8_t)cb;
+    if (act) { cbw[wi] = (uint8_t)cb; wmw[wi] = (uint8_t)wm; }
 }
-// references (WEAK index * 8 + window slot k - 1) into their window anchor's segment
+// references (WEAK index * 8 + window slot k - 1, bit 31: filtered by the SA label) into their
+// window anchor's segment
+#define GP_FILT 0x80000000u
 __global__ __launch_bounds__(BLOCK) void k_gp_fill(Args a, const int *__restrict__ list, int count, int *__restrict__ cur,
                                                    uint32_t *__restrict__ refs) {
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     const bool act = i < count;
-    const uint32_t wi = (uint32_t)a.amap[list[act ? i : count - 1]];
+    const int c = list[act ? i : count - 1];
+    const uint32_t wi = (uint32_t)a.amap[c];
+    const int cid = a.sa_any ? (int)a.sa[c] : 0;
+    const uint32_t filt = cid != 0 ? GP_FILT : 0u;
     const APD_G short2 *anc = a.anchors + (size_t)wi * 9;
 #pragma unroll 1
     for (int k = 1; k < 9; ++k) {
         const short2 ap = anc[k];
-        const bool ok = act && !(ap.x == -1 || ap.y == -1);
-        const int q = ok ? ap.x + ap.y * a.W : -1;
+        const bool valid = act && !(ap.x == -1 || ap.y == -1);
+        const int q = valid ? ap.x + ap.y * a.W : -1;
+        const bool ok = valid && gp_window_used(a, cid, q);
         int hl, rk, len;
         gp_run(ok, q, hl, rk, len);
         int pos = 0;
         if (ok && rk == 0) pos = atomicAdd(&cur[q], len);
         pos = __shfl(pos, hl) + rk;
-        if (ok) refs[pos] = wi * 8u + (uint32_t)(k - 1);
+        if (ok) refs[pos] = (wi * 8u + (uint32_t)(k - 1)) | filt;
     }
 }
 // the window anchors that have references, in raster order (task list for k_gp_dedup): flags, then
@@ -2980,17 +3157,19 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
     while (cap < GP_HS && cap < n * 16) { cap <<= 1; ++lg; }
     const uint32_t msk = (uint32_t)cap - 1u;
     auto slot_of = [&](uint32_t key) { return (key * 0x9E3779B1u) >> (32 - lg); };
-    // candidates (valid, STRONG anchors 1..8) of reference r: bits + positions
+    // candidates (valid, STRONG anchors 1..8) of reference r: bits + keys (candidate position + 1,
+    // GP_FILT when the window is SA-filtered)
     auto cands = [&](int r, uint32_t &wi, uint32_t &k, uint32_t (&qh)[8]) {
         const uint32_t ref = refs[r];
-        wi = ref >> 3;
+        const uint32_t filt = ref & GP_FILT;
+        wi = (ref & ~GP_FILT) >> 3;
         k = ref & 7u;
         const APD_G short2 *anc = a.anchors + (size_t)wi * 9;
         const uint32_t cb = cbw[wi];
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
             const short2 ap = anc[h + 1];
-            qh[h] = (uint32_t)(ap.x + ap.y * a.W);  // (used only where cb has the bit: a valid anchor)
+            qh[h] = ((uint32_t)(ap.x + ap.y * a.W) + 1u) | filt;  // (used only where cb has the bit: a valid anchor)
         }
         return cb;
     };
@@ -3008,7 +3187,7 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
 #pragma unroll
             for (int h = 0; h < 8; ++h) {
                 if (!((cb >> h) & 1u)) continue;
-                const uint32_t key = qh[h] + 1u;
+                const uint32_t key = qh[h];
                 uint32_t sl = slot_of(key);
                 for (;;) {
                     const uint32_t old = atomicCAS(&hs[sl], 0u, key);
@@ -3021,6 +3200,9 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
         }
         __syncthreads();
         const int nd = nfresh;
+        // every thread has read nfresh before any wave's next-batch inserts can add to it (else
+        // `close` and `base` could differ between waves)
+        __syncthreads();
         const bool close = nd >= GP_HS / 2 || b0 + GP_CHUNK >= n;
         if (!close) continue;  // (uniform)
         if (PASS == 1) {
@@ -3044,7 +3226,8 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
             for (int sl = s0; sl < s1; ++sl) {
                 const uint32_t key = hs[sl];
                 if (!key) continue;
-                plist[base + next] = make_int2(qx | (qy << 16), (int)(key - 1u));
+                // (window anchor x | SA-filtered << 15 | y << 16, candidate anchor position)
+                plist[base + next] = make_int2(qx | ((key & GP_FILT) ? 0x8000 : 0) | (qy << 16), (int)((key & ~GP_FILT) - 1u));
                 sid[sl] = (uint16_t)next;
                 ++next;
             }
@@ -3057,7 +3240,7 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
                 for (int h = 0; h < 8; ++h) {
                     pv[h] = GP_NONE;
                     if (!((cb >> h) & 1u)) continue;
-                    const uint32_t key = qh[h] + 1u;
+                    const uint32_t key = qh[h];
                     uint32_t sl = slot_of(key);
                     while (hs[sl] != key) sl = (sl + 1) & msk;
                     pv[h] = (uint32_t)(base + sid[sl]);
@@ -3081,27 +3264,50 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
 
 // every pair in every view: ComputeBilateralNCCNew's k >= 1 window (APD.cu:500-575), the same
 // statements as k_weak_cand_vm's pair windows; pcost[pair][v] rows padded to a multiple of 4 views
-// (< 0: window absent)
+// (< 0: window absent). The block's 256 pairs are consecutive, so their rows are one contiguous
+// range of pcost: the costs are staged in LDS ([pair][Np], gp_cost_lds_bytes) and written with
+// coalesced 16-byte stores after the view loop (a 4-byte store per (pair, view) at the row stride
+// wrote 4.2x the bytes, profiles/r3_pmc_k_gp_cost_c3b.json).
+static inline size_t gp_cost_lds_bytes(int N) { return (size_t)BLOCK * ((N + 3) & ~3) * sizeof(float); }
 template <bool F16>
 __global__ __launch_bounds__(BLOCK) void k_gp_cost(Args a, const int2 *__restrict__ plist, int np, float *__restrict__ pcost) {
     using RT = typename std::conditional<F16, _Float16, float>::type;
     __shared__ RT rref[9 * BLOCK];
-    const int N = a.N, W = a.W, H = a.H;
-    const int i = xcd_remap(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+    float *crow = apd_dyn_lds;  // [BLOCK][Np]
+    const int N = a.N, W = a.W, H = a.H, Np = (N + 3) & ~3;
+    const int i0 = xcd_remap(blockIdx.x, gridDim.x) * BLOCK;
+    const int i = i0 + threadIdx.x;
     const bool act = i < np;
     const int2 pr = plist[act ? i : np - 1];
-    const int ax = pr.x & 0xFFFF, ay = pr.x >> 16;
+    const int ax = pr.x & 0x7FFF, ay = pr.x >> 16;
+    const bool filt = (pr.x & 0x8000) != 0;  // SA-filtered window: taps with the anchor's label only
     const float4 pl = a.plane[pr.y];
-    float sr = 0.0f, srr = 0.0f;
+    float sr = 0.0f, srr = 0.0f, wsum = 9.0f;
+    uint64_t tm = 0x1FFull;
+    if (filt) {
+        // sa_at_dev's out-of-image -1 never equals the anchor's label (> 0); the anchor's own tap
+        // (t = 4) always matches, so wsum >= 1 (APD.cu:543's empty window cannot occur)
+        const int lab = a.sa[ax + ay * W];
+        tm = 0;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int ii = t / 3, jj = t - 3 * (t / 3);
+            if (sa_at_dev(a, ax - 5 + 5 * ii, ay - 5 + 5 * jj) == lab) tm |= 1ull << t;
+        }
+        wsum = (float)__builtin_popcountll(tm);
+    }
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
         const int ii = t / 3, jj = t - 3 * (t / 3);
         const float r = tex_ref(a, ax - 5 + 5 * ii, ay - 5 + 5 * jj);
         rref[t * BLOCK + threadIdx.x] = (RT)r;
-        sr += r;
-        srr = fmaf(r, r, srr);
+        if ((tm >> t) & 1ull) {
+            sr += r;
+            srr = fmaf(r, r, srr);
+        }
     }
     const uint32_t selk = a.sel[ax + ay * W];
+    uint32_t nlive = 0;
     for (int v = 0; v < N; ++v) {
         const int s = v + 1;
         const FastTex<F16, true> T(a, s);
@@ -3118,11 +3324,19 @@ __global__ __launch_bounds__(BLOCK) void k_gp_cost(Args a, const int2 *__restric
         if (__ballot(live)) {
             const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
             float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-            ncc_new_window<F16, 3, 5>(a, &rref[threadIdx.x], BLOCK, 0x1FFull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
-            if (live) res = ncc_finalize(sr, srr, ss, sss, srs, 9.0f);
+            ncc_new_window<F16, 3, 5>(a, &rref[threadIdx.x], BLOCK, tm, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            if (live) res = ncc_finalize(sr, srr, ss, sss, srs, wsum);
         }
-        if (act) pcost[(size_t)i * ((N + 3) & ~3) + v] = res;
+        nlive += live;
+        crow[threadIdx.x * Np + v] = res;
     }
+    if (a.evals) wave_count(a.evals + 5, nlive);  // (profiling: pair windows evaluated)
+    for (int v = N; v < Np; ++v) crow[threadIdx.x * Np + v] = -1.0f;  // (padding, never read)
+    __syncthreads();
+    const int nq = (min(BLOCK, np - i0) * Np) >> 2;  // float4s of the block's rows
+    const float4 *src = reinterpret_cast<const float4 *>(crow);
+    float4 *dst = reinterpret_cast<float4 *>(pcost + (size_t)i0 * Np);
+    for (int j = threadIdx.x; j < nq; j += BLOCK) dst[j] = src[j];
 }
 
 // the focal combination (APD.cu:576-593, Softmax 431-446) of one (pixel, candidate, view): centre
@@ -3155,23 +3369,22 @@ __device__ __forceinline__ float gp_combine(float cc, const float (&sc)[8]) {
     return (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
 }
 
-// the anchor candidates' costs from the pair costs: centre windows + focal combination (as
-// k_weak_cand_vm's phase D, without SA masks); lane = pixel, wave = candidate h.
-//   A  per view (the waves take the views together: one source image, the CU's L1): the centre
-//      window of (pixel, h) -> LDS ccost[v][h][p] (-1: dead, the pixel or its anchor 0 out of frame)
-//   B  per (pixel, h): the 8 windows' pair costs, 4 views per 16-byte load, and the focal
-//      combination of each view
+// the anchor candidates' centre windows (k_weak_cand_comb then combines them with the pair costs);
+// lane = pixel, wave = candidate h. Per view (the waves take the views together: one source image,
+// the CU's L1) the centre window of (pixel, h) -> out[v][h][WEAK index] (-1: dead, the pixel or its
+// anchor 0 projected out of frame). With an SA label at the pixel the centre window is used only
+// when anchor 0 carries the label (else center_cost stays 0, APD.cu:493-497) and its taps are
+// filtered by it (APD.cu:526-530); an empty window leaves center_cost 0 (APD.cu:543).
 template <bool F16>
 __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__restrict__ list, int count,
-                                                          const uint8_t *__restrict__ cbw, const uint32_t *__restrict__ pidx,
-                                                          const float *__restrict__ pcost,
-                                                          float *__restrict__ out, uint8_t *__restrict__ done, int wc) {
+                                                          const uint8_t *__restrict__ cbw, float *__restrict__ out,
+                                                          uint8_t *__restrict__ done, int wc) {
     using RT = typename std::conditional<F16, _Float16, float>::type;
     __shared__ RT cref[36 * VM_P];
     __shared__ float csr[VM_P], csrr[VM_P];
+    __shared__ uint64_t cmask[VM_P];
     __shared__ uint8_t cws[VM_P], cbits[VM_P];
     __shared__ int anc0[VM_P];
-    extern __shared__ float ccost[];  // [N][8][64]
     const int N = a.N, W = a.W, H = a.H;
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int first = blk * VM_P;
@@ -3183,13 +3396,15 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
     const int c1 = list[first + min(p1, np - 1)];
     const int py1 = c1 / W, px1 = c1 - py1 * W;
     const int wi1 = a.amap[c1];
+    const int cid = a.sa_any ? (int)a.sa[c1] : 0;
     const APD_G short2 *anc1 = a.anchors + (size_t)wi1 * 9;
     if (wave == 0) {
         int a0 = -1;
         uint32_t cb = 0;
         if (pv1) {
             const short2 z = anc1[0];
-            a0 = (z.x == -1 || z.y == -1) ? -1 : ((int)(uint16_t)z.x | ((int)z.y << 16));
+            const bool ok = !(z.x == -1 || z.y == -1) && (cid == 0 || (int)a.sa[z.x + z.y * W] == cid);
+            a0 = ok ? ((int)(uint16_t)z.x | ((int)z.y << 16)) : -1;  // (an unused window: as if absent)
             cb = cbw[wi1];
             done[wi1] = 1;
         }
@@ -3206,11 +3421,17 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
         }
     }
     __syncthreads();
-    if (wave == 1) {  // moments in wv_build_windows's tap order
+    if (wave == 1) {  // tap mask and moments in wv_build_windows's tap order
         float sr = 0.0f, srr = 0.0f, ws = 0.0f;
+        uint64_t m = 0;
         if (pv1 && anc0[p1] >= 0) {
+            const int pk = anc0[p1];
+            const int ax = pk & 0xFFFF, ay = pk >> 16;
             for (int t = 0; t < 36; ++t) {
+                const int i = t / 6, j = t - 6 * i;
+                if (cid != 0 && sa_at_dev(a, ax - 5 + 2 * i, ay - 5 + 2 * j) != cid) continue;
                 const float r = (float)cref[t * VM_P + p1];
+                m |= 1ull << t;
                 sr += r;
                 srr = fmaf(r, r, srr);
                 ws += 1.0f;
@@ -3219,9 +3440,11 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
         csr[p1] = sr;
         csrr[p1] = srr;
         cws[p1] = (uint8_t)ws;
+        cmask[p1] = m;
     }
     __syncthreads();
-    const int h = wave;  // PK_WAVES == 8 candidates
+    static_assert(PK_WAVES == 8, "k_weak_cand_g: wave h evaluates candidate h (8 anchor candidates)");
+    const int h = wave;
     const uint32_t cb = cbits[p1];
     const bool want = pv1 && ((cb >> h) & 1u);
     float4 pl = make_float4(0.0f, 0.0f, 1.0f, 1.0f);
@@ -3229,8 +3452,9 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
         const short2 ap = anc1[h + 1];
         pl = a.plane[ap.x + ap.y * W];
     }
-    // ---- A: centre windows
     const int pk0 = anc0[p1];
+    const uint64_t tm = cmask[p1];
+    uint32_t nlive = 0;
     for (int v = 0; v < N; ++v) {
         const int s = v + 1;
         const FastTex<F16, true> T(a, s);
@@ -3248,81 +3472,28 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
             if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) { live = false; dead = true; }
         }
         float center_cost = 0.0f;
-#ifdef GP_ABLATE_A  // timing-only (wrong values): no centre-window taps
-        live = false;
-#endif
         if (__ballot(live)) {
             const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
             float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-            ncc_new_window<F16, 6, 2>(a, &cref[p1], VM_P, ~0ull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            ncc_new_window<F16, 6, 2>(a, &cref[p1], VM_P, tm, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
             if (live) {
                 const float wsum = (float)cws[p1];
                 if (wsum != 0.0f) center_cost = ncc_finalize(csr[p1], csrr[p1], ss, sss, srs, wsum);
             }
         }
-#ifdef GP_FUSED
-        ccost[(v * 8 + h) * VM_P + p1] = dead ? -1.0f : center_cost;
-#else
+        nlive += live;
         // (k_weak_cand_comb reads it back and writes the candidate's cost in its place)
         if (want) out[((size_t)v * 8 + h) * (size_t)wc + wi1] = dead ? -1.0f : center_cost;
-#endif
-#ifdef GP_VIEW_SYNC  // (measured: keeping the waves on one view costs more than the shared L1 gains)
-        __syncthreads();
-#endif
     }
-#ifndef GP_FUSED
-    return;
-#endif
-    if (!want) return;  // (each lane reads back only its own entries: no barrier needed)
-    // ---- B: focal combination (APD.cu:576-593, Softmax 431-446) per view
-    const int Np = (N + 3) & ~3;
-    const float4 *pc4[8];
-    uint32_t pm0 = 0;  // windows whose pair exists (anchor k+1 valid)
-    {
-        const uint32_t *pp = pidx + (size_t)wi1 * 64 + h;  // [window k][candidate h]
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const short2 ak = anc1[k + 1];
-            const uint32_t id = pp[k * 8];
-            const bool ok = !(ak.x == -1 || ak.y == -1) && id != GP_NONE;
-            pc4[k] = reinterpret_cast<const float4 *>(pcost + (size_t)(ok ? id : 0u) * Np);
-            pm0 |= (uint32_t)ok << k;
-        }
-    }
-    for (int v0 = 0; v0 < N; v0 += 4) {
-        float4 q[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) q[k] = ((pm0 >> k) & 1u) ? pc4[k][v0 >> 2] : make_float4(-1.0f, -1.0f, -1.0f, -1.0f);
-#ifdef GP_ABLATE_B  // timing-only (wrong values): no pair-cost loads
-#pragma unroll
-        for (int k = 0; k < 8; ++k) q[k] = make_float4(0.5f, 0.5f, 0.5f, (float)k);
-#endif
-#pragma unroll
-        for (int dv = 0; dv < 4; ++dv) {
-            const int v = v0 + dv;
-            if (v >= N) break;
-            float sc[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) sc[k] = dv == 0 ? q[k].x : dv == 1 ? q[k].y : dv == 2 ? q[k].z : q[k].w;
-            const float cost = gp_combine(ccost[(v * 8 + h) * VM_P + p1], sc);
-            out[((size_t)v * 8 + h) * (size_t)wc + wi1] = cost;
-        }
-    }
+    if (a.evals) wave_count(a.evals + 6, nlive);  // (profiling: centre windows evaluated)
 }
-static inline size_t gp_cand_lds_bytes(int N) {
-#ifdef GP_FUSED
-    return (size_t)N * 8 * VM_P * sizeof(float);
-#else
-    (void)N;
-    return 0;
-#endif
-}
-// Phase B of k_weak_cand_g as its own kernel (the default): a thread per (WEAK pixel, candidate),
-// few registers and many waves in flight for the pair-cost gathers (a timing study of the fused
-// kernel put ~40 ms per C3 iteration on those loads); `out` holds the centre cost (< 0: dead) and
-// receives the candidate's cost in its place. Block = 4 candidates x 64 pixels of one group.
+// The focal combination (APD.cu:576-593, Softmax 431-446) of each (WEAK pixel, candidate) and view,
+// a thread per (pixel, candidate): few registers and many waves in flight for the pair-cost gathers.
+// `out` holds the centre cost (< 0: dead) and receives the candidate's cost in its place; the pixel's
+// used windows (wmw) say which of its 8 pair ids exist. Block = 4 candidates x 64 pixels of one group.
 __global__ __launch_bounds__(BLOCK) void k_weak_cand_comb(Args a, const int *__restrict__ list, int count,
-                                                          const uint8_t *__restrict__ cbw, const uint32_t *__restrict__ pidx,
+                                                          const uint8_t *__restrict__ cbw, const uint8_t *__restrict__ wmw,
+                                                          const uint32_t *__restrict__ pidx,
                                                           const float *__restrict__ pcost, float *__restrict__ out, int wc) {
     const int b = xcd_remap(blockIdx.x, gridDim.x);
     const int h = ((b & 1) << 2) + (threadIdx.x >> 6);
@@ -3331,22 +3502,18 @@ __global__ __launch_bounds__(BLOCK) void k_weak_cand_comb(Args a, const int *__r
     const int wi = a.amap[list[i]];
     if (!((cbw[wi] >> h) & 1u)) return;
     const int N = a.N, Np = (N + 3) & ~3;
-    const APD_G short2 *anc = a.anchors + (size_t)wi * 9;
+    const uint32_t wm = wmw[wi];
     const uint32_t *pp = pidx + (size_t)wi * 64 + h;  // [window k][candidate h]
     const float4 *pc4[8];
-    uint32_t pm0 = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const short2 ak = anc[k + 1];
-        const uint32_t id = pp[k * 8];
-        const bool ok = !(ak.x == -1 || ak.y == -1) && id != GP_NONE;
-        pc4[k] = reinterpret_cast<const float4 *>(pcost + (size_t)(ok ? id : 0u) * Np);
-        pm0 |= (uint32_t)ok << k;
+        const uint32_t id = ((wm >> k) & 1u) ? pp[k * 8] : 0u;
+        pc4[k] = reinterpret_cast<const float4 *>(pcost + (size_t)id * Np);
     }
     for (int v0 = 0; v0 < N; v0 += 4) {
         float4 q[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) q[k] = ((pm0 >> k) & 1u) ? pc4[k][v0 >> 2] : make_float4(-1.0f, -1.0f, -1.0f, -1.0f);
+        for (int k = 0; k < 8; ++k) q[k] = ((wm >> k) & 1u) ? pc4[k][v0 >> 2] : make_float4(-1.0f, -1.0f, -1.0f, -1.0f);
 #pragma unroll
         for (int dv = 0; dv < 4; ++dv) {
             const int v = v0 + dv;
@@ -3723,6 +3890,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
         __syncthreads();
         // ---- P1: (depth, view) tasks
         uint64_t defer = 0;
+        uint32_t n_ncc = 0, n_geo = 0;  // profiling: evaluations issued by this lane
         {
             // the per-view counts are read through readfirstlane: v stays wave-uniform (SGPR), so the
             // view's homography constants, cameras and texel base come through scalar loads
@@ -3747,6 +3915,8 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 const int qx = xy & 0xFFFF, qy = xy >> 16;
                 const int e = dd * VM_P + q;
                 const bool eval = has && pok[e];
+                n_ncc += eval;
+                n_geo += eval && geom;
                 const RefWin rwq{&L.refw[q], L.rmean[q], L.rvar[q], SA ? &saw[q] : nullptr};
                 float tc = 0.0f;
                 bool slow = false;
@@ -3797,6 +3967,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 tcL[(dd * N + v) * VM_P + q] = tc;
             }
         }
+        if (a.evals) { wave_count(a.evals + 3, n_ncc); wave_count(a.evals + 4, n_geo); }
         __syncthreads();
         // ---- P2: in-order weighted view sums per (pixel, depth)
         for (int dd = wave; dd < dc; dd += VM_WAVES) {
@@ -4999,12 +5170,13 @@ static int build_global_pairs(apd_ctx *ctx, int nw) {
     ctx->gp_np = 0;
     if (!try_ensure(ctx, ctx->gp_cnt, (HW + 1) * sizeof(int)) || !try_ensure(ctx, ctx->gp_cur, (HW + 1) * sizeof(int)) ||
         !try_ensure(ctx, ctx->gp_refs, (size_t)nw * 8 * sizeof(uint32_t)) ||
-        !try_ensure(ctx, ctx->gp_pidx, wc * 64 * sizeof(uint32_t)) || !try_ensure(ctx, ctx->gp_cb, wc))
+        !try_ensure(ctx, ctx->gp_pidx, wc * 64 * sizeof(uint32_t)) || !try_ensure(ctx, ctx->gp_cb, 2 * wc))
         return APD_OK;
     int *cnt = (int *)ctx->gp_cnt.p, *cur = (int *)ctx->gp_cur.p;
     HIP_OK(ctx, hipMemsetAsync(cnt, 0, (HW + 1) * sizeof(int), s));
+    // gp_cb: candidate bits [wc], then used windows [wc]
     hipLaunchKernelGGL(k_gp_count, dim3(blocks_for((size_t)nw, BLOCK)), dim3(BLOCK), 0, s, a, (const int *)ctx->wlist.p, nw, cnt,
-                       (uint8_t *)ctx->gp_cb.p);
+                       (uint8_t *)ctx->gp_cb.p, (uint8_t *)ctx->gp_cb.p + wc);
     int st;
     if ((st = exclusive_scan_int(ctx, cnt, cur, HW + 1))) return st == APD_ENOMEM ? APD_OK : st;
     int nrefs = 0;
@@ -5099,9 +5271,12 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
             if ((st = ensure(ctx, ctx->wdone, wc))) return st;
             if ((st = ensure(ctx, ctx->wlist, (size_t)(ctx->cnt[2] + ctx->cnt[3]) * sizeof(int)))) return st;
             if ((st = build_tile_list(ctx, 1, 2, (int *)ctx->wlist.p, tot + 5))) return st;
-            if (ctx->cand_global && !a.sa_any && (size_t)a.HW < (1u << 25) &&
+            (void)hipEventRecord(ctx->ev[14], s);
+            if (ctx->cand_global && (size_t)a.HW < (1u << 25) && a.W < 32768 &&
                 (st = build_global_pairs(ctx, ctx->cnt[2] + ctx->cnt[3])))
                 return st;
+        } else {
+            (void)hipEventRecord(ctx->ev[14], s);
         }
     }
     (void)hipEventRecord(ctx->ev[2], s);
@@ -5193,17 +5368,20 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             Args ac = a;
             ac.evals = evals;  // (only instrumented builds write it)
             if (ctx->gp_on) {
+                hipEvent_t e1 = prof_begin(ctx);
                 if (ctx->gp_np > 0)
-                    LAUNCH_TEX(k_gp_cost, dim3(blocks_for((size_t)ctx->gp_np, BLOCK)), dim3(BLOCK), 0, s, ac,
+                    LAUNCH_TEX(k_gp_cost, dim3(blocks_for((size_t)ctx->gp_np, BLOCK)), dim3(BLOCK), gp_cost_lds_bytes(a.N), s, ac,
                                (const int2 *)ctx->gp_plist.p, ctx->gp_np, (float *)ctx->gp_pcost.p);
-                LAUNCH_TEX(k_weak_cand_g, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), gp_cand_lds_bytes(a.N), s, ac, (const int *)ctx->wlist.p, nw,
-                           (const uint8_t *)ctx->gp_cb.p, (const uint32_t *)ctx->gp_pidx.p, (const float *)ctx->gp_pcost.p, (float *)ctx->wcand.p,
-                           (uint8_t *)ctx->wdone.p, wc);
-#ifndef GP_FUSED
+                prof_end(ctx, e1, APD_PROF_GP_COST, ctx->gp_np);
+                e1 = prof_begin(ctx);
+                LAUNCH_TEX(k_weak_cand_g, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), 0, s, ac, (const int *)ctx->wlist.p, nw,
+                           (const uint8_t *)ctx->gp_cb.p, (float *)ctx->wcand.p, (uint8_t *)ctx->wdone.p, wc);
+                prof_end(ctx, e1, APD_PROF_WEAK_CAND_G, nw);
+                e1 = prof_begin(ctx);
                 hipLaunchKernelGGL(k_weak_cand_comb, dim3(2 * blocks_for((size_t)nw, VM_P)), dim3(BLOCK), 0, s, ac,
-                                   (const int *)ctx->wlist.p, nw, (const uint8_t *)ctx->gp_cb.p, (const uint32_t *)ctx->gp_pidx.p,
-                                   (const float *)ctx->gp_pcost.p, (float *)ctx->wcand.p, wc);
-#endif
+                                   (const int *)ctx->wlist.p, nw, (const uint8_t *)ctx->gp_cb.p, (const uint8_t *)ctx->gp_cb.p + wc,
+                                   (const uint32_t *)ctx->gp_pidx.p, (const float *)ctx->gp_pcost.p, (float *)ctx->wcand.p, wc);
+                prof_end(ctx, e1, APD_PROF_WEAK_CAND_COMB, nw);
             } else {
                 LAUNCH_TEX(k_weak_cand_vm, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK),
                            (ctx->args.tex_f16 ? pk_lds_bytes<true>() : pk_lds_bytes<false>()), s, ac,
@@ -5220,10 +5398,11 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             aw.evals = evals;
             if (!(ctx->wcur_fresh && iter == 0)) aw.wcur = nullptr;
             e0 = prof_begin(ctx);
-            const bool direct = cand != nullptr && !a.sa_any;  // k_sweep_weak_vm's small cost table
+            // k_sweep_weak_vm's small cost table: every pixel's candidates are in `cand`
+            const bool direct = cand != nullptr && (ctx->gp_on || !a.sa_any);
             if (ctx->sweep_vm)
                 LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N, direct) : wv_lds_bytes<false>(a.N, direct)), s,
-                           aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, (const uint8_t *)ctx->wdone.p, wc);
+                           aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, (const uint8_t *)ctx->wdone.p, wc, (int)direct);
             else
                 LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
                            (const int *)list_ptr(ctx, 2 + colour), n, iter);
@@ -5264,7 +5443,11 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
             const int tw = ctx->dw_tile_w, th = VM_P / tw;
             const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
             const int dwc = dw_chunk(a.N, a.geom != 0, sa_lds_bytes(a));
-            LAUNCH_TEX_SA(k_depth_to_weak_vm, dim3(nb), dim3(VM_BLOCK), dw_lds_bytes(a.N, a.geom != 0, dwc) + sa_lds_bytes(a), s, a, dwc, tw);
+            Args ad = a;
+            ad.evals = (ctx->prof && ctx->evals.p) ? (APD_G unsigned long long *)ctx->evals.p : nullptr;
+            hipEvent_t e0 = prof_begin(ctx);
+            LAUNCH_TEX_SA(k_depth_to_weak_vm, dim3(nb), dim3(VM_BLOCK), dw_lds_bytes(a.N, a.geom != 0, dwc) + sa_lds_bytes(a), s, ad, dwc, tw);
+            prof_end(ctx, e0, APD_PROF_DEPTH_TO_WEAK, a.HW);
         } else {
             const size_t lds = group_lds_bytes(a.N, 61 + 36);
             LAUNCH_TEX(k_depth_to_weak, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), lds, s, a);
@@ -5301,6 +5484,8 @@ int32_t apd_run_patchmatch(apd_ctx *ctx) {
     memset(&t, 0, sizeof(t));
     (void)hipEventElapsedTime(&t.total_ms, ctx->ev[0], ctx->ev[13]);
     (void)hipEventElapsedTime(&t.anchors_ms, ctx->ev[0], ctx->ev[1]);
+    (void)hipEventElapsedTime(&t.lists_ms, ctx->ev[1], ctx->ev[14]);
+    (void)hipEventElapsedTime(&t.pairs_ms, ctx->ev[14], ctx->ev[2]);
     (void)hipEventElapsedTime(&t.init_ms, ctx->ev[2], ctx->ev[3]);
     (void)hipEventElapsedTime(&t.sweep_ms, ctx->ev[3], ctx->ev[12]);
     (void)hipEventElapsedTime(&t.post_ms, ctx->ev[12], ctx->ev[13]);

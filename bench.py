@@ -57,6 +57,7 @@ METRIC = "Mpix/s per PatchMatch iteration (ref view, N src) at 1/2/4/8 GPU; dept
 FLOP_PER_NCC_OLD = 36 * 36 + 150   # 36 samples x 36 flop + homography/finalise
 FLOP_PER_NCC_NEW = 108 * 36 + 150  # <= 108 samples (6x6 centre + 8 anchors x 3x3)
 FLOP_PER_GEOM = 80                 # one geometric-consistency term
+FLOP_PER_TAP = 36                  # one bilinear NCC sample (projection, lerp, moments)
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak (packed FP32)
 PEAK_HBM_GBS = 8000.0
 FINAL_ROUND = 3  # C3 has 4 rounds (6048 -> 756 halvings, main.cpp:129-146); the headline is round 3
@@ -109,11 +110,12 @@ def first_init_priors(eng, sc, ids, N):
     return priors
 
 
-def final_round_problem(sc, priors, ref, N):
-    """The REFINE_ITER + APD + geometric pass of main.cpp's last round (main.cpp:336-352, i = 3, j = 0)."""
+def final_round_problem(sc, priors, ref, N, sa=False):
+    """The REFINE_ITER + APD + geometric pass of main.cpp's last round (main.cpp:336-352, i = 3, j = 0);
+    sa: with the reference view's SAM-style segment labels as the SA mask (config C5, APD.cpp:641-652)."""
     import apd_abi as A
     import cases
-    arr = cases.refine_problem(sc, priors, ref, N, state=A.REFINE_ITER, geom=True, apd=True)
+    arr = cases.refine_problem(sc, priors, ref, N, state=A.REFINE_ITER, geom=True, apd=True, sa=sa)
     arr.params.rotate_time = min(2 ** FINAL_ROUND, 4)
     arr.params.ransac_threshold = 0.01 - FINAL_ROUND * 0.00125
     arr.params.weak_peak_radius = max(4 - 2 * 0, 2)
@@ -173,11 +175,21 @@ def weak_roofline(eng, steps, W, N):
     ms = cand["ms_total"] + sweep["ms_total"]
     flop = cnt[1] * FLOP_PER_NCC_NEW + cnt[2] * FLOP_PER_GEOM
     achieved = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+    # device-issued work: the windows the kernels actually evaluated (the pair table evaluates each
+    # distinct (window anchor, candidate) window once per view; RandomInitialization's kept costs and
+    # the exact early exit skip evaluations) -- 3x3 windows 9 taps, 6x6 centre windows 36 taps
+    taps = 9 * (cnt[5] + cnt[8]) + 36 * (cnt[6] + cnt[7])
+    flop_issued = taps * FLOP_PER_TAP + cnt[2] * FLOP_PER_GEOM
+    achieved_issued = flop_issued / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     pmc = latest_pmc("k_sweep_weak_vm", W, N)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     return {
         "bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+        "basis": "algorithmic (effective): the NCC-New evaluations CheckerboardPropagationWeak performs, "
+                 "priced at SURVEY.md §8d's 4038 flop; achieved_issued / frac_issued price the windows the "
+                 "kernels actually evaluated (36 flop per tap)",
+        "achieved_issued": round(achieved_issued, 3), "frac_issued": round(achieved_issued / PEAK_FP32_TFLOPS, 4),
         "kernel": "k_sweep_weak_vm (+ k_gp_cost + k_weak_cand_g + k_weak_cand_comb): CheckerboardPropagationWeak, APD.cu:1442-1615",
         "note": "VALU-FP32 gather/stencil kernels (no matrix work, SURVEY.md §8d); one Weak sweep "
                 "iteration = the anchor-candidate kernels (k_gp_cost + k_weak_cand_g + k_weak_cand_comb) + 2 k_sweep_weak_vm launches; flops = device-counted "
@@ -186,8 +198,16 @@ def weak_roofline(eng, steps, W, N):
         "ms_per_iteration": round(ms / max(steps, 1), 3),
         "flop_per_iteration": flop / max(steps, 1),
         "ncc_new_per_iteration": round(cnt[1] / max(steps, 1)),
+        "issued_windows_per_iteration": {"k_gp_cost 3x3": round(cnt[5] / max(steps, 1)),
+                                         "k_weak_cand_g 6x6": round(cnt[6] / max(steps, 1)),
+                                         "k_sweep_weak_vm 6x6": round(cnt[7] / max(steps, 1)),
+                                         "k_sweep_weak_vm 3x3": round(cnt[8] / max(steps, 1))},
         "geom_terms_per_iteration": round(cnt[2] / max(steps, 1)),
-        "launch_avg_ms": {"k_gp_cost+k_weak_cand_g+k_weak_cand_comb": cand["avg_ms"], "k_sweep_weak_vm": sweep["avg_ms"],
+        "launch_avg_ms": {"k_gp_cost+k_weak_cand_g+k_weak_cand_comb": cand["avg_ms"],
+                          "k_gp_cost": kernel_stats(eng, A.PROF_GP_COST)["avg_ms"],
+                          "k_weak_cand_g": kernel_stats(eng, A.PROF_WEAK_CAND_G)["avg_ms"],
+                          "k_weak_cand_comb": kernel_stats(eng, A.PROF_WEAK_CAND_COMB)["avg_ms"],
+                          "k_sweep_weak_vm": sweep["avg_ms"],
                           "k_sweep_strong_vm": strong["avg_ms"], "k_ransac_fit": ransac["avg_ms"]},
         "launches": {"k_gp_cost+k_weak_cand_g+k_weak_cand_comb": cand["launches"], "k_sweep_weak_vm": sweep["launches"],
                      "k_sweep_strong_vm": strong["launches"], "k_ransac_fit": ransac["launches"]},
@@ -225,38 +245,69 @@ def gt_accuracy(sc, ref, eng, W, H, N):
             "weak_frac_out": round(float((out.weak_info == A.WEAK).mean()), 4)}
 
 
+def depth_to_weak_roofline(eng, W, N):
+    """Roofline of DepthToWeak (k_depth_to_weak_vm, APD.cu:2103-2250) over the profiled launches:
+    device-counted NCC-Old evaluations x 1446 + geometric terms x 80 / launch time."""
+    import apd_abi as A
+    st = kernel_stats(eng, A.PROF_DEPTH_TO_WEAK)
+    cnt = eng.profile_counters()
+    n = max(st["launches"], 1)
+    launch_ms = st["ms_total"] / n
+    flop = (cnt[3] * FLOP_PER_NCC_OLD + cnt[4] * FLOP_PER_GEOM) / n
+    achieved = flop / (launch_ms * 1e-3) / 1e12 if launch_ms > 0 else 0.0
+    pmc = latest_pmc("k_depth_to_weak_vm", W, N)
+    return {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+            "pmc_file": pmc.get("_file") if pmc else None,
+            "kernel": "k_depth_to_weak_vm: DepthToWeak, APD.cu:2103-2250",
+            "launch_ms": round(launch_ms, 3), "launches": st["launches"], "flop_per_launch": flop,
+            "ncc_old_per_launch": round(cnt[3] / n), "geom_terms_per_launch": round(cnt[4] / n)}
+
+
 def end_to_end(eng, arr, sc, ref, W, H, N):
     """One full RunPatchMatch (the main.cpp:157-161 bracket), after an untimed one (first-use
-    allocations and code loading out of the way)."""
+    allocations and code loading out of the way); the timed run is profiled (HIP events around the
+    loop-body kernels and DepthToWeak), which also gives DepthToWeak's roofline."""
     eng.set_problem(arr)
     eng.run()
     eng.set_problem(arr)
+    eng.profile_reset(True)
     t1 = time.perf_counter()
     eng.run()
     t2 = time.perf_counter()
     tm = eng.timing()
+    dtw = depth_to_weak_roofline(eng, W, N)
+    eng.profile_reset(False)
     iters = tm.iterations
+    parts = tm.anchors_ms + tm.lists_ms + tm.pairs_ms + tm.init_ms + tm.sweep_ms + tm.post_ms
     r = {"run_patchmatch_ms": round(tm.total_ms, 3), "host_wall_ms": round((t2 - t1) * 1e3, 3),
          "mpix_s_end_to_end": round(W * H * iters / (tm.total_ms * 1e-3) / 1e6, 3),
-         "anchors_ms": round(tm.anchors_ms, 3), "init_ms": round(tm.init_ms, 3), "sweep_ms": round(tm.sweep_ms, 3),
-         "post_ms": round(tm.post_ms, 3), "iter_ms": [round(x, 3) for x in list(tm.iter_ms)[:iters]]}
+         "anchors_ms": round(tm.anchors_ms, 3), "lists_ms": round(tm.lists_ms, 3), "pairs_ms": round(tm.pairs_ms, 3),
+         "init_ms": round(tm.init_ms, 3), "sweep_ms": round(tm.sweep_ms, 3),
+         "post_ms": round(tm.post_ms, 3), "accounted_frac": round(parts / tm.total_ms, 4) if tm.total_ms else None,
+         "iter_ms": [round(x, 3) for x in list(tm.iter_ms)[:iters]], "roofline_depth_to_weak": dtw}
     r.update(gt_accuracy(sc, ref, eng, W, H, N))
     return r
 
 
-def apd_pass_once(eng, sc, ref, N, label):
+def apd_pass_once(eng, sc, ref, N, label, sa=False):
     """Priors + one fresh timed pass (3 iterations) + end to end, for a secondary scene variant."""
     W, H = sc.width, sc.height
     ids = [ref] + [j for j, _ in sc.pairs[ref]][:N]
     priors = first_init_priors(eng, sc, ids, N)
-    arr = final_round_problem(sc, priors, ref, N)
+    arr = final_round_problem(sc, priors, ref, N, sa=sa)
     el, step_ms = timed_fresh_iterations(eng, arr, arr.params.max_iterations, 1, lambda: None)
     roof = weak_roofline(eng, len(step_ms), W, N)
     eng.profile_reset(False)
     e2e = end_to_end(eng, arr, sc, ref, W, H, N)
-    return {"workload": label, "mpix_s_iter": round(W * H * len(step_ms) / el / 1e6, 3),
-            "iter_ms": [round(x, 2) for x in step_ms], "weak_frac": round(float((arr.weak_info == 0).mean()), 4),
-            "roofline_frac": roof["frac"], "roofline_achieved": roof["achieved"], "end_to_end": e2e}
+    r = {"workload": label, "mpix_s_iter": round(W * H * len(step_ms) / el / 1e6, 3),
+         "iter_ms": [round(x, 2) for x in step_ms], "weak_frac": round(float((arr.weak_info == 0).mean()), 4),
+         "roofline_frac": roof["frac"], "roofline_achieved": roof["achieved"],
+         "launch_avg_ms": roof["launch_avg_ms"], "end_to_end": e2e}
+    if sa:
+        r["sa_labelled_frac"] = round(float((arr.sa_mask > 0).mean()), 4)
+    return r
 
 
 def c2_first_init(eng, steps, warmup):
@@ -293,6 +344,7 @@ def cpu_baseline(eng, texture, N, w, h, threads):
         return None
     t_iter = times[1]
     return {"value": round(w * h / t_iter / 1e6, 5), "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "weak_frac": round(float((arr.weak_info == 0).mean()), 4),
             "sample": f"oracle (C restatement{', OpenMP' if threads > 1 else ', 1 thread'}) on the headline "
                       f"pass (REFINE_ITER, APD + focal + geom + impetus, final-round params) of the same "
                       f"synthetic scan rendered at {w}x{h}, N={N}, one loop-body iteration "
@@ -313,6 +365,7 @@ def main():
     ap.add_argument("--end-to-end", type=int, default=1, help="also time one full RunPatchMatch (0/1)")
     ap.add_argument("--c2", type=int, default=1, help="also measure configs[1] (C2 FIRST_INIT) (0/1)")
     ap.add_argument("--rich", type=int, default=1, help="also measure the texture-rich scene variant (0/1)")
+    ap.add_argument("--sa", type=int, default=1, help="also measure the headline pass with SA labels (C5's pass) (0/1)")
     args = ap.parse_args()
     t_start_all = time.time()
 
@@ -375,7 +428,12 @@ def main():
     line = None
     if rank == 0:
         e2e = end_to_end(eng, arr, sc, ref, W, H, N) if args.end_to_end else None
-        del arr, sc
+        del arr
+        sa_pass = None
+        if args.sa and n_gpus == 1:
+            sa_pass = apd_pass_once(eng, sc, ref, N, f"C5's per-GPU workload: the {workload_name(W, H, N, True)} pass "
+                                                   f"with SAM-style segment labels as the SA mask (APD.cu:464-530)", sa=True)
+        del sc
         single = n_gpus == 1
         c2 = c2_first_init(eng, 6, 2) if (args.c2 and single) else None
         rich = None
@@ -415,11 +473,13 @@ def main():
             "iter_ms": [round(x, 2) for x in step_ms],
             "roofline": roof,
             "roofline_strong_sweep": roof_strong_apd,
+            "roofline_depth_to_weak": e2e["roofline_depth_to_weak"] if e2e else None,
             "cpu_baseline": cpu,
             "cpu_baseline_1core": cpu1,
             "end_to_end": e2e,
             "c2_first_init": c2,
             "rich_texture": rich,
+            "sa_pass": sa_pass,
             "scene_gen_s": round(t_scene, 2),
             "priors_s": round(t_priors, 2),
             "bench_wall_s": round(time.time() - t_start_all, 1),

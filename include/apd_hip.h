@@ -4,7 +4,7 @@
  * This is the drop-in boundary for the per-reference-view PatchMatch hot path of APDe-MVS.
  * It replaces the in-process `class APD` lifecycle of the reference:
  *
- *   reference (APD.h:205-232, APD.cpp:458-842, APD.cu:2663-2737)     this ABI
+ *   reference (APD.h:88-190, APD.cpp:458-842, APD.cu:2663-2737)      this ABI
  *   ---------------------------------------------------------------  -----------------------------
  *   APD::APD(const Problem&)                   APD.cpp:458             apd_create()
  *   APD::InuputInitialization()                APD.cpp:501-685  \
@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define APD_ABI_VERSION 1
+#define APD_ABI_VERSION 2  /* 2: apd_timing.lists_ms / pairs_ms, 9 profiling counters, kinds 4-7 */
 #define APD_MAX_IMAGES 32          /* main.h:40  MAX_IMAGES            */
 #define APD_ANCHOR_NUM 9           /* main.h:41  ANCHOR_NUM            */
 #define APD_MAX_SEARCH_RADIUS 4096 /* main.h:42  MAX_SEARCH_RADIUS     */
@@ -150,6 +150,9 @@ typedef struct apd_timing {
     float post_ms;             /* GetDepthandNormal + filter + DepthToWeak + Confidence + LocalRefine */
     float iter_ms[8];          /* per-iteration sweep time (first 8 iterations)             */
     int32_t iterations;
+    float lists_ms;            /* the sweeps' pixel lists (after NeigbourUpdate)            */
+    float pairs_ms;            /* the Weak candidates' image-wide pair table (APD passes)   */
+    /* total_ms == anchors_ms + lists_ms + pairs_ms + init_ms + sweep_ms + post_ms           */
 } apd_timing;
 
 typedef struct apd_ctx apd_ctx;
@@ -202,8 +205,13 @@ int32_t apd_get_timing(apd_ctx *ctx, apd_timing *timing);
    kind since the reset. apd_profile_query == apd_profile_kernel(APD_PROF_STRONG_SWEEP). */
 #define APD_PROF_STRONG_SWEEP 0 /* k_sweep_strong_vm (CheckerboardPropagationStrong, APD.cu:1098-1440) */
 #define APD_PROF_RANSAC_FIT 1   /* k_ransac_fit (RANSACToGetFitPlane, APD.cu:2486-2598)             */
-#define APD_PROF_WEAK_CAND 2    /* k_weak_cand_vm (anchor-candidate NCC-New of the Weak sweep)       */
+#define APD_PROF_WEAK_CAND 2    /* the Weak sweep's anchor candidates: k_gp_cost + k_weak_cand_g +
+                                   k_weak_cand_comb (pair table), or k_weak_cand_vm                  */
 #define APD_PROF_WEAK_SWEEP 3   /* k_sweep_weak_vm (CheckerboardPropagationWeak, APD.cu:1442-1615)   */
+#define APD_PROF_DEPTH_TO_WEAK 4 /* k_depth_to_weak_vm (DepthToWeak, APD.cu:2103-2250)                */
+#define APD_PROF_GP_COST 5      /* k_gp_cost alone (pair windows, inside APD_PROF_WEAK_CAND)         */
+#define APD_PROF_WEAK_CAND_G 6  /* k_weak_cand_g alone (centre windows, inside APD_PROF_WEAK_CAND)    */
+#define APD_PROF_WEAK_CAND_COMB 7 /* k_weak_cand_comb alone (focal combination, inside WEAK_CAND)   */
 int32_t apd_profile_reset(apd_ctx *ctx, int32_t enable);
 int32_t apd_profile_kernel(apd_ctx *ctx, int32_t kind, double *ms_total, int64_t *launches,
                            int64_t *pixels);
@@ -218,9 +226,19 @@ int32_t apd_profile_query(apd_ctx *ctx, double *sweep_ms_total, int64_t *sweep_l
        them: shared anchor windows in k_weak_cand_vm, RandomInitialization's kept costs, or the
        sweep itself), plus the fit-plane and refinement-candidate evaluations of views with weight
        > 0 the sweep actually issued (those its exact early exit proves unnecessary are not counted);
-   [2] geometric-consistency terms of the same evaluations (APD.cu:1561, 1583, 1037, 1079).
+   [2] geometric-consistency terms of the same evaluations (APD.cu:1561, 1583, 1037, 1079);
+   [3] NCC-Old evaluations DepthToWeak issued (APD.cu:2155-2186: active pixel x disparity in range x
+       selected view; disparities 0 and 60 only with the curve export);
+   [4] geometric-consistency terms DepthToWeak issued;
+   The rest count what the Weak path's kernels actually evaluated (device-issued work, as opposed to
+   [1], the work the reference's CheckerboardPropagationWeak would do):
+   [5] 3x3 pair windows k_gp_cost evaluated (pair x view, window inside the source image);
+   [6] 6x6 centre windows k_weak_cand_g evaluated;
+   [7] 6x6 centre windows k_sweep_weak_vm evaluated itself (current plane, fit plane, refinement
+       candidates, and the anchor candidates when no candidate kernel ran);
+   [8] 3x3 anchor windows k_sweep_weak_vm evaluated itself.
    apd_profile_evaluations(ctx, &n) == apd_profile_counters(ctx, &n, 1). */
-#define APD_PROF_COUNTERS 4
+#define APD_PROF_COUNTERS 9
 int32_t apd_profile_counters(apd_ctx *ctx, int64_t *counts, int32_t n);
 int32_t apd_profile_evaluations(apd_ctx *ctx, int64_t *ncc_evaluations);
 

@@ -107,7 +107,18 @@ CASES = {
     # texture-rich scene variant (synth texture="rich"): fine detail, 30-50 % WEAK
     "first_n6_rich": (128, 96, 6, "first_rich"),
     "refine_iter_apd_geom_rich": (128, 96, 6, "apd_geom_rich"),
+    # config C5's pass (final round with SAM edge priors): SA labels with a label-0 band, N = 10,
+    # rotate_time 4 -- the image-wide pair table keyed by (window anchor, SA-filtered)
+    "refine_iter_sa_n10_apd_geom_rt4": (144, 88, 10, "apd_geom_sa_rt4"),
 }
+
+
+def c5_final_pass(sc, priors, n, ref=0):
+    """main.cpp's last APD + geometric pass (i = 3: rotate_time 4) of a scan with SAM edge priors
+    (APD.cpp:641-652): the reference view's labels, with a label-0 column band so that SA-filtered
+    and unfiltered windows meet in one wave."""
+    return refine_problem(sc, priors, ref, n, state=A.REFINE_ITER, geom=True, apd=True, sa="zero_band",
+                          rotate_time=4, ransac_threshold=0.01 - 3 * 0.00125, weak_peak_radius=4)
 
 
 def make_case(name, oracle_run):
@@ -132,6 +143,8 @@ def make_case(name, oracle_run):
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, sa="zero_band")
     if kind == "apd_geom_sa0":
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, sa="zero_band")
+    if kind == "apd_geom_sa_rt4":
+        return c5_final_pass(sc, priors, n)
     if kind == "apd_geom_rt4":
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, rotate_time=4)
     if kind in ("apd_geom", "apd_geom_rich"):

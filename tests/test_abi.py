@@ -37,7 +37,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_abi_version(lib):
-    assert lib.apd_abi_version() == 1
+    assert lib.apd_abi_version() == 2
 
 
 def test_no_device_is_an_error_not_a_crash(lib):
@@ -62,7 +62,7 @@ int main(void) {
   printf("apd_camera %zu\napd_params %zu\napd_problem %zu\napd_outputs %zu\napd_timing %zu\n",
          sizeof(apd_camera), sizeof(apd_params), sizeof(apd_problem), sizeof(apd_outputs), sizeof(apd_timing));
   P(apd_camera, depth_num) P(apd_params, state) P(apd_params, geom_factor) P(apd_problem, params)
-  P(apd_problem, seed) P(apd_problem, sa_mask) P(apd_outputs, reliable_curve) P(apd_timing, iterations)
+  P(apd_problem, seed) P(apd_problem, sa_mask) P(apd_outputs, reliable_curve) P(apd_timing, iterations) P(apd_timing, pairs_ms)
   printf("apd_fusion_view %zu\n", sizeof(apd_fusion_view));
   P(apd_fusion_view, camera) P(apd_fusion_view, depth) P(apd_fusion_view, confidence)
   return 0;
@@ -88,6 +88,7 @@ int main(void) {
     assert int(got["apd_problem.sa_mask"]) == A.ApdProblem.sa_mask.offset
     assert int(got["apd_outputs.reliable_curve"]) == A.ApdOutputs.reliable_curve.offset
     assert int(got["apd_timing.iterations"]) == A.ApdTiming.iterations.offset
+    assert int(got["apd_timing.pairs_ms"]) == A.ApdTiming.pairs_ms.offset
     assert int(got["apd_fusion_view"]) == C.sizeof(A.ApdFusionView)
     assert int(got["apd_fusion_view.camera"]) == A.ApdFusionView.camera.offset
     assert int(got["apd_fusion_view.depth"]) == A.ApdFusionView.depth.offset

@@ -249,3 +249,47 @@ def test_c3_fullsize_apd_properties(engine, engine_tw16):
         eng.close()
     assert np.isfinite(a.planes[..., 3]).all()
     gt_floor(sc, a)
+
+
+# ---- config C5's per-GPU workload (BASELINE.json configs[4]): the final-round APD pass with SAM edge
+# priors (SA labels, APD.cu:464-530, 664-719) at full resolution
+
+def test_c5_quarter_sa_bit_exact(engine):
+    """C5's pass at 480x264, N = 10 (SA labels with a label-0 band, rotate_time 4), bit-exact against
+    the oracle."""
+    sc = synth.make_scene(480, 264, 10, seed=20251115)
+    priors = slim_priors(engine, sc, 10, range(len(sc.images)))
+    arr = cases.c5_final_pass(sc, priors, 10)
+    assert (arr.weak_info == A.WEAK).any() and (arr.sa_mask > 0).any() and (arr.sa_mask == 0).any()
+    ref = oracle_lib.run(oracle_lib.load(), arr, 16)
+    got = run(engine, arr)
+    assert_same(ref, got, "480x264 N=10 SA APD + geom rt4")
+
+
+def test_c5_fullsize_sa_properties(engine, engine_tw16):
+    """C5's pass at its real shape (6048x4032, N = 10, SA labels with a label-0 band, rotate_time 4):
+    repeat-run identity, list-tile independence, fp32 texels, LocalRefine without the hand-over, the
+    Weak sweep evaluating the anchor candidates itself (APD_NO_CAND_PAIRS=1) == the SA-keyed pair
+    table, finite depths, ground-truth floors."""
+    sc = synth.make_scene(6048, 4032, 10, seed=20251115)
+    priors = slim_priors(engine, sc, 10, range(len(sc.images)))
+    arr = cases.c5_final_pass(sc, priors, 10)
+    del priors
+    assert (arr.sa_mask > 0).mean() > 0.5
+    a = run_slim(engine, arr)
+    assert int(a.weak_count[0]) > 0
+    assert_same_slim(a, run_slim(engine, arr), "C5 repeat run")
+    assert_same_slim(a, run_slim(engine_tw16, arr), "C5 16-wide list tiles")
+    for var, what in (("APD_TEX_F32", "fp32 quad texels"), ("APD_NO_LR_HANDOVER", "LocalRefine without the hand-over"),
+                      ("APD_NO_CAND_PAIRS", "anchor candidates in the sweep")):
+        os.environ[var] = "1"
+        try:
+            eng = A.Engine(0, engine.lib)
+            try:
+                assert_same_slim(a, run_slim(eng, arr), "C5 " + what)
+            finally:
+                eng.close()
+        finally:
+            os.environ.pop(var, None)
+    assert np.isfinite(a.planes[..., 3]).all()
+    gt_floor(sc, a)

@@ -15,8 +15,9 @@ eng.set_problem(arr)
 eng.profile_reset(True)
 eng.prepare()
 eng.synchronize()
-c = (A.C.c_int64 * 32)()
-eng._check(eng.lib.apd_profile_counters(eng.ctx, c, 32), "counters")
+c = (A.C.c_int64 * 64)()
+eng._check(eng.lib.apd_profile_counters(eng.ctx, c, 64), "counters")
+c = list(c)[32:]  # the instrumented builds' slots (APD_INSTR = 32)
 steps = sum(c[20:25])
 print(f"lane steps {steps}: success at attempt 1..4 {[c[20 + i] for i in range(4)]}, none {c[24]}; "
       f"wave steps {c[25]} (lane utilisation {steps / max(64 * c[25], 1):.3f}); "

@@ -19,8 +19,9 @@ eng.run()  # warm
 eng.set_problem(arr)
 eng.profile_reset(True)
 eng.run()
-c = (A.C.c_int64 * 32)()
-eng._check(eng.lib.apd_profile_counters(eng.ctx, c, 32), "counters")
+c = (A.C.c_int64 * 64)()
+eng._check(eng.lib.apd_profile_counters(eng.ctx, c, 64), "counters")
+c = list(c)[32:]  # the instrumented builds' slots (APD_INSTR = 32)
 names = {8: "cand setup (hash, windows)", 9: "cand pair windows", 10: "cand centre windows", 11: "cand focal combination",
          0: "sweep P0 anchors/windows", 1: "sweep P1 current plane", 2: "sweep P2 view selection+geom",
          3: "sweep P3 fit plane", 4: "sweep P4 candidates", 5: "sweep P5 refinement", 6: "sweep P6 acceptance"}

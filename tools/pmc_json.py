@@ -13,6 +13,7 @@ ap.add_argument("--width", type=int, default=3024)
 ap.add_argument("--height", type=int, default=2016)
 ap.add_argument("--n-src", type=int, default=8)
 ap.add_argument("--stats")
+ap.add_argument("--last", type=int, default=0, help="only the last N dispatches of the kernel (e.g. the APD pass after its FIRST_INIT priors)")
 ap.add_argument("--source", default="rocprofv3 --pmc, one pass per counter group (tools/pmc_profile.sh), "
                                     "bench.py --steps 2 --warmup 1")
 a = ap.parse_args()
@@ -25,6 +26,9 @@ for f in glob.glob(os.path.join(a.src, "**", "*counter_collection.csv"), recursi
             continue
         name = r["Kernel_Name"]
         per[(r["Counter_Name"], r["Dispatch_Id"])] += float(r["Counter_Value"])
+    if a.last > 0:
+        keep = sorted({int(i) for (_, i) in per}, reverse=False)[-a.last:]
+        per = {k: v for k, v in per.items() if int(k[1]) in keep}
     for (k, _), v in per.items():
         d[k].append(v)
 m = {k: sum(v) / len(v) for k, v in d.items()}
