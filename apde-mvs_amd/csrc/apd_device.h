@@ -445,27 +445,6 @@ __device__ __forceinline__ RefWin refwin_from_lds(const float *r) {
     w.var = fmaf(-sr, sr, srr);
     return w;
 }
-__device__ __forceinline__ void build_refwin(const Args &a, int px, int py, float *lds_r, int v, int N, RefWin &w) {
-    for (int k = v; k < 36; k += N) {
-        const int i = k / 6, j = k - 6 * (k / 6);
-        lds_r[k] = tex_ref(a, px - 5 + 2 * i, py - 5 + 2 * j);
-    }
-    // LDS operations of one wavefront execute in order: the pixel's other lanes see the writes.
-    __builtin_amdgcn_wave_barrier();
-    float sr = 0.0f, srr = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 36; ++k) {
-        const float r = lds_r[k];
-        sr += r;
-        srr = fmaf(r, r, srr);
-    }
-    const float inv = 1.0f / 36.0f;
-    sr *= inv;
-    srr *= inv;
-    w.r = lds_r;
-    w.mean = sr;
-    w.var = fmaf(-sr, sr, srr);
-}
 
 // Visiting slot k (0..35) of the SA branch: quadrant q = k / 9 with signs (+,+), (-,-), (+,-), (-,+)
 // (sign[] of APD.cu:664-719), tap j = k % 9 at the odd offsets off[] of that branch.
@@ -553,8 +532,9 @@ __device__ __forceinline__ float rcp_newton(float z) {
 // bound on the magnitude of the terms of Z (rounding error of any tap's Z is < 2^-21 S, and Z is
 // affine, so every tap's computed Z keeps the corners' sign and |Z| >= 2^-101); and |h0..h5| <= 2^100
 // so X, Y are finite. NaN -> false.
-__device__ __forceinline__ bool window_rcp_ok(const Hom &Hm, float x0, float y0) {
-    const float x1 = x0 + 10.0f, y1 = y0 + 10.0f;
+// (window_rcp_ok_box: the same proof for every tap in the box [x0, x1] x [y0, y1], e.g. the bounding
+// box of all windows of one NCC-New evaluation: the corners' Z bound every tap's, as Z is affine)
+__device__ __forceinline__ bool window_rcp_ok_box(const Hom &Hm, float x0, float y0, float x1, float y1) {
     const float z00 = fmaf(Hm.h[7], y0, fmaf(Hm.h[6], x0, Hm.h[8]));
     const float z10 = fmaf(Hm.h[7], y0, fmaf(Hm.h[6], x1, Hm.h[8]));
     const float z01 = fmaf(Hm.h[7], y1, fmaf(Hm.h[6], x0, Hm.h[8]));
@@ -568,6 +548,9 @@ __device__ __forceinline__ bool window_rcp_ok(const Hom &Hm, float x0, float y0)
     const float hm = fmaxf(fmaxf(fmaxf(fabsf(Hm.h[0]), fabsf(Hm.h[1])), fmaxf(fabsf(Hm.h[2]), fabsf(Hm.h[3]))),
                            fmaxf(fabsf(Hm.h[4]), fabsf(Hm.h[5])));
     return (mn >= lo || mx <= -lo) && S <= 0x1p100f && hm <= 0x1p100f;
+}
+__device__ __forceinline__ bool window_rcp_ok(const Hom &Hm, float x0, float y0) {
+    return window_rcp_ok_box(Hm, x0, y0, x0 + 10.0f, y0 + 10.0f);
 }
 // v_fma_mix_f32 with both fp16 operands taken from the low (lo) / high (hi) halves: fma(a, (float)b,
 // (float)c) in fp32 with exact fp16->fp32 conversions. Written as inline asm because the SLP
@@ -667,28 +650,6 @@ struct FastTex {
         }
     }
     __device__ __forceinline__ float sample(const Tap &t) const { return finish(t, load(t)); }
-    // Compact tap (2 VGPRs instead of 3, for windows kept in flight together): the fixed-point
-    // fractions (qx & 255, qy & 255) packed in one register and converted at finish -- the same
-    // values as Tap::f ((float)(q & 255) * 2^-8 is exact either way).
-    struct CTap { uint32_t off; uint32_t fq; };
-    __device__ __forceinline__ CTap ctap(apd_f2 XY, float iz) const {
-        apd_f2 p = XY * iz;
-        p.x = __builtin_amdgcn_fmed3f(p.x, -1.0f, Wm1);
-        p.y = __builtin_amdgcn_fmed3f(p.y, -1.0f, Hm1);
-        const apd_f2 q = pk_fma(p, (apd_f2){256.0f, 256.0f}, (apd_f2){512.5f, 512.5f});
-        const int qx = (int)q.x, qy = (int)q.y;
-        CTap t;
-        t.off = ((__umul24((uint32_t)qy >> 8, W1) + ((uint32_t)qx >> 8)) << SHIFT) + vbase;
-        t.fq = ((uint32_t)qx & 255u) | (((uint32_t)qy & 255u) << 16);
-        return t;
-    }
-    __device__ __forceinline__ Raw cload(const CTap &t) const { return *(const APD_G Raw *)(base + t.off); }
-    __device__ __forceinline__ float cfinish(const CTap &c, const Raw &v) const {
-        Tap t;
-        t.off = c.off;
-        t.f = (apd_f2){(float)(c.fq & 255u), (float)(c.fq >> 16)} * 0.00390625f;
-        return finish(t, v);
-    }
 };
 
 // The 36 taps of a ComputeBilateralNCCOld window (6x6, step 2) and their moments, for a texel source
@@ -923,112 +884,8 @@ __device__ __forceinline__ float ncc_old_fast(const Args &a, int px, int py, int
     return ncc_old_fast_h<F16, RS>(a, px, py, s, homography(a, s, pl), rw, slow);
 }
 
-template <bool F16, int RS = 1>
-__device__ __forceinline__ float ncc_old(const Args &a, int px, int py, int s, float4 pl, const RefWin &rw) {
-    bool slow;
-    const float v = ncc_old_fast<F16, RS>(a, px, py, s, pl, rw, slow);
-    if (__builtin_expect(slow, 0)) return ncc_old_slow<F16>(a.self, px, py, s, pl, rw.r, RS, rw.mean, rw.var);
-    return v;
-}
 
-// sa label at a possibly out-of-image linear index (same rule as the oracle's sa_at)
-template <class AT>
-__device__ __forceinline__ int sa_at(const AT &a, int x, int y) {
-    long idx = (long)y * a.W + x;
-    if (idx < 0 || idx >= a.HW) return -1;
-    return a.sa[idx];
-}
 
-// ComputeBilateralNCCNew + Softmax focal weighting (APD.cu:448-593, 431-446)
-template <bool F16>
-__device__ __noinline__ float ncc_new(const APD_G Args *ap, int px, int py, int s, float4 pl) {
-    const APD_G Args &a = *ap;
-    const int W = a.W, H = a.H;
-    const int center = px + py * W;
-    const int cid = a.sa_any ? a.sa[center] : 0;
-    const bool use_sa = cid != 0;
-    Hom Hm = homography(a, s, pl);
-    float ptx, pty;
-    project(Hm, (float)px, (float)py, ptx, pty);
-    if (ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f) return APD_COST_MAX;
-    if (a.weak[center] != APD_WEAK) return 0.0f;
-    const SrcTex<F16> Q(a, s);
-    const APD_G short2 *anc = a.anchors + (size_t)a.amap[center] * 9;
-    float sc[9];
-    int ns = 0;
-    float center_cost = 0.0f, strong_weight = 0.0f;
-    for (int k = 0; k < 9; ++k) {
-        short2 ap = anc[k];
-        int ax = ap.x, ay = ap.y;
-        if (ax == -1 || ay == -1) continue;
-        if (use_sa && sa_at(a, ax, ay) != cid) continue;
-        float asx, asy;
-        project(Hm, (float)ax, (float)ay, asx, asy);
-        if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) {
-            if (k != 0) {
-                if ((a.sel[ax + ay * W] >> (s - 1)) & 1u) {
-#pragma unroll
-                    for (int t = 0; t < 9; ++t) if (t == ns) sc[t] = APD_COST_MAX;
-                    ns++;
-                    strong_weight += 1.0f;
-                }
-                continue;
-            }
-            return APD_COST_MAX;
-        }
-        const int inc = (k == 0) ? 2 : 5;
-        float sr = 0.0f, srr = 0.0f, ss = 0.0f, sss = 0.0f, srs = 0.0f, wsum = 0.0f;
-        for (int i = -5; i <= 5; i += inc) {
-            const float x = (float)(ax + i);
-            const float cx = fmaf(Hm.h[0], x, Hm.h[2]);
-            const float cy = fmaf(Hm.h[3], x, Hm.h[5]);
-            const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
-            for (int j = -5; j <= 5; j += inc) {
-                int rx = ax + i, ry = ay + j;
-                if (use_sa && sa_at(a, rx, ry) != cid) continue;
-                float r = tex_ref(a, rx, ry);
-                const float y = (float)ry;
-                float X = fmaf(Hm.h[1], y, cx);
-                float Y = fmaf(Hm.h[4], y, cy);
-                float Z = fmaf(Hm.h[7], y, cz);
-                float iz = 1.0f / Z;
-                float v = sample_src(Q, W, H, X * iz, Y * iz);
-                sr += r; srr = fmaf(r, r, srr);
-                ss += v; sss = fmaf(v, v, sss);
-                srs = fmaf(r, v, srs);
-                wsum += 1.0f;
-            }
-        }
-        if (wsum == 0.0f) continue;
-        float c = ncc_finalize(sr, srr, ss, sss, srs, wsum);
-        if (k == 0) {
-            center_cost = c;
-        } else {
-#pragma unroll
-            for (int t = 0; t < 9; ++t) if (t == ns) sc[t] = c;
-            ns++;
-            strong_weight += 1.0f;
-        }
-    }
-    if (strong_weight <= 1e-6f) return center_cost;
-    // Softmax over the anchor costs, then the focal-weighted mean (APD.cu:576-586)
-    float mx = -1e10f;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) if (t < ns && sc[t] > mx) mx = sc[t];
-    float e[9];
-    float sum = 0.0f;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-        if (t < ns) { e[t] = d_expf(sc[t] - mx); sum += e[t]; }
-    }
-    float acc = 0.0f;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-        if (t < ns) { float w = e[t] / sum; acc = fmaf(w, sc[t], acc); }
-    }
-    acc = (acc > APD_COST_MAX) ? APD_COST_MAX : acc;
-    return (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
-}
 
 // ComputeGeomConsistencyCost (APD.cu:865-902)
 __device__ __forceinline__ float geom_cost(const Args &a, int px, int py, int s, float4 pl) {

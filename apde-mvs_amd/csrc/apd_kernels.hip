@@ -35,12 +35,17 @@ using namespace apd;
 // phase; LANE_STAT / APD_ANCHOR_STATS at APD_INSTR + their slot; read with apd_profile_counters(ctx, c, 64))
 #define APD_PROF_SLOTS 64
 #define APD_INSTR 32
+// Each slot has APD_PROF_SPREAD copies (workgroup index modulo the spread picks one; the host sums
+// them): a few million per-wave atomics on one address per launch serialise in L2 and cost the
+// profiled C3 step ~10 ms.
+#define APD_PROF_SPREAD 64
+#define PROF_AT(ev, k) ((ev) + (k) + APD_PROF_SLOTS * (blockIdx.x & (APD_PROF_SPREAD - 1)))
 #ifdef APD_PHASE_STAMPS
 #define PHASE_STAMP(i)                                                                       \
     do {                                                                                     \
         if (a.evals && threadIdx.x == 0) {                                                   \
             const long long t_ = clock64();                                                  \
-            atomicAdd(a.evals + APD_INSTR + 8 + (i), (unsigned long long)(t_ - t_phase_));    \
+            atomicAdd(PROF_AT(a.evals, APD_INSTR + 8 + (i)), (unsigned long long)(t_ - t_phase_)); \
             t_phase_ = t_;                                                                   \
         }                                                                                    \
     } while (0)
@@ -50,8 +55,8 @@ using namespace apd;
     do {                                                                                     \
         const unsigned long long b_ = __ballot(pred);                                        \
         if (a.evals && b_ && (threadIdx.x & 63) == 0) {                                      \
-            atomicAdd(a.evals + APD_INSTR + (slot), 1ull);                                   \
-            atomicAdd(a.evals + APD_INSTR + (slot) + 1, (unsigned long long)__builtin_popcountll(b_)); \
+            atomicAdd(PROF_AT(a.evals, APD_INSTR + (slot)), 1ull);                            \
+            atomicAdd(PROF_AT(a.evals, APD_INSTR + (slot) + 1), (unsigned long long)__builtin_popcountll(b_)); \
         }                                                                                    \
     } while (0)
 #else
@@ -75,32 +80,8 @@ struct Group {
     unsigned long long gmask;
 };
 
-__device__ __forceinline__ Group make_group(int N, int count, int wave) {
-    Group G;
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int P = WAVE / N;
-    int g = lane / N;
-    const bool lane_ok = g < P;
-    int v = lane - g * N;
-    if (!lane_ok) { g = 0; v = (lane - P * N) % N; }  // spare lanes mirror group 0, never write
-    G.v = v;
-    G.base = g * N;
-    G.slot = g;
-    G.li = wave * P + g;
-    G.valid = lane_ok && G.li < count;
-    if (G.li >= count) G.li = count - 1;
-    G.gmask = (N >= 64) ? ~0ull : ((1ull << N) - 1ull);
-    return G;
-}
-// Dynamic LDS of the view-group kernels: per wavefront slot, per pixel of the wave, 36 floats of
-// reference window (RefWin) [+ 61 floats of DepthToWeak cost curve].
+// Dynamic LDS of the view-major kernels.
 extern __shared__ float apd_dyn_lds[];
-__device__ __forceinline__ float *lds_slot(const Group &G, int P, int floats_per_px, int base_floats) {
-    return apd_dyn_lds + base_floats + ((threadIdx.x >> 6) * P + G.slot) * floats_per_px;
-}
-static inline size_t group_lds_bytes(int N, int floats_per_px) {
-    return (size_t)(BLOCK / WAVE) * (WAVE / N) * floats_per_px * sizeof(float);
-}
 // position of the r-th (0-based) set bit of m (m has more than r set bits)
 __device__ __forceinline__ int nth_set_bit(uint64_t m, int r) {
     int pos = 0;
@@ -527,8 +508,8 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
                     }
 #ifdef APD_ANCHOR_STATS  // measurement build: steps, the attempt that succeeded, wave-level steps
                     if (a.evals) {
-                        atomicAdd(a.evals + APD_INSTR + 20 + (used == 4 && !((dvalid >> di) & 1u) ? 4 : used - 1), 1ull);
-                        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(true))) atomicAdd(a.evals + APD_INSTR + 25, 1ull);
+                        atomicAdd(PROF_AT(a.evals, APD_INSTR + 20 + (used == 4 && !((dvalid >> di) & 1u) ? 4 : used - 1)), 1ull);
+                        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(true))) atomicAdd(PROF_AT(a.evals, APD_INSTR + 25), 1ull);
                     }
 #endif
                     g.n = n0 + 4u * (uint32_t)used;
@@ -681,81 +662,6 @@ __global__ __launch_bounds__(BLOCK) void k_ransac_fit(Args a, int iter) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// RandomInitialization (APD.cu:919-948) + ComputeMultiViewInitialCostandSelectedViews (723-774)
-// ---------------------------------------------------------------------------------------------
-template <bool F16>
-__global__ __launch_bounds__(BLOCK) void k_random_init(Args a) {
-    const int N = a.N;
-    const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
-    const int P = WAVE / N;
-    if (wave * P >= a.HW) return;
-    const Group G = make_group(N, a.HW, wave);
-    const int c = G.li;
-    const int py = c / a.W, px = c - py * a.W;
-    const APD_C Cam &cam = a.cams[0];
-    float4 pl;
-    if (a.state == APD_FIRST_INIT) {
-        Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_INIT);
-        float depth = g.uniform() * (a.dmax - a.dmin) + a.dmin;
-        pl = random_normal(cam, px, py, g, depth);
-        pl.w = dist2origin(cam, px, py, depth, pl);
-    } else {
-        pl = to_ref(cam, a.plane[c]);
-        float depth = pl.w;
-        pl.w = dist2origin(cam, px, py, depth, pl);
-    }
-    const bool use_new = a.use_apd && a.weak[c] == APD_WEAK;
-    const int s = G.v + 1;
-    float cv;
-    if (use_new) {
-        cv = ncc_new<F16>(a.self, px, py, s, pl);
-    } else {
-        RefWin rw;
-        build_refwin(a, px, py, lds_slot(G, WAVE / N, 36, 0), G.v, N, rw);
-        cv = ncc_old<F16>(a, px, py, s, pl, rw);
-    }
-    // stable top-k of the N costs (insertion sort, APD.cu:3-12, 754-769)
-    const int topk_max = 4;
-    float t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-    int nt = 0, nvalid = 0;
-    for (int k = 0; k < N; ++k) {
-        const float x = __shfl(cv, G.base + k);
-        if (x < APD_COST_MAX) nvalid++;
-        // position = number of kept values <= x
-        int p = (nt > 0 && t0 <= x) + (nt > 1 && t1 <= x) + (nt > 2 && t2 <= x) + (nt > 3 && t3 <= x);
-        if (p < topk_max) {
-            if (p <= 2) t3 = t2;
-            if (p <= 1) t2 = t1;
-            if (p <= 0) t1 = t0;
-            if (p == 0) t0 = x;
-            else if (p == 1) t1 = x;
-            else if (p == 2) t2 = x;
-            else t3 = x;
-            if (nt < topk_max) nt++;
-        }
-    }
-    const int top_k = min(nvalid, a.top_k);
-    const float thr = top_k <= 1 ? t0 : (top_k == 2 ? t1 : (top_k == 3 ? t2 : t3));
-    const uint32_t bits = group_bits(cv <= thr, G);
-    if (G.valid && G.v == 0) {
-        float cost_out = APD_COST_MAX;
-        uint32_t sv = 0;
-        if (top_k > 0) {
-            float sum = 0.0f;
-            sum += t0;
-            if (top_k > 1) sum += t1;
-            if (top_k > 2) sum += t2;
-            if (top_k > 3) sum += t3;
-            cost_out = sum / (float)top_k;
-            sv = bits;
-        }
-        a.plane[c] = pl;
-        a.cost[c] = cost_out;
-        a.sel_next[c] = sv;  // launch-start snapshot semantics (oracle k_random_init)
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
 // shared pieces of the two checkerboard sweeps
 // ---------------------------------------------------------------------------------------------
 // Multi-hypothesis joint view selection (APD.cu:1339-1374 / 1505-1540) for the lane's view.
@@ -856,209 +762,6 @@ __device__ __forceinline__ Cands refine_candidates(const Args &a, int px, int py
 __device__ __forceinline__ float4 candidate(const Cands &C, int k, float4 cur0, float d0, float &dk) {
     dk = (k == 0 || k == 2) ? C.drand : (k == 4 ? C.dpert : d0);
     return (k == 0 || k == 4) ? cur0 : (k == 3 ? C.npert : C.nrand);
-}
-
-// ---------------------------------------------------------------------------------------------
-// CheckerboardPropagationStrong + PlaneHypothesisRefinementStrong (APD.cu:1098-1440, 950-1006)
-// ---------------------------------------------------------------------------------------------
-template <bool F16>
-__global__ __launch_bounds__(BLOCK, APD_SWEEP_WAVES) void k_sweep_strong(Args a, const int *__restrict__ list, int count, int iter) {
-    const int N = a.N, W = a.W, H = a.H;
-    const int wave = xcd_remap(blockIdx.x, gridDim.x) * (BLOCK / WAVE) + (threadIdx.x >> 6);
-    if (wave * (WAVE / N) >= count) return;
-    const Group G = make_group(N, count, wave);
-    const int c = list[G.li];
-    const int py = c / W, px = c - py * W;
-    const int s = G.v + 1;
-    const APD_C Cam &cam0 = a.cams[0];
-    const APD_G float *__restrict__ cost = a.cost;
-
-    // adaptive checkerboard neighbour selection (APD.cu:1127-1316); identical in every lane
-    int pos[8];
-    bool flag[8];
-    {
-        float cmin;
-        int cminp;
-        int up_near = c - W, up_far = c - 3 * W, down_near = c + W, down_far = c + 3 * W;
-        int left_near = c - 1, left_far = c - 3, right_near = c + 1, right_far = c + 3;
-        flag[1] = py > 2;
-        if (flag[1]) {
-            cmin = cost[up_far]; cminp = up_far;
-            for (int i = 1; i < 11; ++i)
-                if (py > 2 + 2 * i) { int t = up_far - 2 * i * W; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
-            up_far = cminp;
-        }
-        flag[3] = py < H - 3;
-        if (flag[3]) {
-            cmin = cost[down_far]; cminp = down_far;
-            for (int i = 1; i < 11; ++i)
-                if (py < H - 3 - 2 * i) { int t = down_far + 2 * i * W; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
-            down_far = cminp;
-        }
-        flag[5] = px > 2;
-        if (flag[5]) {
-            cmin = cost[left_far]; cminp = left_far;
-            for (int i = 1; i < 11; ++i)
-                if (px > 2 + 2 * i) { int t = left_far - 2 * i; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
-            left_far = cminp;
-        }
-        flag[7] = px < W - 3;
-        if (flag[7]) {
-            cmin = cost[right_far]; cminp = right_far;
-            for (int i = 1; i < 11; ++i)
-                if (px < W - 3 - 2 * i) { int t = right_far + 2 * i; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
-            right_far = cminp;
-        }
-        flag[0] = py > 0;
-        if (flag[0]) {
-            cmin = cost[up_near]; cminp = up_near;
-            for (int i = 0; i < 3; ++i) {
-                if (py > 1 + i && px > i) { int t = up_near - (1 + i) * W - (i + 1); float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
-                if (py > 1 + i && px < W - 1 - i) { int t = up_near - (1 + i) * W + (i + 1); float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
-            }
-            up_near = cminp;
-        }
-        flag[2] = py < H - 1;
-        if (flag[2]) {
-            cmin = cost[down_near]; cminp = down_near;
-            for (int i = 0; i < 3; ++i) {
-                if (py < H - 2 - i && px > i) { int t = down_near + (1 + i) * W - (i + 1); float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
-                if (py < H - 2 - i && px < W - 1 - i) { int t = down_near + (1 + i) * W + (i + 1); float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
-            }
-            down_near = cminp;
-        }
-        flag[4] = px > 0;
-        if (flag[4]) {
-            cmin = cost[left_near]; cminp = left_near;
-            for (int i = 0; i < 3; ++i) {
-                if (px > 1 + i && py > i) { int t = left_near - (1 + i) - (i + 1) * W; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
-                if (px > 1 + i && py < H - 1 - i) { int t = left_near - (1 + i) + (i + 1) * W; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
-            }
-            left_near = cminp;
-        }
-        flag[6] = px < W - 1;
-        if (flag[6]) {
-            cmin = cost[right_near]; cminp = right_near;
-            for (int i = 0; i < 3; ++i) {
-                if (px < W - 2 - i && py > i) { int t = right_near + (1 + i) - (i + 1) * W; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
-                if (px < W - 2 - i && py < H - 1 - i) { int t = right_near + (1 + i) + (i + 1) * W; float v = cost[t]; if (v < cmin) { cmin = v; cminp = t; } }
-            }
-            right_near = cminp;
-        }
-        pos[0] = up_near; pos[1] = up_far; pos[2] = down_near; pos[3] = down_far;
-        pos[4] = left_near; pos[5] = left_far; pos[6] = right_near; pos[7] = right_far;
-    }
-
-    RefWin rw;
-    build_refwin(a, px, py, lds_slot(G, WAVE / N, 36, 0), G.v, N, rw);
-    const bool geom_imp = a.geom && a.impetus;
-    const float gf = a.gf;
-    const float4 cur = a.plane[c];
-
-    // hypotheses 0..7 = propagated planes, 8 = current plane (cost_now)
-    float ca[8];
-    float cv_now = 0.0f;
-#pragma unroll 1
-    for (int h = 0; h < 9; ++h) {
-        int ph = pos[0];
-        bool fh = flag[0];
-#pragma unroll
-        for (int k = 1; k < 8; ++k) if (h == k) { ph = pos[k]; fh = flag[k]; }
-        if (h == 8) fh = true;
-        float val = (h == 0 && G.v == 0) ? 2.0f : 0.0f;  // float cost_array[8][32] = {2.0f} (APD.cu:1120)
-        if (fh) {
-            const float4 pl = (h == 8) ? cur : a.plane[ph];
-            val = ncc_old<F16>(a, px, py, s, pl, rw);
-            if (h == 8 && geom_imp) val = fmaf(gf, geom_cost(a, px, py, s, pl), val);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) if (h == k) ca[k] = val;
-        if (h == 8) cv_now = val;
-    }
-
-    // view selection priors from the 4 direct neighbours (APD.cu:1323-1337)
-    float prior = 0.0f;
-    {
-        const int nb[4] = {c - W, c + W, c - 1, c + 1};
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (flag[2 * i]) prior += ((a.sel[nb[i]] >> G.v) & 1u) ? 0.9f : 0.1f;
-    }
-    Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ord_strong(iter));
-    const int w = view_selection(ca, prior, iter, g, G, N);
-    const uint32_t tsel = group_bits(w > 0, G);
-
-    // weighted hypothesis costs (APD.cu:1388-1399), weight_norm, cost_now (1401-1413)
-    float fc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    float wn = 0.0f, cost_now = 0.0f;
-    for (int k = 0; k < N; ++k) {
-        const int wk = __shfl(w, G.base + k);
-        const float fwk = (float)wk;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float ck = __shfl(ca[j], G.base + k);
-            if (wk > 0) fc[j] = fmaf(fwk, ck, fc[j]);
-        }
-        if (wk > 0) wn += fwk;
-        cost_now = fmaf(fwk, __shfl(cv_now, G.base + k), cost_now);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fc[j] /= wn;
-    cost_now /= wn;
-    const float cost_init = cost_now;
-    int mi = 0;
-    {
-        float m = fc[0];
-#pragma unroll
-        for (int j = 1; j < 8; ++j) if (fc[j] <= m) { m = fc[j]; mi = j; }
-    }
-    float depth_now = depth_from_plane(cam0, cur, px, py);
-    float4 pnow = cur;
-    {
-        int pm = pos[0];
-        bool fm = flag[0];
-        float fcm = fc[0];
-#pragma unroll
-        for (int k = 1; k < 8; ++k) if (mi == k) { pm = pos[k]; fm = flag[k]; fcm = fc[k]; }
-        if (fm) {
-            const float4 cand = a.plane[pm];
-            const float db = depth_from_plane(cam0, cand, px, py);
-            if (db >= a.dmin && db <= a.dmax && fcm < cost_now) {
-                depth_now = db; pnow = cand; cost_now = fcm;
-                if (G.valid && G.v == 0) a.sel[c] = tsel;
-            }
-        }
-    }
-
-    // PlaneHypothesisRefinementStrong (APD.cu:950-1006)
-    const Cands C = refine_candidates(a, px, py, g, pnow, depth_now);
-    const float4 cur0 = pnow;
-    const float d0 = depth_now;
-#pragma unroll 1
-    for (int k = 0; k < 5; ++k) {
-        float dk;
-        float4 t = candidate(C, k, cur0, d0, dk);
-        t.w = dist2origin(cam0, px, py, dk, t);
-        float cv = ncc_old<F16>(a, px, py, s, t, rw);
-        if (geom_imp) cv = fmaf(gf, geom_cost(a, px, py, s, t), cv);
-        float tc = 0.0f;
-        for (int kk = 0; kk < N; ++kk) tc = fmaf((float)__shfl(w, G.base + kk), __shfl(cv, G.base + kk), tc);
-        tc /= wn;
-        const float db = depth_from_plane(cam0, t, px, py);
-        if (db >= a.dmin && db <= a.dmax && tc < cost_now) { depth_now = db; pnow = t; cost_now = tc; }
-    }
-    if (G.valid) {
-        a.vw[(size_t)G.v * a.HW + c] = (uint8_t)w;
-        if (G.v == 0) {
-            if (a.state == APD_REFINE_INIT) {
-                if ((double)cost_now < (double)cost_init - 0.1) { a.cost[c] = cost_now; a.plane[c] = pnow; }
-                else a.cost[c] = cost_init;
-            } else {
-                a.cost[c] = cost_now;
-                a.plane[c] = pnow;
-            }
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1489,7 +1192,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
         uint32_t sum = issued;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-        if (lane == 0) atomicAdd(a.evals, (unsigned long long)sum);
+        if (lane == 0) atomicAdd(PROF_AT(a.evals, 0), (unsigned long long)sum);
     }
 
     // ---- P4: weighted candidate costs in view order, acceptance, writes
@@ -1549,6 +1252,7 @@ struct WvRefT {
     typename std::conditional<F16, _Float16, float>::type rref[108 * VM_P];
     uint16_t tmask[8 * VM_P];
     uint8_t wsum[9 * VM_P];      // valid taps per window (<= 36)
+    uint32_t box[2 * VM_P];      // bounding box of the anchors 0..8 (x0 | y0 << 16, x1 | y1 << 16)
 };
 // the Weak sweep's per-workgroup state: the reference side plus the hypotheses and per-pixel state
 template <bool F16>
@@ -1562,11 +1266,11 @@ struct WvLdsT : WvRefT<F16> {
     int pxy[VM_P];               // packed (x, y) of pixel slot p (P5's packed items)
 };
 #define WV_CAND(L) ((L).hyp)
-// 52.2 KiB with the cost table at N = 8 (fp16 reference taps): three workgroups per CU.
-static_assert(sizeof(WvLdsT<true>) + 9 * 8 * VM_P * sizeof(float) + 8 * VM_P <= 53 * 1024,
+// 53.2 KiB with the 9-slot cost table at N = 8 (fp16 reference taps): three workgroups per CU.
+static_assert(sizeof(WvLdsT<true>) + 9 * 8 * VM_P * sizeof(float) + 8 * VM_P <= 160 * 1024 / 3,
               "k_sweep_weak_vm at N = 8 must fit three workgroups per CU (160 KiB LDS)");
-// `direct` (k_weak_cand_vm handled every pixel, no SA masks): the sweep reads the anchor candidates'
-// costs from k_weak_cand_vm's buffer in P2 and its table holds [5][N][64] (current plane, fit plane,
+// `direct` (the pair-table kernels handled every pixel): the sweep reads the anchor candidates'
+// costs from their buffer in P2 and its table holds [5][N][64] (current plane, fit plane,
 // refinement candidates) instead of [9][N][64]: 48 KiB at N = 10, three workgroups per CU instead of two.
 template <bool F16>
 static inline size_t wv_lds_bytes(int N, bool direct = false) {
@@ -1686,58 +1390,6 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const typename std
     if (sm && live && !fast) ncc_new_window_slow<F16, NW, INC>(a, rb, rs, mask, Hm, ax, ay, Q, ss, sss, srs);
 }
 
-// Two 3x3 anchor windows (INC 5) with all 18 gathers in flight before the first is consumed: the
-// fast-tap statements of ncc_new_window<F16, 3, 5> for each window, lanes f0 / f1 only (the rest of
-// each window's lanes take ncc_new_window_slow). Compact taps keep the pair at 72 VGPRs of tap state.
-template <bool F16>
-__device__ __forceinline__ void ncc_new_window_pair(const typename std::conditional<F16, _Float16, float>::type *rb0,
-                                                    const typename std::conditional<F16, _Float16, float>::type *rb1,
-                                                    int rs, uint32_t m0, uint32_t m1, const Hom &Hm, int ax0, int ay0,
-                                                    int ax1, int ay1, bool f0, bool f1, const FastTex<F16, true> &T,
-                                                    float (&s0)[3], float (&s1)[3]) {
-    using TT = FastTex<F16, true>;
-    typename TT::CTap t0[9], t1[9];
-    typename TT::Raw q0[9], q1[9];
-    auto taps = [&](int ax, int ay, typename TT::CTap *t) {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const float x = (float)(ax - 5 + 5 * i);
-            const apd_f2 cxy = {fmaf(Hm.h[0], x, Hm.h[2]), fmaf(Hm.h[3], x, Hm.h[5])};
-            const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const float y = (float)(ay - 5 + 5 * j);
-                const apd_f2 XY = pk_fma((apd_f2){Hm.h[1], Hm.h[4]}, (apd_f2){y, y}, cxy);
-                t[i * 3 + j] = T.ctap(XY, rcp_newton(fmaf(Hm.h[7], y, cz)));
-            }
-        }
-    };
-    auto consume = [&](const typename TT::CTap *t, const typename TT::Raw *q, uint32_t m,
-                       const typename std::conditional<F16, _Float16, float>::type *rb, float (&sa)[3]) {
-#pragma unroll
-        for (int tk = 0; tk < 9; ++tk) {
-            const float v = T.cfinish(t[tk], q[tk]);
-            if ((m >> tk) & 1u) {
-                const float r = rb[tk * rs];
-                sa[0] += v;
-                sa[1] = fmaf(v, v, sa[1]);
-                sa[2] = fmaf(r, v, sa[2]);
-            }
-        }
-    };
-    if (f0) {
-        taps(ax0, ay0, t0);
-#pragma unroll
-        for (int k = 0; k < 9; ++k) q0[k] = T.cload(t0[k]);
-    }
-    if (f1) {
-        taps(ax1, ay1, t1);
-#pragma unroll
-        for (int k = 0; k < 9; ++k) q1[k] = T.cload(t1[k]);
-    }
-    if (f0) consume(t0, q0, m0, rb0, s0);
-    if (f1) consume(t1, q1, m1, rb1, s1);
-}
 
 // NCC-New reference side of pixel slot p (APD.cu:448-575): the 9 windows' reference taps, SA tap
 // masks and moments; wave w builds windows w, w + nwaves, ... (tap order = the reference's). Each
@@ -1805,7 +1457,10 @@ __device__ __forceinline__ void wv_build_windows(const Args &a, WvRefT<F16> &L, 
 // `want` = the lane evaluates this task. Same operations, in the same order, as ncc_new. `seldep`
 // (optional) is set when the result read an anchor's selected views (a window anchor projected out
 // of the source image, APD.cu:510-520), the one input the Strong sweep changes between launches.
-template <bool F16>
+// SA = false: no SA masks in this problem, so every window's tap mask is full (compile-time constant:
+// no per-tap mask selects). BOX: L.box holds the pixel's anchor bounding box, and one
+// window_rcp_ok_box over it (taps included) stands for the per-window checks when it holds.
+template <bool F16, bool SA = true, bool BOX = false>
 __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L, int p, int px, int py, int s, float4 pl,
                                             bool want, bool *seldep = nullptr, uint32_t *nwc = nullptr,
                                             uint32_t *nwa = nullptr) {
@@ -1821,12 +1476,22 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
     int ns = 0;
     float center_cost = 0.0f, strong_weight = 0.0f;
     bool dead = !alive;  // COST_MAX (centre or centre-anchor projected out of the image)
-#ifndef WV_PAIR_WINDOWS  // (A/B: the anchor windows one at a time / in pairs)
+    bool box_ok = false;
+    if constexpr (BOX) {
+        const uint32_t b0 = L.box[p], b1 = L.box[VM_P + p];
+        box_ok = alive && window_rcp_ok_box(Hm, (float)((int)(b0 & 0xFFFFu) - 5), (float)((int)(b0 >> 16) - 5),
+                                            (float)((int)(b1 & 0xFFFFu) + 5), (float)((int)(b1 >> 16) + 5));
+    }
 #pragma unroll 1
     for (int k = 0; k < 9; ++k) {
         const int pk = L.anc[k * VM_P + p];
         const bool has = alive && pk >= 0 && ((awin >> k) & 1u);
+#ifdef APD_ABLATE_ANCHOR_LOCAL  // timing-only (wrong values): anchor windows k >= 1 next to the pixel
+        const int ax = has ? (k == 0 ? (pk & 0xFFFF) : min(max(px + 6 * (((k - 1) % 3) - 1), 0), W - 1)) : px;
+        const int ay = has ? (k == 0 ? (pk >> 16) : min(max(py + 6 * (((k - 1) / 3) - 1), 0), H - 1)) : py;
+#else
         const int ax = has ? (pk & 0xFFFF) : px, ay = has ? (pk >> 16) : py;
+#endif
         bool live = has;
         if (has) {
             float asx, asy;
@@ -1848,13 +1513,15 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
             }
         }
         if (!__ballot(live)) continue;
-        const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
+        bool fast = live && box_ok;
+        if (!BOX || __ballot(live && !box_ok))
+            if (live && !box_ok) fast = window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
         float ss = 0.0f, sss = 0.0f, srs = 0.0f;
         if (k == 0)
-            ncc_new_window<F16, 6, 2>(a, &L.rref[p], VM_P, L.tmask0[p], Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            ncc_new_window<F16, 6, 2>(a, &L.rref[p], VM_P, SA ? L.tmask0[p] : ~0ull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
         else
-            ncc_new_window<F16, 3, 5>(a, &L.rref[(36 + 9 * (k - 1)) * VM_P + p], VM_P, (uint64_t)L.tmask[(k - 1) * VM_P + p], Hm, ax, ay,
-                                      live, fast, T, Q, ss, sss, srs);
+            ncc_new_window<F16, 3, 5>(a, &L.rref[(36 + 9 * (k - 1)) * VM_P + p], VM_P,
+                                      SA ? (uint64_t)L.tmask[(k - 1) * VM_P + p] : 0x1FFull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
         if (!live) continue;
         if (nwc) { if (k == 0) ++*nwc; else ++*nwa; }  // (profiling: windows evaluated)
         const float wsum = (float)L.wsum[k * VM_P + p];
@@ -1869,90 +1536,6 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
             strong_weight += 1.0f;
         }
     }
-#else
-    // The window states in the reference's k order (APD.cu:488-571): evaluated (livem), an
-    // out-of-frame COST_MAX entry (maxm), or absent. Anchor 0 out of frame kills the pixel first.
-    uint32_t livem = 0, maxm = 0;
-#pragma unroll 1
-    for (int k = 0; k < 9; ++k) {
-        const int pk = L.anc[k * VM_P + p];
-        if (!(alive && pk >= 0 && ((awin >> k) & 1u))) continue;
-        const int ax = pk & 0xFFFF, ay = pk >> 16;
-        float asx, asy;
-        project(Hm, (float)ax, (float)ay, asx, asy);
-        if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) {
-            if (k != 0) {
-                if (seldep) *seldep = true;
-                if ((a.sel[ax + ay * W] >> (s - 1)) & 1u) maxm |= 1u << k;
-            } else {
-                dead = true;
-                alive = false;
-            }
-        } else {
-            livem |= 1u << k;
-        }
-    }
-    const bool live0 = livem & 1u;
-    if (__ballot(live0)) {  // the centre window (6x6, step 2)
-        const int pk = L.anc[p];
-        const int ax = live0 ? (pk & 0xFFFF) : px, ay = live0 ? (pk >> 16) : py;
-        const bool fast = live0 && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
-        float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-        ncc_new_window<F16, 6, 2>(a, &L.rref[p], VM_P, L.tmask0[p], Hm, ax, ay, live0, fast, T, Q, ss, sss, srs);
-        if (live0) {
-            if (nwc) ++*nwc;
-            const float wsum = (float)L.wsum[p];
-            if (wsum != 0.0f) center_cost = ncc_finalize(L.wsr[p], L.wsrr[p], ss, sss, srs, wsum);
-        }
-    }
-    // the anchor windows two at a time (18 gathers in flight), entries appended in k order
-#pragma unroll 1
-    for (int k = 1; k < 9; k += 2) {
-        const bool l0 = (livem >> k) & 1u, l1 = (livem >> (k + 1)) & 1u;
-        float c0 = 0.0f, c1 = 0.0f;
-        bool e0 = false, e1 = false;
-        if (__ballot(l0 || l1)) {
-            const int pk0 = L.anc[k * VM_P + p], pk1 = L.anc[(k + 1) * VM_P + p];
-            const int ax0 = l0 ? (pk0 & 0xFFFF) : px, ay0 = l0 ? (pk0 >> 16) : py;
-            const int ax1 = l1 ? (pk1 & 0xFFFF) : px, ay1 = l1 ? (pk1 >> 16) : py;
-            const bool f0 = l0 && window_rcp_ok(Hm, (float)(ax0 - 5), (float)(ay0 - 5));
-            const bool f1 = l1 && window_rcp_ok(Hm, (float)(ax1 - 5), (float)(ay1 - 5));
-            const auto *rb0 = &L.rref[(36 + 9 * (k - 1)) * VM_P + p], *rb1 = rb0 + 9 * VM_P;
-            const uint32_t m0 = L.tmask[(k - 1) * VM_P + p], m1 = L.tmask[k * VM_P + p];
-            float s0[3] = {0.0f, 0.0f, 0.0f}, s1[3] = {0.0f, 0.0f, 0.0f};
-            ncc_new_window_pair<F16>(rb0, rb1, VM_P, m0, m1, Hm, ax0, ay0, ax1, ay1, f0, f1, T, s0, s1);
-            if (__ballot((l0 && !f0) || (l1 && !f1))) {
-                if (l0 && !f0) ncc_new_window_slow<F16, 3, 5>(a, rb0, VM_P, m0, Hm, ax0, ay0, Q, s0[0], s0[1], s0[2]);
-                if (l1 && !f1) ncc_new_window_slow<F16, 3, 5>(a, rb1, VM_P, m1, Hm, ax1, ay1, Q, s1[0], s1[1], s1[2]);
-            }
-            if (l0) {
-                if (nwa) ++*nwa;
-                const float wsum = (float)L.wsum[k * VM_P + p];
-                if (wsum != 0.0f) { c0 = ncc_finalize(L.wsr[k * VM_P + p], L.wsrr[k * VM_P + p], s0[0], s0[1], s0[2], wsum); e0 = true; }
-            }
-            if (l1) {
-                if (nwa) ++*nwa;
-                const float wsum = (float)L.wsum[(k + 1) * VM_P + p];
-                if (wsum != 0.0f) { c1 = ncc_finalize(L.wsr[(k + 1) * VM_P + p], L.wsrr[(k + 1) * VM_P + p], s1[0], s1[1], s1[2], wsum); e1 = true; }
-            }
-        }
-        const bool x0 = (maxm >> k) & 1u, x1 = (maxm >> (k + 1)) & 1u;
-        if (x0 || e0) {
-            const float c = x0 ? APD_COST_MAX : c0;
-#pragma unroll
-            for (int t = 0; t < 9; ++t) if (t == ns) sc[t] = c;
-            ns++;
-            strong_weight += 1.0f;
-        }
-        if (x1 || e1) {
-            const float c = x1 ? APD_COST_MAX : c1;
-#pragma unroll
-            for (int t = 0; t < 9; ++t) if (t == ns) sc[t] = c;
-            ns++;
-            strong_weight += 1.0f;
-        }
-    }
-#endif
     if (dead) return APD_COST_MAX;
     if (strong_weight <= 1e-6f) return center_cost;
     float mx = -1e10f;
@@ -1988,16 +1571,16 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
 #define WV_P5_CHUNKS 3  // P5 batches: whole views until at least this many 64-item chunks
 #endif
 #define WV_BLOCK (WV_WAVES * WAVE)
-template <bool F16>
+template <bool F16, bool SA>
 __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
-                                                                int iter, const float *__restrict__ cand,
-                                                                const uint8_t *__restrict__ cand_done, int wc, int direct_) {
+                                                                int iter, const float *__restrict__ cand, int wc) {
     const int N = a.N, W = a.W;
     PHASE_BEGIN;
-    // direct: the candidate kernels evaluated every pixel's anchor candidates (the pair table, or
-    // k_weak_cand_vm without SA masks: no group is left to the sweep), so P2 reads their costs from
-    // `cand` and the table is [N][64] (current plane), later [5][N][64] (wv_lds_bytes)
-    const bool direct = cand != nullptr && direct_ != 0;
+    // direct: the pair-table kernels evaluated every pixel's anchor candidates, so P2 reads their
+    // costs from `cand` and the table is [N][64] (current plane), later [5][N][64] (wv_lds_bytes);
+    // without them (cand == nullptr: APD_NO_CAND_PAIRS=1 or a pair table that does not fit) P1
+    // evaluates the candidates here
+    const bool direct = cand != nullptr;
     WvLdsT<F16> &L = *reinterpret_cast<WvLdsT<F16> *>(apd_dyn_lds);
     float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64] (direct: [N][64]), later [5][N][64]
     uint8_t *wts = reinterpret_cast<uint8_t *>(costL + (direct ? 5 : 9) * N * VM_P);  // [N][64] view weights
@@ -2052,32 +1635,33 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             L.flags[p1] = hflag | (awin << 16);
             L.hyp[8 * VM_P + p1] = cur;
             L.pxy[p1] = px1 | (py1 << 16);
+            int bx0 = px1, by0 = py1, bx1 = px1, by1 = py1;  // anchors' bounding box (+ the pixel)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                if (ap[k].x == -1 || ap[k].y == -1) continue;
+                bx0 = min(bx0, (int)ap[k].x); bx1 = max(bx1, (int)ap[k].x);
+                by0 = min(by0, (int)ap[k].y); by1 = max(by1, (int)ap[k].y);
+            }
+            L.box[p1] = (uint32_t)bx0 | ((uint32_t)by0 << 16);
+            L.box[VM_P + p1] = (uint32_t)bx1 | ((uint32_t)by1 << 16);
         }
         wv_build_windows<F16>(a, L, p1, anc, cid, wave, WV_WAVES);
     }
     __syncthreads();
     PHASE_STAMP(0);
 
-    // ---- P1: (anchor hypothesis, view) tasks, lane = pixel; where k_weak_cand_vm handled this group
-    // (`cand_done`) the candidates' costs are read instead (direct: P2 reads them itself, no tasks).
-    // The current plane is evaluated after the view selection (P1b), for the views it weights only:
-    // cost_now = sum of fmaf(w_v, c_v) over all views, and a weight-0 view adds fmaf(0, c_v, .) == the
-    // sum itself (c_v finite), so its value is never needed.
+    // ---- P1 (not direct): (anchor hypothesis, view) tasks, lane = pixel. The current plane is
+    // evaluated after the view selection (P1b), for the views it weights only: cost_now = sum of
+    // fmaf(w_v, c_v) over all views, and a weight-0 view adds fmaf(0, c_v, .) == the sum itself (c_v
+    // finite), so its value is never needed.
     uint32_t nwc = 0, nwa = 0;  // profiling: centre / anchor windows this lane evaluated
-    const int wi1 = cand ? a.amap[c1] : 0;
-    const bool cand_ok = cand && pv1 && cand_done[wi1];  // per pixel (groups of k_weak_cand_vm span both colours)
     const int ntask = direct ? 0 : 8 * N;
     for (int u = wave; u < ntask; u += WV_WAVES) {  // view-major: the waves share a source image
         const int v = u / 8, h = u - 8 * v, t = h * N + v;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
         const bool want = pv1 && ((L.flags[p1] >> h) & 1u);
-        if (cand && !__ballot(want && !cand_ok)) {  // every lane that needs it has its cost
-            if (want) val = cand[((size_t)v * 8 + h) * (size_t)wc + wi1];
-            costL[t * VM_P + p1] = val;
-            continue;
-        }
         const float4 pl = L.hyp[h * VM_P + p1];
-        const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
+        const float nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
         if (want) val = nv;
         costL[t * VM_P + p1] = val;
     }
@@ -2109,7 +1693,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             if (pk >= 0) prior += ((a.sel[(pk & 0xFFFF) + (pk >> 16) * W] >> v) & 1u) ? 0.9f : 0.1f;
         }
         float ca[8];
-        if (direct) {  // the candidates' costs from k_weak_cand_vm; absent ones as P1 sets them
+        if (direct) {  // the candidates' costs from the pair-table kernels; absent ones as P1 sets them
             const size_t wi = (size_t)a.amap[c];
 #pragma unroll
             for (int h = 0; h < 8; ++h)
@@ -2137,7 +1721,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             for (int k = 0; k < 8; ++k) if (j == k) gval[k] = vv;
         }
 #ifdef APD_PHASE_STAMPS
-        if (a.evals && threadIdx.x == 0) atomicAdd(a.evals + APD_INSTR + 8 + 7, (unsigned long long)(clock64() - tg0_));
+        if (a.evals && threadIdx.x == 0) atomicAdd(PROF_AT(a.evals, APD_INSTR + 8 + 7), (unsigned long long)(clock64() - tg0_));
 #endif
         float fc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         float wn = 0.0f;
@@ -2189,7 +1773,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             if (iter == 0 && a.wcur && !__ballot(want && __builtin_isnan(kept)))
                 nv = kept;
             else
-                nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
+                nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
             if (want) {
                 val = nv;
                 if (geom) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
@@ -2278,7 +1862,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[p1];
             LANE_STAT(22, want);
             const float4 fit = fit1;
-            const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, fit, want, nullptr, &nwc, &nwa);
+            const float nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, fit, want, nullptr, &nwc, &nwa);
             if (want) {
                 cv = nv;
                 if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, fit), cv);
@@ -2376,7 +1960,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
                     const int px = pxy & 0xFFFF, py = pxy >> 16;
                     const float4 tp = WV_CAND(L)[k * VM_P + p];
                     LANE_STAT(20, want);
-                    const float nv = ncc_new_vm<F16>(a, L, p, px, py, v + 1, tp, want, nullptr, &nwc, &nwa);
+                    const float nv = ncc_new_vm<F16, SA, true>(a, L, p, px, py, v + 1, tp, want, nullptr, &nwc, &nwa);
                     if (want) {
                         float cv = nv;
                         if (geom) cv = fmaf(gf, geom_cost(a, px, py, v + 1, tp), cv);
@@ -2418,7 +2002,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[(1 + k) * VM_P + p1];
             LANE_STAT(20, want);
             const float4 tp = WV_CAND(L)[k * VM_P + p1];
-            const float nv = ncc_new_vm<F16>(a, L, p1, px1, py1, v + 1, tp, want, nullptr, &nwc, &nwa);
+            const float nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, tp, want, nullptr, &nwc, &nwa);
             if (want) {
                 cv = nv;
                 if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
@@ -2437,7 +2021,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         // for this pixel (APD.cu:1471-1482, 1577-1589, 1026-1094) whose values are used: the valid
         // anchor candidates x N views, the current plane x N, and -- when the fit plane exists -- the
         // fit plane and the 5 refinement candidates x the views with weight > 0. Counted whether the
-        // values came from k_weak_cand_vm, RandomInitialization's kept costs or this kernel.
+        // values came from the pair-table kernels, RandomInitialization's kept costs or this kernel.
         uint32_t nn = 0, ng = 0;
         if (pv1) {
             int nsel = 0;
@@ -2448,7 +2032,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) { nn += __shfl_xor(nn, o); ng += __shfl_xor(ng, o); }
-        if (lane == 0) { atomicAdd(a.evals + 1, (unsigned long long)nn); atomicAdd(a.evals + 2, (unsigned long long)ng); }
+        if (lane == 0) { atomicAdd(PROF_AT(a.evals, 1), (unsigned long long)nn); atomicAdd(PROF_AT(a.evals, 2), (unsigned long long)ng); }
     }
     if (a.evals) {  // ... plus the fit-plane and refinement evaluations every wave issued (P3, P5)
         uint32_t nn = issued_nn, ng = issued_g, wc0 = nwc, wa0 = nwa;
@@ -2458,8 +2042,8 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
             wc0 += __shfl_xor(wc0, o); wa0 += __shfl_xor(wa0, o);
         }
         if (lane == 0) {
-            atomicAdd(a.evals + 1, (unsigned long long)nn); atomicAdd(a.evals + 2, (unsigned long long)ng);
-            atomicAdd(a.evals + 7, (unsigned long long)wc0); atomicAdd(a.evals + 8, (unsigned long long)wa0);
+            atomicAdd(PROF_AT(a.evals, 1), (unsigned long long)nn); atomicAdd(PROF_AT(a.evals, 2), (unsigned long long)ng);
+            atomicAdd(PROF_AT(a.evals, 7), (unsigned long long)wc0); atomicAdd(PROF_AT(a.evals, 8), (unsigned long long)wa0);
         }
     }
 
@@ -2496,526 +2080,9 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     PHASE_STAMP(6);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Candidate costs of the Weak sweep with the anchor windows shared across pixels.
-// For a WEAK pixel, candidate h is the plane of its STRONG anchor h+1, and ComputeBilateralNCCNew
-// (APD.cu:448-593) of that plane is the centre window (at anchor 0, pixel-specific) combined by the
-// focal softmax with the 3x3 windows at anchors 1..8. An anchor window's cost is a function of
-// (window anchor, candidate plane, view, SA label) only -- the out-of-frame rule reads the
-// anchor's selected_views, which only the Strong sweep writes -- and neighbouring WEAK pixels share
-// anchors: a 64-pixel group at 3024x2016 (N = 8) holds ~1.8k distinct (window anchor, candidate
-// anchor) pairs of ~4.0k evaluations (2.2x; 2.6x at 6048x4032). This kernel evaluates every
-// distinct pair once per view, the centre windows per pixel, and writes each (candidate, view,
-// pixel) cost -- bit-identical to ncc_new_vm (same statements, same softmax order) -- for the
-// sweep's P1, which then evaluates only the current plane. With SA masks anchors are keyed by
-// (position, the pixel's label slot); a group holding more than 3 labels is left to the sweep
-// (done[group] = 0).
-//   A/B  hash the group's anchors 1..8 into distinct ids (deterministic slot order), build their
-//        3x3 reference windows and the pixels' 6x6 centre windows (wv_build_windows's statements)
-//   C    hash the (window anchor, candidate anchor) pairs, pair ids in slot order
-//   D    per view: pair windows (lane = pair), centre windows (lane = pixel), then per (candidate,
-//        pixel) the focal combination in anchor order
-// ---------------------------------------------------------------------------------------------
-#define PK_D 512    // distinct anchors per group (<= 8 per pixel)
-#define PK_P 4096   // distinct pairs per group (<= 64 per pixel)
-#define PK_AH 1024  // anchor hash slots
-#define PK_NONE 0xFFFFu
-#ifndef PK_WAVES
-#define PK_WAVES 8  // 8-wave workgroups: 2 per CU (LDS) still give 16 waves per CU
-#endif
+// k_weak_cand_g's workgroups: 8 waves, wave h = anchor candidate h
+#define PK_WAVES 8
 #define PK_BLOCK (PK_WAVES * WAVE)
-template <bool F16>
-struct PkLds {
-    using RT = typename std::conditional<F16, _Float16, float>::type;
-    union {
-        int hash[PK_P];             // C: pair key + 1 (19 bits) | pair id << 19
-        float pcost[PK_P];          // D: per-view pair cost (< 0: window absent)
-    } u;
-    uint32_t plist[PK_P];           // pair id -> window anchor id | candidate anchor id << 16
-    uint16_t pidx[64 * VM_P];       // [h * 8 + k - 1][p]: pair id of (anchor k window, candidate h)
-    RT aref[9 * PK_D];              // [tap][d] anchor window reference taps
-    float4 apl[PK_D];               // plane of anchor d (candidates)
-    int apos[PK_D];                 // packed (x, y) of anchor d
-    float asr[PK_D], asrr[PK_D];    // window moments
-    uint32_t ahash[PK_AH];          // anchor hash: pk_key + 1 (0 = empty)
-    RT cref[36 * VM_P];             // [tap][p] centre window reference taps
-    float csr[VM_P], csrr[VM_P];
-    uint64_t cmask[VM_P];           // centre window tap mask (SA)
-    union {
-        int kcnt[PK_D];             // C: pairs per window anchor, then their offsets
-        struct {
-            float ccost[8 * VM_P];  // D: [h][p] centre window cost of candidate h (per view)
-            uint8_t cstat[8 * VM_P];  // D: [h][p] bit 0 dead (centre or its anchor out of frame)
-        } d;
-    } w;
-    uint16_t aid[8 * VM_P];         // [k-1][p]: id of (anchor k, the pixel's SA label), PK_NONE if invalid
-    uint16_t amask[PK_D];           // anchor window tap mask (SA)
-    uint16_t awin[VM_P];            // bit k: window k present (anchor valid, SA label matches; APD.cu:455-470)
-    int anc0[VM_P];                 // packed anchor 0, -1 if invalid
-    uint8_t alc[PK_D], aws[PK_D];   // alc: SA label slot (bits 0-1) | anchor STRONG (bit 7)
-    uint8_t cws[VM_P];
-    uint8_t cand[VM_P];             // bit h: candidate h present (anchor h+1 valid and STRONG)
-    uint8_t plc[VM_P];              // the pixel's SA label slot
-    int gcid[4];                    // SA labels of the group (+1; 0 = free slot), at most 3
-    int ovf;                        // more than 3 SA labels: the sweep evaluates this group itself
-    int scan[PK_BLOCK / WAVE + 1];
-    int nD, nP;
-};
-static_assert(sizeof(PkLds<true>) <= 80 * 1024, "k_weak_cand_vm: two 8-wave workgroups per CU (160 KiB LDS)");
-template <bool F16>
-static inline size_t pk_lds_bytes() { return sizeof(PkLds<F16>); }
-
-// anchor keys: x | y << 15 | SA label slot << 30 (x, y < 32768), + 1 in the hash (0 = empty slot);
-// their order (the anchor ids) is raster order within a label slot
-__device__ __forceinline__ uint32_t pk_mix(uint32_t k) {
-    k ^= k >> 15;
-    k *= 0x2C1B3C6Du;
-    k ^= k >> 12;
-    return k;
-}
-// Block-wide ordered compaction of hash slots: every thread owns `per` consecutive slots; returns
-// the id of slot (tid * per + i) through ids[] (valid where the slot is used) and the total.
-template <int PER>
-__device__ __forceinline__ int pk_compact(const bool (&used)[PER], int (&ids)[PER], int *scan_lds) {
-    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid >> 6;
-    int cnt = 0;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) cnt += used[i];
-    // inclusive scan over the wave, then over the waves
-    int x = cnt;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == WAVE - 1) scan_lds[wave] = x;
-    __syncthreads();
-    int base = 0;
-    for (int w = 0; w < wave; ++w) base += scan_lds[w];
-    int total = 0;
-    for (int w = 0; w < PK_BLOCK / WAVE; ++w) total += scan_lds[w];
-    int next = base + x - cnt;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        ids[i] = next;
-        next += used[i];
-    }
-    __syncthreads();
-    return total;
-}
-
-template <bool F16>
-__global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a, const int *__restrict__ list, int count,
-                                                           float *__restrict__ out, uint8_t *__restrict__ done, int wc) {
-    PHASE_BEGIN;
-    const int N = a.N, W = a.W, H = a.H;
-    PkLds<F16> &L = *reinterpret_cast<PkLds<F16> *>(apd_dyn_lds);
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int first = blk * VM_P;
-    const int np = min(VM_P, count - first);
-    const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
-    const int p1 = lane;
-    const bool pv1 = p1 < np;
-    const int c1 = list[first + min(p1, np - 1)];
-    const int py1 = c1 / W, px1 = c1 - py1 * W;
-
-    // ---- A: SA label slots, anchors into the hash
-    for (int i = tid; i < PK_P; i += PK_BLOCK) L.u.hash[i] = 0;
-    for (int i = tid; i < PK_AH; i += PK_BLOCK) L.ahash[i] = 0;
-    if (tid < 4) L.gcid[tid] = 0;
-    if (tid == 0) L.ovf = 0;
-    __syncthreads();
-    const int cid1 = a.sa_any ? a.sa[c1] : 0;  // the pixel's label (0: no SA masking)
-    if (pv1 && wave == 0) {
-        int slot = -1;
-        for (int k = 0; k < 3 && slot < 0; ++k) {
-            const int old = atomicCAS(&L.gcid[k], 0, cid1 + 1);
-            if (old == 0 || old == cid1 + 1) slot = k;
-        }
-        if (slot < 0) L.ovf = 1;
-        L.plc[p1] = (uint8_t)max(slot, 0);
-    }
-    __syncthreads();
-    const int wi1 = a.amap[c1];  // the pixel's WEAK index: outputs are [view][candidate][WEAK index]
-    if (L.ovf) {  // uniform: the Weak sweep evaluates this group's candidates itself
-        if (pv1 && wave == 0) done[wi1] = 0;
-        return;
-    }
-    const uint32_t lc1 = L.plc[p1];
-    auto pk_key = [](int x, int y, uint32_t lc) { return (uint32_t)x | ((uint32_t)y << 15) | (lc << 30); };
-    const APD_G short2 *anc1 = a.anchors + (size_t)a.amap[c1] * 9;
-    if (pv1 && wave == 0) {
-        const short2 a0 = anc1[0];
-        L.anc0[p1] = (a0.x == -1 || a0.y == -1) ? -1 : ((int)(uint16_t)a0.x | ((int)a0.y << 16));
-    }
-    if (pv1 && wave < 2) {  // waves 0/1: anchors 1-4 / 5-8
-        for (int k = 1 + 4 * wave; k < 5 + 4 * wave; ++k) {
-            const short2 ap = anc1[k];
-            if (ap.x == -1 || ap.y == -1) continue;
-            const uint32_t key = pk_key(ap.x, ap.y, lc1) + 1u;
-            uint32_t slot = pk_mix(key) & (PK_AH - 1);
-            for (;;) {
-                const uint32_t old = atomicCAS(&L.ahash[slot], 0u, key);
-                if (old == 0u || old == key) break;
-                slot = (slot + 1) & (PK_AH - 1);
-            }
-        }
-    }
-    __syncthreads();
-    // ---- B: anchor ids in raster order of the anchors (the rank of each key), so the pairs of one
-    // window anchor, and of nearby ones, take neighbouring lanes (gather locality); their windows;
-    // the pixels' centre windows
-    {
-        constexpr int PER = PK_AH / PK_BLOCK;
-        bool used[PER];
-        int ids[PER];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) used[i] = L.ahash[tid * PER + i] != 0;
-        const int nd = pk_compact<PER>(used, ids, L.scan);
-        uint32_t *keys = L.plist;  // plist is free until C: keys[0..nd) unordered
-#pragma unroll
-        for (int i = 0; i < PER; ++i)
-            if (used[i]) keys[ids[i]] = L.ahash[tid * PER + i];
-        if (tid == 0) L.nD = nd;
-        __syncthreads();
-        // id = rank of the key among the group's keys (distinct, so ranks are a permutation):
-        // raster order without a sort network (each rank is nd broadcast LDS reads)
-        uint32_t *slot_id = keys + PK_D;
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const uint32_t key = L.ahash[tid * PER + i];
-            uint32_t id = PK_NONE;
-            if (key != 0) {
-                id = 0;
-                for (int j = 0; j < nd; ++j) id += keys[j] < key;
-            }
-            slot_id[tid * PER + i] = id;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const uint32_t key = L.ahash[tid * PER + i];
-            if (key != 0) {
-                const uint32_t k0 = key - 1u, d = slot_id[tid * PER + i];
-                L.apos[d] = (int)((k0 & 0x7FFFu) | (((k0 >> 15) & 0x7FFFu) << 16));
-                L.alc[d] = (uint8_t)(k0 >> 30);
-            }
-        }
-    }
-    __syncthreads();
-    if (pv1 && wave < 2) {
-        for (int k = 1 + 4 * wave; k < 5 + 4 * wave; ++k) {
-            const short2 ap = anc1[k];
-            uint16_t id = PK_NONE;
-            if (!(ap.x == -1 || ap.y == -1)) {
-                const uint32_t key = pk_key(ap.x, ap.y, lc1) + 1u;
-                uint32_t slot = pk_mix(key) & (PK_AH - 1);
-                while (L.ahash[slot] != key) slot = (slot + 1) & (PK_AH - 1);
-                id = (uint16_t)L.plist[PK_D + slot];
-            }
-            L.aid[(k - 1) * VM_P + p1] = id;
-        }
-    }
-    if (pv1 && wave == PK_WAVES - 1) {  // windows present (APD.cu:455-470: anchor valid and, with SA, its label matches)
-        uint32_t aw = 0;
-        for (int k = 0; k < 9; ++k) {
-            const short2 ap = anc1[k];
-            if (!(ap.x == -1 || ap.y == -1) && !(cid1 != 0 && sa_at_dev(a, ap.x, ap.y) != cid1)) aw |= 1u << k;
-        }
-        L.awin[p1] = (uint16_t)aw;
-    }
-    const int nD = L.nD;
-    for (int d = tid; d < nD; d += PK_BLOCK) {  // distinct anchor windows (wv_build_windows, k >= 1)
-        const int pk = L.apos[d];
-        const int ax = pk & 0xFFFF, ay = pk >> 16;
-        const int q = ax + ay * W;
-        const int cid = L.gcid[L.alc[d]] - 1;
-        const bool use_sa = cid != 0;
-        L.alc[d] |= (uint8_t)((a.weak[q] == APD_STRONG) << 7);
-        L.apl[d] = a.plane[q];
-        float sr = 0.0f, srr = 0.0f, ws = 0.0f;
-        uint32_t mask = 0;
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) {
-                const int rx = ax - 5 + 5 * i, ry = ay - 5 + 5 * j;
-                if (use_sa && sa_at_dev(a, rx, ry) != cid) {
-                    L.aref[(i * 3 + j) * PK_D + d] = 0.0f;
-                    continue;
-                }
-                const float r = tex_ref(a, rx, ry);
-                L.aref[(i * 3 + j) * PK_D + d] = r;
-                mask |= 1u << (i * 3 + j);
-                sr += r;
-                srr = fmaf(r, r, srr);
-                ws += 1.0f;
-            }
-        L.asr[d] = sr;
-        L.asrr[d] = srr;
-        L.aws[d] = (uint8_t)ws;
-        L.amask[d] = (uint16_t)mask;
-    }
-    if (pv1) {  // centre windows (k = 0: 6x6, step 2): taps fetched by all waves, summed below
-        const int pk = L.anc0[p1];
-        if (pk >= 0) {
-            const int ax = pk & 0xFFFF, ay = pk >> 16;
-            for (int t = wave; t < 36; t += PK_WAVES) {
-                const int i = t / 6, j = t - 6 * i;
-                const int rx = ax - 5 + 2 * i, ry = ay - 5 + 2 * j;
-                L.cref[t * VM_P + p1] = (cid1 != 0 && sa_at_dev(a, rx, ry) != cid1) ? 0.0f : tex_ref(a, rx, ry);
-            }
-        }
-    }
-    __syncthreads();
-    if (pv1 && wave == 2) {  // the moments and tap mask in wv_build_windows's tap order (texels are exact in RT)
-        float sr = 0.0f, srr = 0.0f, ws = 0.0f;
-        uint64_t mask = 0;
-        const int pk = L.anc0[p1];
-        if (pk >= 0) {
-            const int ax = pk & 0xFFFF, ay = pk >> 16;
-            for (int t = 0; t < 36; ++t) {
-                const int i = t / 6, j = t - 6 * i;
-                if (cid1 != 0 && sa_at_dev(a, ax - 5 + 2 * i, ay - 5 + 2 * j) != cid1) continue;
-                const float r = (float)L.cref[t * VM_P + p1];
-                mask |= 1ull << t;
-                sr += r;
-                srr = fmaf(r, r, srr);
-                ws += 1.0f;
-            }
-        }
-        L.csr[p1] = sr;
-        L.csrr[p1] = srr;
-        L.cws[p1] = (uint8_t)ws;
-        L.cmask[p1] = mask;
-    }
-    // ---- C: candidate bits, pairs into the hash
-    if (pv1 && wave == 3) {
-        uint32_t cb = 0;
-        for (int h = 0; h < 8; ++h) {
-            const uint16_t id = L.aid[h * VM_P + p1];
-            if (id != PK_NONE && (L.alc[id] >> 7)) cb |= 1u << h;
-        }
-        L.cand[p1] = (uint8_t)cb;
-    }
-    __syncthreads();
-    if (pv1) {
-        const uint32_t cb = L.cand[p1];
-        for (int h = wave; h < 8; h += PK_WAVES) {
-            if (!((cb >> h) & 1u)) continue;
-            const uint32_t hid = L.aid[h * VM_P + p1];
-            const uint32_t aw = L.awin[p1];
-            for (int k = 0; k < 8; ++k) {
-                const uint32_t kid = L.aid[k * VM_P + p1];
-                if (kid == PK_NONE || !((aw >> (k + 1)) & 1u)) continue;
-                const int key = (int)(kid | (hid << 9)) + 1;  // <= 2^18
-                uint32_t slot = pk_mix((uint32_t)key) & (PK_P - 1);
-                for (;;) {
-                    const int old = atomicCAS(&L.u.hash[slot], 0, key);
-                    if (old == 0 || old == key) break;
-                    slot = (slot + 1) & (PK_P - 1);
-                }
-            }
-        }
-    }
-    __syncthreads();
-    // pair ids ordered by window anchor (counting sort; the order inside one anchor's run does not
-    // matter: a pair id only labels a window cost)
-    for (int d = tid; d < PK_D; d += PK_BLOCK) L.w.kcnt[d] = 0;
-    __syncthreads();
-    {
-        constexpr int PER = PK_P / PK_BLOCK;
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int hv = L.u.hash[tid * PER + i];
-            if (hv != 0) {
-                const int r = atomicAdd(&L.w.kcnt[(hv - 1) & 511], 1);
-                L.u.hash[tid * PER + i] = hv | (r << 19);
-            }
-        }
-    }
-    __syncthreads();
-    if (wave == 0) {  // exclusive scan of the 512 anchor counts, 8 per lane
-        int c[8], sum = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) { c[i] = L.w.kcnt[lane * 8 + i]; sum += c[i]; }
-        int x = sum;
-#pragma unroll
-        for (int o = 1; o < WAVE; o <<= 1) {
-            const int y = __shfl_up(x, o);
-            if (lane >= o) x += y;
-        }
-        int off = x - sum;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) { L.w.kcnt[lane * 8 + i] = off; off += c[i]; }
-        if (lane == WAVE - 1) L.nP = x;
-    }
-    __syncthreads();
-    {
-        constexpr int PER = PK_P / PK_BLOCK;
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int hv = L.u.hash[tid * PER + i];
-            if (hv != 0) {
-                const int key = (hv & 0x7FFFF) - 1, r = hv >> 19;
-                const int pid = L.w.kcnt[key & 511] + r;
-                L.plist[pid] = (uint32_t)(key & 511) | ((uint32_t)(key >> 9) << 16);
-                L.u.hash[tid * PER + i] = (key + 1) | (pid << 19);
-            }
-        }
-    }
-    __syncthreads();
-    if (pv1) {
-        const uint32_t cb = L.cand[p1];
-        for (int h = wave; h < 8; h += PK_WAVES) {
-            const uint32_t hid = L.aid[h * VM_P + p1];
-            for (int k = 0; k < 8; ++k) {
-                const uint32_t kid = L.aid[k * VM_P + p1];
-                uint16_t pid = PK_NONE;
-                if (((cb >> h) & 1u) && kid != PK_NONE && ((L.awin[p1] >> (k + 1)) & 1u)) {
-                    const int key = (int)(kid | (hid << 9)) + 1;
-                    uint32_t slot = pk_mix((uint32_t)key) & (PK_P - 1);
-                    while ((L.u.hash[slot] & 0x7FFFF) != key) slot = (slot + 1) & (PK_P - 1);
-                    pid = (uint16_t)(L.u.hash[slot] >> 19);
-                }
-                L.pidx[(h * 8 + k) * VM_P + p1] = pid;
-            }
-        }
-    }
-    __syncthreads();
-    const int nP = L.nP;
-
-    if (pv1 && wave == 0) done[wi1] = 1;
-    PHASE_STAMP(8);
-    // ---- D: per view
-    for (int v = 0; v < N; ++v) {
-        const int s = v + 1;
-        const FastTex<F16, true> T(a, s);
-        const SrcTex<F16> Q(a, s);
-        // pair windows: ComputeBilateralNCCNew's k >= 1 iteration for a live pixel (APD.cu:500-575)
-        for (int base = 0; base < nP; base += PK_BLOCK) {
-            const int pid = base + tid;
-            const bool act = pid < nP;
-            const uint32_t pr = act ? L.plist[pid] : 0u;
-            const int kid = pr & 0xFFFF, hid = pr >> 16;
-            const int pk = L.apos[kid];
-            const int ax = pk & 0xFFFF, ay = pk >> 16;
-            const Hom Hm = homography(a, s, L.apl[hid]);
-            float asx, asy;
-            project(Hm, (float)ax, (float)ay, asx, asy);
-            bool live = act;
-            float res = -1.0f;  // absent
-            LANE_STAT(26, act);
-            if (act && (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H)) {
-                live = false;
-                if ((a.sel[ax + ay * W] >> (s - 1)) & 1u) res = APD_COST_MAX;
-            }
-#ifdef APD_ABLATE_PAIRS  // timing-only (wrong values): no pair-window taps
-            live = false;
-#endif
-            if (__ballot(live)) {
-                const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
-                float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-                ncc_new_window<F16, 3, 5>(a, &L.aref[kid], PK_D, (uint64_t)L.amask[kid], Hm, ax, ay, live, fast, T, Q, ss,
-                                          sss, srs);
-                if (live) {
-                    const float wsum = (float)L.aws[kid];
-                    if (wsum != 0.0f) res = ncc_finalize(L.asr[kid], L.asrr[kid], ss, sss, srs, wsum);
-                }
-            }
-            if (act) L.u.pcost[pid] = res;
-        }
-#ifdef APD_PHASE_STAMPS
-        __syncthreads();  // instrumented builds only: pair windows and centre windows timed apart
-        PHASE_STAMP(9);
-#endif
-        // centre windows: lane = pixel, wave = candidate
-        {
-            const uint32_t cb = pv1 ? L.cand[p1] : 0u;
-            for (int h = wave; h < 8; h += PK_WAVES) {
-                const bool want = (cb >> h) & 1u;
-                const uint16_t hid = L.aid[h * VM_P + p1];
-                LANE_STAT(28, want);
-                const float4 pl = want ? L.apl[hid] : make_float4(0.0f, 0.0f, 1.0f, 1.0f);
-                const Hom Hm = homography(a, s, pl);
-                float ptx, pty;
-                project(Hm, (float)px1, (float)py1, ptx, pty);
-                const bool alive = want && !(ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f);
-                const int pk = L.anc0[p1];
-                const bool has = alive && pk >= 0 && (L.awin[p1] & 1u);
-                const int ax = has ? (pk & 0xFFFF) : px1, ay = has ? (pk >> 16) : py1;
-                bool live = has, dead = !alive;
-                if (has) {
-                    float asx, asy;
-                    project(Hm, (float)ax, (float)ay, asx, asy);
-                    if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) { live = false; dead = true; }
-                }
-                float cc = 0.0f;
-                bool present = false;
-                if (__ballot(live)) {
-                    const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
-                    float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-                    ncc_new_window<F16, 6, 2>(a, &L.cref[p1], VM_P, L.cmask[p1], Hm, ax, ay, live, fast, T, Q, ss,
-                                              sss, srs);
-                    if (live) {
-                        const float wsum = (float)L.cws[p1];
-                        if (wsum != 0.0f) { cc = ncc_finalize(L.csr[p1], L.csrr[p1], ss, sss, srs, wsum); present = true; }
-                    }
-                }
-                L.w.d.ccost[h * VM_P + p1] = cc;
-                L.w.d.cstat[h * VM_P + p1] = (uint8_t)(dead ? 1 : 0) | (present ? 2 : 0);
-            }
-        }
-        __syncthreads();
-        PHASE_STAMP(10);
-        // focal combination (APD.cu:576-593, Softmax 431-446) per (candidate, pixel)
-        if (pv1) {
-            const uint32_t cb = L.cand[p1];
-            for (int h = wave; h < 8; h += PK_WAVES) {
-                if (!((cb >> h) & 1u)) continue;
-                float cost;
-                if (L.w.d.cstat[h * VM_P + p1] & 1u) {
-                    cost = APD_COST_MAX;
-                } else {
-                    const float center_cost = L.w.d.ccost[h * VM_P + p1];
-                    // the windows present, in anchor order: a compacted list in the reference, a
-                    // presence mask here (same values, same order; no dynamically indexed arrays)
-                    float sc[8];
-                    uint32_t pm = 0;
-                    float strong_weight = 0.0f;
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const uint16_t pid = L.pidx[(h * 8 + k) * VM_P + p1];
-                        sc[k] = pid == PK_NONE ? -1.0f : L.u.pcost[pid];
-                        if (sc[k] >= 0.0f) { pm |= 1u << k; strong_weight += 1.0f; }
-                    }
-                    if (strong_weight <= 1e-6f) {
-                        cost = center_cost;
-                    } else {
-                        float mx = -1e10f;
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) if (((pm >> k) & 1u) && sc[k] > mx) mx = sc[k];
-                        float e[8];
-                        float sum = 0.0f;
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            e[k] = 0.0f;
-                            if ((pm >> k) & 1u) { e[k] = d_expf(sc[k] - mx); sum += e[k]; }
-                        }
-                        float acc = 0.0f;
-#pragma unroll
-                        for (int k = 0; k < 8; ++k)
-                            if ((pm >> k) & 1u) { const float w = e[k] / sum; acc = fmaf(w, sc[k], acc); }
-                        acc = (acc > APD_COST_MAX) ? APD_COST_MAX : acc;
-                        cost = (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
-                    }
-                }
-                out[((size_t)v * 8 + h) * (size_t)wc + wi1] = cost;
-            }
-        }
-        __syncthreads();
-        PHASE_STAMP(11);
-    }
-}
 
 // ---------------------------------------------------------------------------------------------
 // Image-wide anchor-window pairs (no SA masks). A WEAK pixel's anchor candidate h (the plane of its
@@ -3035,17 +2102,17 @@ __global__ __launch_bounds__(PK_BLOCK, PK_WAVES / 2) void k_weak_cand_vm(Args a,
 //   per iteration: k_gp_cost evaluates every pair in every view (lane = pair, consecutive pairs share
 //     a window anchor) into pcost[pair][view]; k_weak_cand_g evaluates the centre windows (lane =
 //     pixel, wave = candidate) and the focal combination reading the pair costs, and writes the same
-//     [view][candidate][WEAK index] costs as k_weak_cand_vm.
+//     [view][candidate][WEAK index] costs the sweep reads (direct mode).
 // ---------------------------------------------------------------------------------------------
 #define GP_CHUNK 256   // references per batch of k_gp_dedup (one workgroup per window anchor)
 #define GP_HS 8192     // LDS hash slots (a table closes at GP_HS / 2 keys; + <= 8 * GP_CHUNK per batch: load <= 0.75)
 #define GP_NONE 0xFFFFFFFFu
 
 // profiling: a wave's sum of the lanes' counts, one atomic per wave
-__device__ __forceinline__ void wave_count(unsigned long long *slot, uint32_t n) {
+__device__ __forceinline__ void wave_count(APD_G unsigned long long *evals, int k, uint32_t n) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
-    if ((threadIdx.x & (WAVE - 1)) == 0 && n) atomicAdd(slot, (unsigned long long)n);
+    if ((threadIdx.x & (WAVE - 1)) == 0 && n) atomicAdd(PROF_AT(evals, k), (unsigned long long)n);
 }
 // Lanes are consecutive WEAK pixels in tile order, whose anchor k is often the same STRONG point: per
 // slot k the runs of equal anchors among neighbouring lanes take one atomic (run head).
@@ -3263,13 +2330,16 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
 }
 
 // every pair in every view: ComputeBilateralNCCNew's k >= 1 window (APD.cu:500-575), the same
-// statements as k_weak_cand_vm's pair windows; pcost[pair][v] rows padded to a multiple of 4 views
+// statements as ncc_new_vm's anchor windows; pcost[pair][v] rows padded to a multiple of 4 views
 // (< 0: window absent). The block's 256 pairs are consecutive, so their rows are one contiguous
 // range of pcost: the costs are staged in LDS ([pair][Np], gp_cost_lds_bytes) and written with
 // coalesced 16-byte stores after the view loop (a 4-byte store per (pair, view) at the row stride
 // wrote 4.2x the bytes, profiles/r3_pmc_k_gp_cost_c3b.json).
-static inline size_t gp_cost_lds_bytes(int N) { return (size_t)BLOCK * ((N + 3) & ~3) * sizeof(float); }
-template <bool F16>
+#ifndef GP_COST_STAGED
+#define GP_COST_STAGED 1  // (A/B: 0 = one 4-byte store per (pair, view))
+#endif
+static inline size_t gp_cost_lds_bytes(int N) { return GP_COST_STAGED ? (size_t)BLOCK * ((N + 3) & ~3) * sizeof(float) : 0; }
+template <bool F16, bool SA>
 __global__ __launch_bounds__(BLOCK) void k_gp_cost(Args a, const int2 *__restrict__ plist, int np, float *__restrict__ pcost) {
     using RT = typename std::conditional<F16, _Float16, float>::type;
     __shared__ RT rref[9 * BLOCK];
@@ -3280,7 +2350,7 @@ __global__ __launch_bounds__(BLOCK) void k_gp_cost(Args a, const int2 *__restric
     const bool act = i < np;
     const int2 pr = plist[act ? i : np - 1];
     const int ax = pr.x & 0x7FFF, ay = pr.x >> 16;
-    const bool filt = (pr.x & 0x8000) != 0;  // SA-filtered window: taps with the anchor's label only
+    const bool filt = SA && (pr.x & 0x8000) != 0;  // SA-filtered window: taps with the anchor's label only
     const float4 pl = a.plane[pr.y];
     float sr = 0.0f, srr = 0.0f, wsum = 9.0f;
     uint64_t tm = 0x1FFull;
@@ -3328,9 +2398,11 @@ __global__ __launch_bounds__(BLOCK) void k_gp_cost(Args a, const int2 *__restric
             if (live) res = ncc_finalize(sr, srr, ss, sss, srs, wsum);
         }
         nlive += live;
-        crow[threadIdx.x * Np + v] = res;
+        if (GP_COST_STAGED) crow[threadIdx.x * Np + v] = res;
+        else if (act) pcost[(size_t)i * Np + v] = res;
     }
-    if (a.evals) wave_count(a.evals + 5, nlive);  // (profiling: pair windows evaluated)
+    if (a.evals) wave_count(a.evals, 5, nlive);  // (profiling: pair windows evaluated)
+    if (!GP_COST_STAGED) return;
     for (int v = N; v < Np; ++v) crow[threadIdx.x * Np + v] = -1.0f;  // (padding, never read)
     __syncthreads();
     const int nq = (min(BLOCK, np - i0) * Np) >> 2;  // float4s of the block's rows
@@ -3375,10 +2447,9 @@ __device__ __forceinline__ float gp_combine(float cc, const float (&sc)[8]) {
 // anchor 0 projected out of frame). With an SA label at the pixel the centre window is used only
 // when anchor 0 carries the label (else center_cost stays 0, APD.cu:493-497) and its taps are
 // filtered by it (APD.cu:526-530); an empty window leaves center_cost 0 (APD.cu:543).
-template <bool F16>
+template <bool F16, bool SA>
 __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__restrict__ list, int count,
-                                                          const uint8_t *__restrict__ cbw, float *__restrict__ out,
-                                                          uint8_t *__restrict__ done, int wc) {
+                                                          const uint8_t *__restrict__ cbw, float *__restrict__ out, int wc) {
     using RT = typename std::conditional<F16, _Float16, float>::type;
     __shared__ RT cref[36 * VM_P];
     __shared__ float csr[VM_P], csrr[VM_P];
@@ -3406,7 +2477,6 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
             const bool ok = !(z.x == -1 || z.y == -1) && (cid == 0 || (int)a.sa[z.x + z.y * W] == cid);
             a0 = ok ? ((int)(uint16_t)z.x | ((int)z.y << 16)) : -1;  // (an unused window: as if absent)
             cb = cbw[wi1];
-            done[wi1] = 1;
         }
         anc0[p1] = a0;
         cbits[p1] = (uint8_t)cb;
@@ -3453,7 +2523,7 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
         pl = a.plane[ap.x + ap.y * W];
     }
     const int pk0 = anc0[p1];
-    const uint64_t tm = cmask[p1];
+    const uint64_t tm = SA ? cmask[p1] : ~0ull;  // (no SA masks: every tap)
     uint32_t nlive = 0;
     for (int v = 0; v < N; ++v) {
         const int s = v + 1;
@@ -3485,7 +2555,7 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
         // (k_weak_cand_comb reads it back and writes the candidate's cost in its place)
         if (want) out[((size_t)v * 8 + h) * (size_t)wc + wi1] = dead ? -1.0f : center_cost;
     }
-    if (a.evals) wave_count(a.evals + 6, nlive);  // (profiling: centre windows evaluated)
+    if (a.evals) wave_count(a.evals, 6, nlive);  // (profiling: centre windows evaluated)
 }
 // The focal combination (APD.cu:576-593, Softmax 431-446) of each (WEAK pixel, candidate) and view,
 // a thread per (pixel, candidate): few registers and many waves in flight for the pair-cost gathers.
@@ -3523,170 +2593,6 @@ __global__ __launch_bounds__(BLOCK) void k_weak_cand_comb(Args a, const int *__r
             for (int k = 0; k < 8; ++k) sc[k] = dv == 0 ? q[k].x : dv == 1 ? q[k].y : dv == 2 ? q[k].z : q[k].w;
             float *o = out + ((size_t)v * 8 + h) * (size_t)wc + wi;
             *o = gp_combine(*o, sc);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// CheckerboardPropagationWeak + PlaneHypothesisRefinementWeak (APD.cu:1442-1615, 1008-1096)
-// ---------------------------------------------------------------------------------------------
-template <bool F16>
-__global__ __launch_bounds__(BLOCK) void k_sweep_weak(Args a, const int *__restrict__ list, int count, int iter) {
-    const int N = a.N, W = a.W;
-    const int wave = xcd_remap(blockIdx.x, gridDim.x) * (BLOCK / WAVE) + (threadIdx.x >> 6);
-    if (wave * (WAVE / N) >= count) return;
-    const Group G = make_group(N, count, wave);
-    const int c = list[G.li];
-    const int py = c / W, px = c - py * W;
-    const int s = G.v + 1;
-    const APD_C Cam &cam0 = a.cams[0];
-    const APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
-    const bool geom = a.geom != 0;
-    const float gf = a.gf;
-    const float4 cur = a.plane[c];
-
-    int pos[8];
-    bool flag[8];
-    float prior = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const short2 ap = anc[i + 1];
-        const bool ok = !(ap.x == -1 || ap.y == -1);
-        pos[i] = ok ? ap.x + ap.y * W : 0;
-        flag[i] = ok && a.weak[pos[i]] == APD_STRONG;
-        if (ok) prior += ((a.sel[pos[i]] >> G.v) & 1u) ? 0.9f : 0.1f;
-    }
-    float ca[8];
-    float cv_now = 0.0f;
-#pragma unroll 1
-    for (int h = 0; h < 9; ++h) {
-        int ph = pos[0];
-        bool fh = flag[0];
-#pragma unroll
-        for (int k = 1; k < 8; ++k) if (h == k) { ph = pos[k]; fh = flag[k]; }
-        if (h == 8) fh = true;
-        float val = (h == 0 && G.v == 0) ? 2.0f : 0.0f;
-        if (fh) {
-            const float4 pl = (h == 8) ? cur : a.plane[ph];
-            val = ncc_new<F16>(a.self, px, py, s, pl);
-            if (h == 8 && geom) val = fmaf(gf, geom_cost(a, px, py, s, pl), val);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) if (h == k) ca[k] = val;
-        if (h == 8) cv_now = val;
-    }
-    Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ord_weak(iter));
-    const int w = view_selection(ca, prior, iter, g, G, N);
-    const uint32_t tsel = group_bits(w > 0, G);
-
-    // hypothesis costs with the geometric term (APD.cu:1554-1573)
-    float gval[8];
-#pragma unroll 1
-    for (int j = 0; j < 8; ++j) {
-        int pj = pos[0];
-        bool fj = flag[0];
-        float cj = ca[0];
-#pragma unroll
-        for (int k = 1; k < 8; ++k) if (j == k) { pj = pos[k]; fj = flag[k]; cj = ca[k]; }
-        float v = cj;
-        if (geom && w > 0) v = fj ? fmaf(gf, geom_cost(a, px, py, s, a.plane[pj]), cj) : fmaf(gf, 3.0f, cj);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) if (j == k) gval[k] = v;
-    }
-    float fc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    float wn = 0.0f, cost_now = 0.0f;
-    for (int k = 0; k < N; ++k) {
-        const int wk = __shfl(w, G.base + k);
-        const float fwk = (float)wk;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float vk = __shfl(gval[j], G.base + k);
-            if (wk > 0) fc[j] = fmaf(fwk, vk, fc[j]);
-        }
-        if (wk > 0) wn += fwk;
-        cost_now = fmaf(fwk, __shfl(cv_now, G.base + k), cost_now);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) fc[j] /= wn;
-    cost_now /= wn;
-    const float cost_init = cost_now;
-    int mi = 0;
-    {
-        float m = fc[0];
-#pragma unroll
-        for (int j = 1; j < 8; ++j) if (fc[j] <= m) { m = fc[j]; mi = j; }
-    }
-    float depth_now = depth_from_plane(cam0, cur, px, py);
-    float4 pnow = cur;
-    {
-        int pm = pos[0];
-        bool fm = flag[0];
-        float fcm = fc[0];
-#pragma unroll
-        for (int k = 1; k < 8; ++k) if (mi == k) { pm = pos[k]; fm = flag[k]; fcm = fc[k]; }
-        if (fm) {
-            const float4 cand = a.plane[pm];
-            const float db = depth_from_plane(cam0, cand, px, py);
-            if (db >= a.dmin && db <= a.dmax && fcm < cost_now) {
-                depth_now = db; pnow = cand; cost_now = fcm;
-                if (G.valid && G.v == 0) a.sel[c] = tsel;
-            }
-        }
-    }
-    // PlaneHypothesisRefinementWeak (APD.cu:1008-1096): fit plane first, then 5 random candidates;
-    // a zero fit normal skips the whole refinement (APD.cu:1028-1030).
-    const float4 fit = a.fit[c];
-    if (!(fit.x == 0 && fit.y == 0 && fit.z == 0)) {  // group-uniform
-        {
-            float cv = 0.0f;
-            if (w > 0) {
-                cv = ncc_new<F16>(a.self, px, py, s, fit);
-                if (geom) cv = fmaf(gf, geom_cost(a, px, py, s, fit), cv);
-            }
-            float tc = 0.0f;
-            for (int kk = 0; kk < N; ++kk) {
-                const int wk = __shfl(w, G.base + kk);
-                const float vk = __shfl(cv, G.base + kk);
-                if (wk > 0) tc = fmaf((float)wk, vk, tc);
-            }
-            tc /= wn;
-            const float db = depth_from_plane(cam0, fit, px, py);
-            if (db >= a.dmin && db <= a.dmax && tc < cost_now) { depth_now = db; pnow = fit; cost_now = tc; }
-        }
-        const Cands C = refine_candidates(a, px, py, g, pnow, depth_now);
-        const float4 cur0 = pnow;
-        const float d0 = depth_now;
-#pragma unroll 1
-        for (int k = 0; k < 5; ++k) {
-            float dk;
-            float4 t = candidate(C, k, cur0, d0, dk);
-            t.w = dist2origin(cam0, px, py, dk, t);
-            float cv = 0.0f;
-            if (w > 0) {
-                cv = ncc_new<F16>(a.self, px, py, s, t);
-                if (geom) cv = fmaf(gf, geom_cost(a, px, py, s, t), cv);
-            }
-            float tc = 0.0f;
-            for (int kk = 0; kk < N; ++kk) {
-                const int wk = __shfl(w, G.base + kk);
-                const float vk = __shfl(cv, G.base + kk);
-                if (wk > 0) tc = fmaf((float)wk, vk, tc);
-            }
-            tc /= wn;
-            const float db = depth_from_plane(cam0, t, px, py);
-            if (db >= a.dmin && db <= a.dmax && tc < cost_now) { depth_now = db; pnow = t; cost_now = tc; }
-        }
-    }
-    if (G.valid) {
-        a.vw[(size_t)G.v * a.HW + c] = (uint8_t)w;
-        if (G.v == 0) {
-            if (a.state == APD_REFINE_INIT) {
-                if ((double)cost_now < (double)cost_init - 0.1) { a.cost[c] = cost_now; a.plane[c] = pnow; }
-                else a.cost[c] = cost_init;
-            } else {
-                a.cost[c] = cost_now;
-                a.plane[c] = pnow;
-            }
         }
     }
 }
@@ -3967,7 +2873,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 tcL[(dd * N + v) * VM_P + q] = tc;
             }
         }
-        if (a.evals) { wave_count(a.evals + 3, n_ncc); wave_count(a.evals + 4, n_geo); }
+        if (a.evals) { wave_count(a.evals, 3, n_ncc); wave_count(a.evals, 4, n_geo); }
         __syncthreads();
         // ---- P2: in-order weighted view sums per (pixel, depth)
         for (int dd = wave; dd < dc; dd += VM_WAVES) {
@@ -4122,9 +3028,8 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, in
             if (a.wcur && T.pv && use_new) a.wcur[(size_t)v * a.HW + c] = seldep ? __int_as_float(0x7fc00000) : nv;
         }
         if (T.pv) {
-            if (use_new) {
-                if constexpr (APD) cv = nv;
-                else cv = ncc_new<F16>(a.self, px, py, v + 1, pl);
+            if (use_new) {  // (APD instantiations only: use_new needs a.use_apd)
+                cv = nv;
             } else {
                 bool slow;
                 cv = ncc_old_fast<F16, VM_P>(a, px, py, v + 1, pl, rw, slow);
@@ -4347,101 +3252,6 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_local_refine_vm(Args a, i
     if (wave == 0 && run && (double)(L.cost_now[p] - min_cost) > 0.1) a.plane[c].w = best;
 }
 
-template <bool F16>
-__global__ __launch_bounds__(BLOCK) void k_depth_to_weak(Args a) {
-    const int N = a.N, W = a.W, H = a.H;
-    const int P = WAVE / N;
-    const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
-    const Group G = make_group(N, a.HW, wave);   // no early exit: __syncthreads below
-    const int c = G.li;
-    const int py = c / W, px = c - py * W;
-    const int s = G.v + 1;
-    const APD_C Cam &cam0 = a.cams[0];
-    float *pc = lds_slot(G, P, 61, 0);
-    const bool border = px < 6 || py < 6 || px >= W - 6 || py >= H - 6;
-    const float4 pl = to_ref(cam0, a.plane[c]);
-    const float od = pl.w;
-    const uint32_t sv = a.sel[c];
-    const bool mine = (sv >> G.v) & 1u;
-    const int wv = a.vw[(size_t)G.v * a.HW + c];
-    float mydist;
-    {
-        const APD_C Cam &sc = a.cams[s];
-        float d0 = cam0.c[0] - sc.c[0], d1 = cam0.c[1] - sc.c[1], d2 = cam0.c[2] - sc.c[2];
-        mydist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
-    }
-    float base = 0.0f, wn = 0.0f;
-    int valid = 0;
-    for (int k = 0; k < N; ++k) {
-        const float dk = __shfl(mydist, G.base + k);
-        const int wk = __shfl(wv, G.base + k);
-        if ((sv >> k) & 1u) { wn += (float)wk; base += dk; valid++; }
-    }
-    // per-pixel early outs (group-uniform)
-    int state = -1;
-    if (border || od == 0) state = APD_UNKNOWN;
-    else if (valid == 0) state = APD_UNKNOWN;
-    const bool active = state < 0;
-    if (active) base /= (float)valid;
-    const float disp = cam0.K[0] * base / od;
-    RefWin rw;
-    build_refwin(a, px, py, lds_slot(G, P, 36, (BLOCK / WAVE) * P * 61), G.v, N, rw);
-    const bool geom = a.geom != 0;
-    const float gf = a.gf;
-#pragma unroll 1
-    for (int d = 0; d < 61; ++d) {
-        const float pdepth = cam0.K[0] * base / (disp + (float)(d - 30));
-        const bool in_range = !(pdepth < a.dmin || pdepth > a.dmax);
-        float tc = 0.0f;
-        if (active && in_range && mine) {
-            float4 t = pl;
-            t.w = dist2origin(cam0, px, py, pdepth, t);
-            tc = ncc_old<F16>(a, px, py, s, t, rw);
-            if (geom) tc = fmaf(gf, geom_cost(a, px, py, s, t), tc);
-        }
-        float p = 0.0f;
-        for (int k = 0; k < N; ++k) {
-            const float tk = __shfl(tc, G.base + k);
-            const int wk = __shfl(wv, G.base + k);
-            if ((sv >> k) & 1u) p = fmaf(tk, (float)wk, p);
-        }
-        p /= wn;
-        const float val = in_range ? ((2.0f > p) ? p : 2.0f) : 2.0f;
-        if (G.v == 0 && G.valid) {
-            pc[d] = val;
-            if (a.curve && active) a.curve[(size_t)c * 61 + d] = val;
-        }
-    }
-    __syncthreads();
-    if (active) {
-        int cnt = 0, min_peak = 0;
-        float min_cost = 2.0f;
-        uint64_t peaks = 0;
-        for (int i = 2; i < 59; ++i) {
-            const float ci = pc[i];
-            if (pc[i - 1] > ci && pc[i + 1] > ci) {
-                peaks |= 1ull << i;
-                cnt++;
-                if (ci < min_cost) { min_peak = i; min_cost = ci; }
-            }
-        }
-        if (abs(min_peak - 30) > a.peak_radius || pc[min_peak] > 0.5f) {
-            state = APD_WEAK;
-        } else if (cnt == 1) {
-            state = (pc[min_peak] <= 0.15f) ? APD_STRONG : APD_WEAK;
-        } else {
-            float var = 0.0f;
-            for (int i = 2; i < 59; ++i) {
-                if (((peaks >> i) & 1ull) && i != min_peak) { float dd = pc[i] - min_cost; var = fmaf(dd, dd, var); }
-            }
-            var = sqrtf(var);
-            var /= (float)(cnt - 1);
-            state = (var > 0.2f) ? APD_STRONG : APD_WEAK;
-        }
-    }
-    if (G.valid && G.v == 0) a.weak[c] = (uint8_t)state;
-}
-
 // ConfidenceCompute (APD.cu:2282-2344)
 __global__ __launch_bounds__(BLOCK) void k_confidence(Args a) {
     const int c = blockIdx.x * BLOCK + threadIdx.x;
@@ -4475,83 +3285,6 @@ __global__ __launch_bounds__(BLOCK) void k_confidence(Args a) {
     }
     if (nc > 255) nc = 255;
     a.conf[c] = (uint8_t)nc;
-}
-
-// LocalRefine (APD.cu:2346-2432)
-template <bool F16>
-__global__ __launch_bounds__(BLOCK) void k_local_refine(Args a) {
-    const int N = a.N, W = a.W;
-    const int wave = blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
-    if (wave * (WAVE / N) >= a.HW) return;
-    const Group G = make_group(N, a.HW, wave);
-    const int c = G.li;
-    const int py = c / W, px = c - py * W;
-    const int s = G.v + 1;
-    const APD_C Cam &cam0 = a.cams[0];
-    const float4 pl = to_ref(cam0, a.plane[c]);
-    const float od = pl.w;
-    const uint32_t sv = a.sel[c];
-    const bool mine = (sv >> G.v) & 1u;
-    const int wv = a.vw[(size_t)G.v * a.HW + c];
-    const bool geom = a.geom != 0;
-    const float gf = a.gf;
-    RefWin rw;
-    build_refwin(a, px, py, lds_slot(G, WAVE / N, 36, 0), G.v, N, rw);
-    float mydist, tc0 = 0.0f;
-    {
-        const APD_C Cam &sc = a.cams[s];
-        float d0 = cam0.c[0] - sc.c[0], d1 = cam0.c[1] - sc.c[1], d2 = cam0.c[2] - sc.c[2];
-        mydist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
-    }
-    const bool live = od != 0;  // group-uniform
-    if (live && mine) {
-        float4 t = pl;
-        t.w = dist2origin(cam0, px, py, od, t);
-        tc0 = ncc_old<F16>(a, px, py, s, t, rw);
-        if (geom) tc0 = fmaf(gf, geom_cost(a, px, py, s, t), tc0);
-    }
-    float cost_now = 0.0f, base = 0.0f, wn = 0.0f;
-    int valid = 0;
-    for (int k = 0; k < N; ++k) {
-        const float tk = __shfl(tc0, G.base + k);
-        const int wk = __shfl(wv, G.base + k);
-        const float dk = __shfl(mydist, G.base + k);
-        if ((sv >> k) & 1u) {
-            cost_now = fmaf(tk, (float)wk, cost_now);
-            wn += (float)wk;
-            base += dk;
-            valid++;
-        }
-    }
-    const bool run = live && !(wn == 0 || valid == 0);
-    if (run) { cost_now /= wn; base /= (float)valid; }
-    const float disp = cam0.K[0] * base / od;
-    float min_cost = 2.0f, best = od;
-#pragma unroll 1
-    for (int d = -5; d <= 5; ++d) {
-        const float pdepth = cam0.K[0] * base / (disp + (float)d);
-        const bool in_range = !(pdepth < a.dmin || pdepth > a.dmax);
-        float nv = 0.0f, gv = 0.0f;
-        if (run && in_range && mine) {
-            float4 t = pl;
-            t.w = dist2origin(cam0, px, py, pdepth, t);
-            nv = ncc_old<F16>(a, px, py, s, t, rw);
-            if (geom) gv = gf * geom_cost(a, px, py, s, t);
-        }
-        float tc = 0.0f;
-        for (int k = 0; k < N; ++k) {
-            const float nk = __shfl(nv, G.base + k);
-            const float gk = __shfl(gv, G.base + k);
-            const int wk = __shfl(wv, G.base + k);
-            if ((sv >> k) & 1u) {
-                tc = fmaf(nk, (float)wk, tc);
-                if (geom) tc = fmaf(gk, (float)wk, tc);
-            }
-        }
-        tc /= wn;
-        if (run && in_range && tc < min_cost) { min_cost = tc; best = pdepth; }
-    }
-    if (run && G.valid && G.v == 0 && (double)(cost_now - min_cost) > 0.1) a.plane[c].w = best;
 }
 
 // cv::resize INTER_NEAREST between device buffers with the host library's index arithmetic
@@ -4614,18 +3347,17 @@ struct apd_ctx {
     std::string err;
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
-        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, wdone, lrs, wcur,
+        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, lrs, wcur,
         wlist, gp_cb, gp_cnt, gp_cur, gp_refs, gp_ccnt, gp_cbase, gp_plist, gp_pidx, gp_pcost, gp_tmp;
     int n_near = 0;
     int host_stat[4] = {0, 0, 0, 0};  // apd_set_problem's read-back (see there)
     int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
     Args args{};
     bool loaded = false, prepared = false;
-    bool sweep_vm = true;          // view-major Strong sweep (APD_SWEEP_LANES=1 selects k_sweep_strong)
     int dw_tile_w = 8;             // DepthToWeak pixel tile width (64 / tile height); APD_DW_TILE_W
     int tile_w = 8;                // sweep list tile width (tile = tile_w x 256/tile_w positions); APD_TILE_W
-    bool cand_pairs = true;        // Weak sweep candidates through k_weak_cand_vm; APD_NO_CAND_PAIRS=1 disables
-    bool cand_global = true;       // ... through the image-wide pair table (no SA); APD_NO_GLOBAL_PAIRS=1 disables
+    bool cand_pairs = true;        // Weak sweep candidates through the image-wide pair table; APD_NO_CAND_PAIRS=1
+                                   // leaves them to the sweep
     bool gp_on = false;            // the pair table of the prepared problem is built (apd_stage_prepare)
     int gp_np = 0;                 // its distinct pairs
     bool lr_handover = true;       // LocalRefine reads DepthToWeak's samples; APD_NO_LR_HANDOVER=1 disables
@@ -4648,6 +3380,7 @@ struct apd_ctx {
     };
     bool prof = false;
     std::vector<ProfEv> prof_ev;
+    std::vector<hipEvent_t> prof_pool;  // recycled events (created once; no system-scope fence)
 };
 
 #define HIP_OK(ctx, call)                                                                          \
@@ -4789,11 +3522,6 @@ static bool inlier_limit(float D, float t, float *limit) {
 }
 
 static inline unsigned blocks_for(size_t n, int per_block) { return (unsigned)((n + per_block - 1) / per_block); }
-static inline unsigned group_blocks(int n_pixels, int N) {
-    const int P = WAVE / N;
-    const int waves = (n_pixels + P - 1) / P;
-    return (unsigned)((waves + (BLOCK / WAVE) - 1) / (BLOCK / WAVE));
-}
 
 extern "C" {
 
@@ -4826,10 +3554,8 @@ apd_ctx *apd_create(int32_t device) {
         delete ctx;
         return nullptr;
     }
-    for (auto &e : ctx->ev) (void)hipEventCreate(&e);
-    ctx->sweep_vm = getenv("APD_SWEEP_LANES") == nullptr;
+    for (auto &e : ctx->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);  // timing only
     ctx->cand_pairs = getenv("APD_NO_CAND_PAIRS") == nullptr;
-    ctx->cand_global = getenv("APD_NO_GLOBAL_PAIRS") == nullptr;
     ctx->lr_handover = getenv("APD_NO_LR_HANDOVER") == nullptr;
     ctx->wcur_on = getenv("APD_NO_WCUR") == nullptr;
     // tile_pix needs the tile width to divide the 64-pixel tile (otherwise two workgroups share pixels)
@@ -4845,8 +3571,8 @@ apd_ctx *apd_create(int32_t device) {
     const void *vm_kernels[] = {
         (const void *)k_sweep_strong_vm<true, false>, (const void *)k_sweep_strong_vm<false, false>,
         (const void *)k_sweep_strong_vm<true, true>, (const void *)k_sweep_strong_vm<false, true>,
-        (const void *)k_weak_cand_vm<true>, (const void *)k_weak_cand_vm<false>,
-        (const void *)k_sweep_weak_vm<true>, (const void *)k_sweep_weak_vm<false>,
+        (const void *)k_sweep_weak_vm<true, false>, (const void *)k_sweep_weak_vm<false, false>,
+        (const void *)k_sweep_weak_vm<true, true>, (const void *)k_sweep_weak_vm<false, true>,
         (const void *)k_depth_to_weak_vm<true, false>, (const void *)k_depth_to_weak_vm<false, false>,
         (const void *)k_depth_to_weak_vm<true, true>, (const void *)k_depth_to_weak_vm<false, true>,
         (const void *)k_local_refine_vm<true, false>, (const void *)k_local_refine_vm<false, false>,
@@ -4866,13 +3592,14 @@ void apd_destroy(apd_ctx *ctx) {
     DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
-                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand, &ctx->wdone,
+                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand,
                       &ctx->lrs, &ctx->wcur, &ctx->wlist, &ctx->gp_cb, &ctx->gp_cnt, &ctx->gp_cur, &ctx->gp_refs, &ctx->gp_ccnt,
                       &ctx->gp_cbase, &ctx->gp_plist, &ctx->gp_pidx, &ctx->gp_pcost, &ctx->gp_tmp};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
     for (auto &pe : ctx->prof_ev) { (void)hipEventDestroy(pe.e0); (void)hipEventDestroy(pe.e1); }
+    for (hipEvent_t e : ctx->prof_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -5048,7 +3775,7 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     a.lr_ncc = nullptr;
     a.lr_geo = nullptr;
     a.wcur = nullptr;
-    if (ctx->sweep_vm && ctx->wcur_on) {  // the initial planes' costs per view (NCC-New for WEAK pixels), [N][H*W]
+    if (ctx->wcur_on) {  // the initial planes' costs per view (NCC-New for WEAK pixels), [N][H*W]
         if ((st = ensure(ctx, ctx->wcur, HW * N * sizeof(float)))) return st;
         a.wcur = devptr<decltype(a.wcur)>(ctx->wcur.p);
     }
@@ -5079,7 +3806,7 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     // pass does not keep it through the next round's init pass), and only when it fits in the
     // device's free memory with 4 GiB to spare -- else LocalRefine evaluates the samples itself.
     ctx->lrs_need = 0;
-    if (ctx->sweep_vm && ctx->lr_handover) {
+    if (ctx->lr_handover) {
         const int tw = ctx->dw_tile_w, th = VM_P / tw;
         const size_t slots = (size_t)(((W + tw - 1) / tw) * ((H + th - 1) / th)) * VM_P;
         const size_t need = (size_t)11 * N * slots * sizeof(float) * (P.geom_consistency ? 2 : 1);
@@ -5262,25 +3989,25 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         for (int i = 0; i < 4; ++i) {
             if ((st = build_tile_list(ctx, modes[i][0], modes[i][1], list_ptr(ctx, i), tot + i))) return st;
         }
-        if (a.use_apd && ctx->sweep_vm && ctx->cand_pairs && ctx->cnt[2] + ctx->cnt[3] > 0) {
-            // k_weak_cand_vm runs once per iteration over the WEAK pixels of both colours (tile
-            // order): between the two Weak launches no anchor plane or selection changes, and the
-            // denser groups share more anchor windows. Costs are kept by WEAK index.
+        if (a.use_apd && ctx->cand_pairs && ctx->cnt[2] + ctx->cnt[3] > 0) {
+            // the anchor candidates' kernels run once per iteration over the WEAK pixels of both
+            // colours (tile order): between the two Weak launches no anchor plane or selection
+            // changes. Costs are kept by WEAK index.
             const size_t wc = (size_t)std::max(ctx->weak_count, 1);
             if ((st = ensure(ctx, ctx->wcand, (size_t)a.N * 8 * wc * sizeof(float)))) return st;
-            if ((st = ensure(ctx, ctx->wdone, wc))) return st;
             if ((st = ensure(ctx, ctx->wlist, (size_t)(ctx->cnt[2] + ctx->cnt[3]) * sizeof(int)))) return st;
             if ((st = build_tile_list(ctx, 1, 2, (int *)ctx->wlist.p, tot + 5))) return st;
             (void)hipEventRecord(ctx->ev[14], s);
-            if (ctx->cand_global && (size_t)a.HW < (1u << 25) && a.W < 32768 &&
-                (st = build_global_pairs(ctx, ctx->cnt[2] + ctx->cnt[3])))
+            // (the table's keys hold a pixel index below 2^25 and x below 2^15; else the sweep
+            // evaluates the candidates itself)
+            if ((size_t)a.HW < (1u << 25) && a.W < 32768 && (st = build_global_pairs(ctx, ctx->cnt[2] + ctx->cnt[3])))
                 return st;
         } else {
             (void)hipEventRecord(ctx->ev[14], s);
         }
     }
     (void)hipEventRecord(ctx->ev[2], s);
-    if (ctx->sweep_vm) {
+    {
         const int tw = ctx->dw_tile_w, th = VM_P / tw;
         const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
         if (a.use_apd) {
@@ -5300,8 +4027,6 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
                 else hipLaunchKernelGGL((k_random_init_vm<false, false, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, false>(a.N)), s, a, tw);
             }
         }
-    } else {
-        LAUNCH_TEX(k_random_init, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);
     }
     HIP_OK(ctx, hipMemcpyAsync(ctx->sel.p, ctx->sel2.p, (size_t)a.HW * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     if ((st = check_launch(ctx, "k_random_init"))) return st;
@@ -5311,19 +4036,31 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
     return APD_OK;
 }
 
-// profiling brackets around one launch (no-ops unless apd_profile_reset(ctx, 1))
+// profiling brackets around one launch (no-ops unless apd_profile_reset(ctx, 1)). The events are
+// timing-only: without the system-scope release fence a record does not write back and invalidate
+// the caches between the bracketed kernels (with the default fence the brackets cost the C3 step
+// ~15 ms), and they are recycled instead of created per launch.
+static hipEvent_t prof_event(apd_ctx *ctx) {
+    hipEvent_t e = nullptr;
+    if (!ctx->prof_pool.empty()) {
+        e = ctx->prof_pool.back();
+        ctx->prof_pool.pop_back();
+    } else {
+        (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+    }
+    return e;
+}
 static hipEvent_t prof_begin(apd_ctx *ctx) {
     hipEvent_t e0 = nullptr;
     if (ctx->prof) {
-        (void)hipEventCreate(&e0);
+        e0 = prof_event(ctx);
         (void)hipEventRecord(e0, ctx->stream);
     }
     return e0;
 }
 static void prof_end(apd_ctx *ctx, hipEvent_t e0, int kind, int64_t px) {
     if (!ctx->prof) return;
-    hipEvent_t e1 = nullptr;
-    (void)hipEventCreate(&e1);
+    hipEvent_t e1 = prof_event(ctx);
     (void)hipEventRecord(e1, ctx->stream);
     ctx->prof_ev.push_back({e0, e1, kind, px});
 }
@@ -5342,12 +4079,8 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
         Args ak = a;
         ak.evals = evals;
         if (!(ctx->wcur_fresh && iter == 0)) ak.wcur = nullptr;  // RandomInitialization's costs: iteration 0 only
-        if (ctx->sweep_vm)
-            LAUNCH_TEX_SA(k_sweep_strong_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), vm_lds_bytes(a.N) + sa_lds_bytes(a), s,
-                       ak, (const int *)list_ptr(ctx, colour), n, iter);
-        else
-            LAUNCH_TEX(k_sweep_strong, dim3(group_blocks(n, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a,
-                       (const int *)list_ptr(ctx, colour), n, iter);
+        LAUNCH_TEX_SA(k_sweep_strong_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), vm_lds_bytes(a.N) + sa_lds_bytes(a), s,
+                      ak, (const int *)list_ptr(ctx, colour), n, iter);
         prof_end(ctx, e0, APD_PROF_STRONG_SWEEP, n);
         if ((st = check_launch(ctx, "k_sweep_strong"))) return st;
     }
@@ -5358,36 +4091,29 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
         const int nw = ctx->cnt[2] + ctx->cnt[3];
         const int wc = std::max(ctx->weak_count, 1);
         const float *cand = nullptr;
-        if (ctx->sweep_vm && ctx->cand_pairs && nw > 0) {
-            if (ctx->wcand.bytes < (size_t)a.N * 8 * (size_t)wc * sizeof(float) || ctx->wdone.bytes < (size_t)wc ||
-                ctx->wlist.bytes < (size_t)nw * sizeof(int)) {
+        if (ctx->cand_pairs && nw > 0 && ctx->gp_on) {
+            if (ctx->wcand.bytes < (size_t)a.N * 8 * (size_t)wc * sizeof(float) || ctx->wlist.bytes < (size_t)nw * sizeof(int)) {
                 ctx->err = "candidate cost buffers not sized by apd_stage_prepare";
                 return APD_ESTATE;
             }
-            e0 = prof_begin(ctx);
             Args ac = a;
-            ac.evals = evals;  // (only instrumented builds write it)
-            if (ctx->gp_on) {
+            ac.evals = evals;
+            {
                 hipEvent_t e1 = prof_begin(ctx);
                 if (ctx->gp_np > 0)
-                    LAUNCH_TEX(k_gp_cost, dim3(blocks_for((size_t)ctx->gp_np, BLOCK)), dim3(BLOCK), gp_cost_lds_bytes(a.N), s, ac,
+                    LAUNCH_TEX_SA(k_gp_cost, dim3(blocks_for((size_t)ctx->gp_np, BLOCK)), dim3(BLOCK), gp_cost_lds_bytes(a.N), s, ac,
                                (const int2 *)ctx->gp_plist.p, ctx->gp_np, (float *)ctx->gp_pcost.p);
                 prof_end(ctx, e1, APD_PROF_GP_COST, ctx->gp_np);
                 e1 = prof_begin(ctx);
-                LAUNCH_TEX(k_weak_cand_g, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), 0, s, ac, (const int *)ctx->wlist.p, nw,
-                           (const uint8_t *)ctx->gp_cb.p, (float *)ctx->wcand.p, (uint8_t *)ctx->wdone.p, wc);
+                LAUNCH_TEX_SA(k_weak_cand_g, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), 0, s, ac, (const int *)ctx->wlist.p, nw,
+                           (const uint8_t *)ctx->gp_cb.p, (float *)ctx->wcand.p, wc);
                 prof_end(ctx, e1, APD_PROF_WEAK_CAND_G, nw);
                 e1 = prof_begin(ctx);
                 hipLaunchKernelGGL(k_weak_cand_comb, dim3(2 * blocks_for((size_t)nw, VM_P)), dim3(BLOCK), 0, s, ac,
                                    (const int *)ctx->wlist.p, nw, (const uint8_t *)ctx->gp_cb.p, (const uint8_t *)ctx->gp_cb.p + wc,
                                    (const uint32_t *)ctx->gp_pidx.p, (const float *)ctx->gp_pcost.p, (float *)ctx->wcand.p, wc);
                 prof_end(ctx, e1, APD_PROF_WEAK_CAND_COMB, nw);
-            } else {
-                LAUNCH_TEX(k_weak_cand_vm, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK),
-                           (ctx->args.tex_f16 ? pk_lds_bytes<true>() : pk_lds_bytes<false>()), s, ac,
-                           (const int *)ctx->wlist.p, nw, (float *)ctx->wcand.p, (uint8_t *)ctx->wdone.p, wc);
             }
-            prof_end(ctx, e0, APD_PROF_WEAK_CAND, nw);
             cand = (const float *)ctx->wcand.p;
         }
         for (int colour = 0; colour < 2; ++colour) {
@@ -5398,14 +4124,11 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             aw.evals = evals;
             if (!(ctx->wcur_fresh && iter == 0)) aw.wcur = nullptr;
             e0 = prof_begin(ctx);
-            // k_sweep_weak_vm's small cost table: every pixel's candidates are in `cand`
-            const bool direct = cand != nullptr && (ctx->gp_on || !a.sa_any);
-            if (ctx->sweep_vm)
-                LAUNCH_TEX(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N, direct) : wv_lds_bytes<false>(a.N, direct)), s,
-                           aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, (const uint8_t *)ctx->wdone.p, wc, (int)direct);
-            else
-                LAUNCH_TEX(k_sweep_weak, dim3(group_blocks(n, a.N)), dim3(BLOCK), 0, s, a,
-                           (const int *)list_ptr(ctx, 2 + colour), n, iter);
+            // k_sweep_weak_vm's small cost table when every pixel's candidates are in `cand`
+            const bool direct = cand != nullptr;
+            LAUNCH_TEX_SA(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
+                       (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N, direct) : wv_lds_bytes<false>(a.N, direct)), s,
+                       aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
             prof_end(ctx, e0, APD_PROF_WEAK_SWEEP, n);
         }
         if ((st = check_launch(ctx, "weak sweep"))) return st;
@@ -5431,7 +4154,7 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
     if (ctx->want_curve && ctx->curve.p) a.curve = devptr<decltype(a.curve)>(ctx->curve.p);
     a.lr_ncc = nullptr;
     a.lr_geo = nullptr;
-    if (ctx->sweep_vm && ctx->lr_handover && ctx->lrs_need > 0 && ctx->lrs.p && ctx->lrs.bytes >= ctx->lrs_need) {
+    if (ctx->lr_handover && ctx->lrs_need > 0 && ctx->lrs.p && ctx->lrs.bytes >= ctx->lrs_need) {
         // DepthToWeak hands LocalRefine the NCC-Old / geometric terms of the 11 samples they share
         // (buffer sized by apd_set_problem; without it LocalRefine evaluates them itself)
         const size_t plane = ctx->lrs_need / (sizeof(float) * (a.geom ? 2 : 1));
@@ -5439,27 +4162,20 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
         a.lr_geo = a.geom ? devptr<decltype(a.lr_geo)>((float *)ctx->lrs.p + plane) : nullptr;
     }
     {
-        if (ctx->sweep_vm) {
-            const int tw = ctx->dw_tile_w, th = VM_P / tw;
-            const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
-            const int dwc = dw_chunk(a.N, a.geom != 0, sa_lds_bytes(a));
-            Args ad = a;
-            ad.evals = (ctx->prof && ctx->evals.p) ? (APD_G unsigned long long *)ctx->evals.p : nullptr;
-            hipEvent_t e0 = prof_begin(ctx);
-            LAUNCH_TEX_SA(k_depth_to_weak_vm, dim3(nb), dim3(VM_BLOCK), dw_lds_bytes(a.N, a.geom != 0, dwc) + sa_lds_bytes(a), s, ad, dwc, tw);
-            prof_end(ctx, e0, APD_PROF_DEPTH_TO_WEAK, a.HW);
-        } else {
-            const size_t lds = group_lds_bytes(a.N, 61 + 36);
-            LAUNCH_TEX(k_depth_to_weak, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), lds, s, a);
-        }
+        const int tw = ctx->dw_tile_w, th = VM_P / tw;
+        const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
+        const int dwc = dw_chunk(a.N, a.geom != 0, sa_lds_bytes(a));
+        Args ad = a;
+        ad.evals = (ctx->prof && ctx->evals.p) ? (APD_G unsigned long long *)ctx->evals.p : nullptr;
+        hipEvent_t e0 = prof_begin(ctx);
+        LAUNCH_TEX_SA(k_depth_to_weak_vm, dim3(nb), dim3(VM_BLOCK), dw_lds_bytes(a.N, a.geom != 0, dwc) + sa_lds_bytes(a), s, ad, dwc, tw);
+        prof_end(ctx, e0, APD_PROF_DEPTH_TO_WEAK, a.HW);
     }
     if (a.geom || a.use_apd) hipLaunchKernelGGL(k_confidence, dim3(gpx), dim3(BLOCK), 0, s, a);
-    if (ctx->sweep_vm) {
+    {
         const int tw = ctx->dw_tile_w, th = VM_P / tw;
         const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
         LAUNCH_TEX_SA(k_local_refine_vm, dim3(nb), dim3(VM_BLOCK), lr_lds_bytes(a.N) + sa_lds_bytes(a), s, a, lr_chunk(a.N), tw);
-    } else {
-        LAUNCH_TEX(k_local_refine, dim3(group_blocks(a.HW, a.N)), dim3(BLOCK), group_lds_bytes(a.N, 36), s, a);
     }
     if ((st = check_launch(ctx, "finish"))) return st;
     return APD_OK;
@@ -5538,13 +4254,14 @@ int32_t apd_profile_reset(apd_ctx *ctx, int32_t enable) {
     if (!ctx) return APD_EINVAL;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    for (auto &pe : ctx->prof_ev) { (void)hipEventDestroy(pe.e0); (void)hipEventDestroy(pe.e1); }
+    for (auto &pe : ctx->prof_ev) { ctx->prof_pool.push_back(pe.e0); ctx->prof_pool.push_back(pe.e1); }
     ctx->prof_ev.clear();
     ctx->prof = enable != 0;
     if (ctx->prof) {
-        int st = ensure(ctx, ctx->evals, APD_PROF_SLOTS * sizeof(unsigned long long));
+        const size_t bytes = (size_t)APD_PROF_SLOTS * APD_PROF_SPREAD * sizeof(unsigned long long);
+        int st = ensure(ctx, ctx->evals, bytes);
         if (st) return st;
-        HIP_OK(ctx, hipMemsetAsync(ctx->evals.p, 0, APD_PROF_SLOTS * sizeof(unsigned long long), ctx->stream));
+        HIP_OK(ctx, hipMemsetAsync(ctx->evals.p, 0, bytes, ctx->stream));
     }
     return APD_OK;
 }
@@ -5553,9 +4270,14 @@ int32_t apd_profile_counters(apd_ctx *ctx, int64_t *counts, int32_t n) {
     if (!ctx || !counts || n < 0) return APD_EINVAL;
     (void)hipSetDevice(ctx->device);
     HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
-    unsigned long long c[APD_PROF_SLOTS] = {};
-    if (ctx->evals.p) HIP_OK(ctx, hipMemcpy(c, ctx->evals.p, sizeof(c), hipMemcpyDeviceToHost));
-    for (int i = 0; i < n; ++i) counts[i] = i < APD_PROF_SLOTS ? (int64_t)c[i] : 0;
+    std::vector<unsigned long long> c((size_t)APD_PROF_SLOTS * APD_PROF_SPREAD, 0ull);
+    if (ctx->evals.p) HIP_OK(ctx, hipMemcpy(c.data(), ctx->evals.p, c.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) {
+        int64_t t = 0;
+        if (i < APD_PROF_SLOTS)
+            for (int r = 0; r < APD_PROF_SPREAD; ++r) t += (int64_t)c[(size_t)r * APD_PROF_SLOTS + i];
+        counts[i] = t;
+    }
     return APD_OK;
 }
 
@@ -5571,12 +4293,17 @@ int32_t apd_profile_kernel(apd_ctx *ctx, int32_t kind, double *ms_total, int64_t
     double tot = 0.0;
     int64_t nl = 0, px = 0;
     for (auto &pe : ctx->prof_ev) {
-        if (pe.kind != kind) continue;
+        // APD_PROF_WEAK_CAND: the three candidate kernels together (one launch = one k_weak_cand_g)
+        const bool sub = kind == APD_PROF_WEAK_CAND &&
+                         (pe.kind == APD_PROF_GP_COST || pe.kind == APD_PROF_WEAK_CAND_G || pe.kind == APD_PROF_WEAK_CAND_COMB);
+        if (pe.kind != kind && !sub) continue;
         float ms = 0.0f;
         (void)hipEventElapsedTime(&ms, pe.e0, pe.e1);
         tot += ms;
-        ++nl;
-        px += pe.px;
+        if (!sub || pe.kind == APD_PROF_WEAK_CAND_G) {
+            ++nl;
+            px += pe.px;
+        }
     }
     if (ms_total) *ms_total = tot;
     if (launches) *launches = nl;

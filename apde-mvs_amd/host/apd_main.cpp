@@ -266,16 +266,26 @@ struct DevStore {
     std::map<int, Map> pend_depth, pend_planes;  // Jacobi: this pass's outputs until commit()
     Map scratch;                                 // resized priors of one problem
     long uploaded = 0;                           // bytes copied from the host (images)
+    // bytes held; an allocation that fails (or would pass APD_DEVICE_STATE_CAP_MB, a test hook) makes
+    // the caller fall back to the host path for that image / problem / view
+    size_t used = 0, cap = (size_t)-1;
 
     bool reserve(Map &m, size_t bytes) {
         if (m.p && m.bytes >= bytes) return true;
         release(m);
-        if (apd_device_alloc(ctx, bytes, &m.p) != APD_OK) return false;
+        if (used + bytes > cap || apd_device_alloc(ctx, bytes, &m.p) != APD_OK) {
+            m = Map{};
+            return false;
+        }
         m.bytes = bytes;
+        used += bytes;
         return true;
     }
     void release(Map &m) {
-        if (m.p) apd_device_free(ctx, m.p);
+        if (m.p) {
+            apd_device_free(ctx, m.p);
+            used -= m.bytes;
+        }
         m = Map{};
     }
     void release_all(std::map<int, Map> &ms) {
@@ -303,11 +313,25 @@ struct DevStore {
         if (apd_device_resize_nearest(ctx, m.p, m.w, m.h, dst, w, h, elem) != APD_OK) return nullptr;
         return dst;
     }
-    // device buffers for view `id`'s new maps at w x h
+    // view `id` leaves the device state (HBM exhausted): every later problem reads its priors from
+    // the store, which always holds the same values (the files are written either way)
+    void forget(int id) {
+        for (auto *ms : {&depth, &planes, &pend_depth, &pend_planes}) {
+            auto it = ms->find(id);
+            if (it != ms->end()) {
+                release(it->second);
+                ms->erase(it);
+            }
+        }
+    }
+    // device buffers for view `id`'s new maps at w x h (false: no room, the view was forgotten)
     bool output(int id, bool pending, int w, int h, float **d, float **pl) {
         Map &md = (pending ? pend_depth : depth)[id], &mp = (pending ? pend_planes : planes)[id];
         const size_t n = (size_t)w * h;
-        if (!reserve(md, n * sizeof(float)) || !reserve(mp, n * 4 * sizeof(float))) return false;
+        if (!reserve(md, n * sizeof(float)) || !reserve(mp, n * 4 * sizeof(float))) {
+            forget(id);
+            return false;
+        }
         md.w = mp.w = w;
         md.h = mp.h = h;
         *d = static_cast<float *>(md.p);
@@ -483,7 +507,10 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     if (dev) {
         for (int i = 0; i < NI; ++i) {
             img_ptrs[i] = dev->image(dense + "/images/" + format_index(ids[i]) + pb.img_ext, *scaled[i]);
-            if (!img_ptrs[i]) { SAY("device image upload failed: " << apd_last_error(ctx)); return false; }
+            if (!img_ptrs[i]) {  // no room in HBM: this image is uploaded per problem, as the reference does
+                dev->images.erase(dense + "/images/" + format_index(ids[i]) + pb.img_ext);
+                img_ptrs[i] = scaled[i]->img.data();
+            }
         }
         auto held = [](const std::map<int, DevStore::Map> &ms, int id) {
             auto it = ms.find(id);
@@ -494,17 +521,15 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
         if (dev_priors && need_planes) dev_priors = held(dev->planes, ids[0]);
         if (dev_priors) {
             const size_t slots = need_depths ? (size_t)NI : 0;
-            if (!dev->reserve(dev->scratch, HW * sizeof(float) * (slots + 4))) {
-                SAY("device scratch allocation failed: " << apd_last_error(ctx));
-                return false;
-            }
+            // (no room for the resized priors in HBM: this problem reads them from the store)
+            if (!dev->reserve(dev->scratch, HW * sizeof(float) * (slots + 4))) dev_priors = false;
             uint8_t *s = static_cast<uint8_t *>(dev->scratch.p);
-            for (size_t i = 0; i < slots; ++i) {
+            for (size_t i = 0; i < slots && dev_priors; ++i) {
                 dep_ptrs[i] = static_cast<const float *>(
                     dev->fitted(dev->depth[ids[i]], width, height, 4, s + i * HW * sizeof(float)));
                 if (!dep_ptrs[i]) { SAY("device resize failed: " << apd_last_error(ctx)); return false; }
             }
-            if (need_planes) {
+            if (need_planes && dev_priors) {
                 dev_planes = static_cast<const float *>(
                     dev->fitted(dev->planes[ids[0]], width, height, 16, s + slots * HW * sizeof(float)));
                 if (!dev_planes) { SAY("device resize failed: " << apd_last_error(ctx)); return false; }
@@ -644,8 +669,10 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     if (st != APD_OK) { SAY("apd_get_results failed: " << apd_last_error(ctx)); return false; }
     if (dev) {  // this view's next priors, kept in HBM (Jacobi: visible after the pass, as the files)
         float *dd = nullptr, *dp = nullptr;
-        if (!dev->output(pb.ref_image_id, jacobi, width, height, &dd, &dp) ||
-            apd_result_device(ctx, dd, dp) != APD_OK) {
+        if (!dev->output(pb.ref_image_id, jacobi, width, height, &dd, &dp)) {
+            // HBM exhausted: the view's later priors come from the store (dev->forget)
+            SAY("device state full: view " << pb.ref_image_id << " falls back to the host store");
+        } else if (apd_result_device(ctx, dd, dp) != APD_OK) {
             SAY("apd_result_device failed: " << apd_last_error(ctx));
             return false;
         }
@@ -842,6 +869,7 @@ int main(int argc, char **argv) {
     if (ctxs.size() == 1 && !(getenv("APD_DEVICE_STATE") && std::string(getenv("APD_DEVICE_STATE")) == "0")) {
         drv.dev = std::make_unique<DevStore>();
         drv.dev->ctx = ctxs[0];
+        if (const char *e = getenv("APD_DEVICE_STATE_CAP_MB")) drv.dev->cap = (size_t)std::max(0L, atol(e)) << 20;
     }
     std::vector<Job> jobs(problems.size());
     for (size_t i = 0; i < problems.size(); ++i) jobs[i].pb = problems[i];

@@ -1,4 +1,6 @@
-// capi.cpp — C entry points over the host helpers, for the CPU tests (tests/test_host.py) only.
+// capi.cpp -- C entry points over the host helpers (image decode, OpenCV-rule resize, cam.txt / pair.txt
+// parsing) as libapdhost.so: used by the multi-process scan runner (apde-mvs_amd/scan_runner.py) and by
+// the CPU tests (tests/test_host.py).
 #include <cstring>
 #include <string>
 

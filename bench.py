@@ -22,7 +22,7 @@ timing barriers and a max-reduction of the elapsed time (no data-path collective
 
 Besides the headline the JSON line carries:
   roofline      the dominant kernels of the step, the Weak sweep (the anchor candidates -- k_gp_cost +
-                k_weak_cand_g + k_weak_cand_comb, or k_weak_cand_vm with SA masks -- + 2 x k_sweep_weak_vm,
+                k_weak_cand_g + k_weak_cand_comb -- + 2 x k_sweep_weak_vm,
                 95 % of it at C3): algorithmic FP32 flops = NCC-New evaluations x 4038 +
                 geometric terms x 80, both counted on the device for the evaluations
                 CheckerboardPropagationWeak uses (apd_profile_counters), / their summed launch time from

@@ -206,7 +206,7 @@ int32_t apd_get_timing(apd_ctx *ctx, apd_timing *timing);
 #define APD_PROF_STRONG_SWEEP 0 /* k_sweep_strong_vm (CheckerboardPropagationStrong, APD.cu:1098-1440) */
 #define APD_PROF_RANSAC_FIT 1   /* k_ransac_fit (RANSACToGetFitPlane, APD.cu:2486-2598)             */
 #define APD_PROF_WEAK_CAND 2    /* the Weak sweep's anchor candidates: k_gp_cost + k_weak_cand_g +
-                                   k_weak_cand_comb (pair table), or k_weak_cand_vm                  */
+                                   k_weak_cand_comb (the image-wide pair table)                      */
 #define APD_PROF_WEAK_SWEEP 3   /* k_sweep_weak_vm (CheckerboardPropagationWeak, APD.cu:1442-1615)   */
 #define APD_PROF_DEPTH_TO_WEAK 4 /* k_depth_to_weak_vm (DepthToWeak, APD.cu:2103-2250)                */
 #define APD_PROF_GP_COST 5      /* k_gp_cost alone (pair windows, inside APD_PROF_WEAK_CAND)         */
@@ -223,7 +223,7 @@ int32_t apd_profile_query(apd_ctx *ctx, double *sweep_ms_total, int64_t *sweep_l
        plane + refinement candidates of views with weight > 0);
    [1] NCC-New evaluations of the Weak sweep: valid anchor candidates x N + current plane x views
        with weight > 0 (the values CheckerboardPropagationWeak needs, however the engine obtained
-       them: shared anchor windows in k_weak_cand_vm, RandomInitialization's kept costs, or the
+       them: the image-wide pair table, RandomInitialization's kept costs, or the
        sweep itself), plus the fit-plane and refinement-candidate evaluations of views with weight
        > 0 the sweep actually issued (those its exact early exit proves unnecessary are not counted);
    [2] geometric-consistency terms of the same evaluations (APD.cu:1561, 1583, 1037, 1079);

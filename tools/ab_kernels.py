@@ -22,7 +22,9 @@ engs = [make_engine(p) for p in sys.argv[1:]]
 ids = [0] + [j for j, _ in sc.pairs[0]][:N]
 priors = bench.first_init_priors(engs[0][1], sc, ids, N)
 arr = bench.final_round_problem(sc, priors, 0, N)
-kinds = {"strong": A.PROF_STRONG_SWEEP, "ransac": A.PROF_RANSAC_FIT, "cand": A.PROF_WEAK_CAND, "weak": A.PROF_WEAK_SWEEP}
+kinds = {"strong": A.PROF_STRONG_SWEEP, "ransac": A.PROF_RANSAC_FIT, "cand": A.PROF_WEAK_CAND, "weak": A.PROF_WEAK_SWEEP,
+         "gp_cost": A.PROF_GP_COST, "cand_g": A.PROF_WEAK_CAND_G, "comb": A.PROF_WEAK_CAND_COMB,
+         "dtw": A.PROF_DEPTH_TO_WEAK}
 for rnd in range(2):
     for name, e in engs:
         e.set_problem(arr)

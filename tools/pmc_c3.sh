@@ -5,11 +5,11 @@
 # its own timeout; stops at the first failure. Summarise with tools/pmc_json.py.
 set -e
 OUT=${1:-gpurun_out/pmc_c3}
-RE=${2:-"k_sweep_weak_vm|k_weak_cand_vm"}
+RE=${2:-"k_sweep_weak_vm|k_weak_cand_g|k_gp_cost"}
 EXTRA="${*:3}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-CMD="python3 bench.py --steps 3 --warmup 0 --no-cpu-baseline --end-to-end 0 --c2 0 --rich 0 $EXTRA"
+CMD="python3 bench.py --steps 3 --warmup 0 --no-cpu-baseline --end-to-end 0 --c2 0 --rich 0 --sa 0 $EXTRA"
 i=0
 for grp in \
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU" \

@@ -49,3 +49,24 @@ if ht:
           "results %.2f epilogue %.2f emit %.2f" % (a[0], a[1], a[2], a[3], a[2] - a[3], a[4], a[5], a[6]), flush=True)
 print(f"scan {W}x{H} x{V} views: wall {wall:.1f} s, problems {len(rpm)}, RunPatchMatch total {sum(rpm)/1e3:.1f} s, "
       f"per-problem cost total {sum(cost)/1e3:.1f} s, host overhead {wall - sum(rpm)/1e3:.1f} s", flush=True)
+# per round / pass: summed RunPatchMatch time and problem count, in log order
+cur_round, cur_pass, per = None, None, {}
+for line in out.stdout.splitlines():
+    m = re.match(r"=+ Round (\d+) =+", line)
+    if m:
+        cur_round = int(m.group(1))
+        continue
+    m = re.match(r"=+ iteration (\d+)=+", line)
+    if m:
+        cur_pass = int(m.group(1))
+        continue
+    m = re.match(r"RunPatchMatch time: (\d+) ms", line)
+    if m:
+        k = (cur_round, cur_pass)
+        t, n = per.get(k, (0, 0))
+        per[k] = (t + int(m.group(1)), n + 1)
+for (r, pss), (t, n) in sorted(per.items(), key=lambda kv: (kv[0][0] or 0, kv[0][1] or 0)):
+    print(f"round {r} pass {pss}: {n} problems, RunPatchMatch {t / 1e3:.2f} s ({t / max(n, 1):.0f} ms per problem)", flush=True)
+for r in sorted({k[0] for k in per}, key=lambda x: x or 0):
+    t = sum(v[0] for k, v in per.items() if k[0] == r)
+    print(f"round {r}: RunPatchMatch {t / 1e3:.2f} s", flush=True)
