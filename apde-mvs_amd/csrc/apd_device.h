@@ -887,13 +887,17 @@ __device__ __forceinline__ float ncc_old_fast(const Args &a, int px, int py, int
 
 
 
-// ComputeGeomConsistencyCost (APD.cu:865-902)
-__device__ __forceinline__ float geom_cost(const Args &a, int px, int py, int s, float4 pl) {
+// ComputeGeomConsistencyCost (APD.cu:865-902). geom_cost_p: from the view-independent world point
+// P = world_point(ref, depth_from_plane(plane)) onwards (a kernel scoring one plane in several views
+// computes P once); geom_cost: the whole statement sequence.
+__device__ __forceinline__ void geom_point(const Args &a, int px, int py, float4 pl, float P[3]) {
+    const APD_C Cam &rc = a.cams[0];
+    float depth = depth_from_plane(rc, pl, px, py);
+    world_point(rc, (float)px, (float)py, depth, P);
+}
+__device__ __forceinline__ float geom_cost_p(const Args &a, int px, int py, int s, const float P[3]) {
     const APD_C Cam &rc = a.cams[0];
     const APD_C Cam &sc = a.cams[s];
-    float depth = depth_from_plane(rc, pl, px, py);
-    float P[3];
-    world_point(rc, (float)px, (float)py, depth, P);
     float sx, sy, sd;
     project_cam(P, sc, sx, sy, sd);
     float src_depth = a.depth[(size_t)s * a.HW + trunc_clamp(sy, a.H) * a.W + trunc_clamp(sx, a.W)];
@@ -905,6 +909,11 @@ __device__ __forceinline__ float geom_cost(const Args &a, int px, int py, int s,
     float dx = (float)px - bx, dy = (float)py - by;
     float e = sqrtf(dx * dx + dy * dy);
     return fminf(3.0f, e);
+}
+__device__ __forceinline__ float geom_cost(const Args &a, int px, int py, int s, float4 pl) {
+    float P[3];
+    geom_point(a, px, py, pl, P);
+    return geom_cost_p(a, px, py, s, P);
 }
 
 }  // namespace apd

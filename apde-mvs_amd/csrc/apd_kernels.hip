@@ -2683,7 +2683,7 @@ struct DwLds {
 // per-(disparity, pixel) plane terms of the chunk [3][chunk][64] fp32 (+ [chunk][64] plane w with
 // geometric consistency) and evaluation flags [chunk][64] u8; the chunk is the largest that keeps
 // the workgroup within DW_LDS_BUDGET
-static inline size_t dw_per_disp(int N, bool geom) { return (size_t)N * VM_P * sizeof(float) + (size_t)VM_P * (13 + (geom ? 4 : 0)); }
+static inline size_t dw_per_disp(int N, bool geom) { return (size_t)N * VM_P * sizeof(float) + (size_t)VM_P * (13 + (geom ? 12 : 0)); }
 static inline int dw_chunk(int N, bool geom, size_t extra) {
     const long fixed = (long)(sizeof(DwLds) + (size_t)2 * N * VM_P + extra);
     return std::max(1, std::min(61, (int)((DW_LDS_BUDGET - fixed) / (long)dw_per_disp(N, geom))));
@@ -2700,8 +2700,8 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
     uint8_t *vslot = wts + N * VM_P;                                 // [N][64] pixel slots per view
     const bool geom = a.geom != 0;
     float *ptm = reinterpret_cast<float *>(vslot + N * VM_P);         // [3][chunk][64] plane terms
-    float *ptw = ptm + 3 * chunk * VM_P;                              // [chunk][64] plane w (geom only)
-    uint8_t *pok = reinterpret_cast<uint8_t *>(ptw + (geom ? chunk * VM_P : 0));  // [chunk][64] evaluated
+    float *ptp = ptm + 3 * chunk * VM_P;                              // [3][chunk][64] the geometric term's world point
+    uint8_t *pok = reinterpret_cast<uint8_t *>(ptp + (geom ? 3 * chunk * VM_P : 0));  // [chunk][64] evaluated
     SaWin *saw = reinterpret_cast<SaWin *>(pok + chunk * VM_P);       // [64] when a.sa_any
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & (WAVE - 1);
@@ -2790,7 +2790,11 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 tp.w = dist2origin(cam0, xy & 0xFFFF, xy >> 16, pdepth, tp);
                 const float3 m = plane_terms(a, tp);
                 ptm[e] = m.x; ptm[chunk * VM_P + e] = m.y; ptm[2 * chunk * VM_P + e] = m.z;
-                if (geom) ptw[e] = tp.w;
+                if (geom) {  // (geom_cost's view-independent head, once per (disparity, pixel))
+                    float P[3];
+                    geom_point(a, xy & 0xFFFF, xy >> 16, tp, P);
+                    ptp[e] = P[0]; ptp[chunk * VM_P + e] = P[1]; ptp[2 * chunk * VM_P + e] = P[2];
+                }
             }
         }
         __syncthreads();
@@ -2833,9 +2837,8 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 }
                 float g = 0.0f;
                 if (eval && geom) {
-                    float4 tp = L.pl[q];
-                    tp.w = ptw[e];
-                    g = geom_cost(a, qx, qy, v + 1, tp);
+                    const float P[3] = {ptp[e], ptp[chunk * VM_P + e], ptp[2 * chunk * VM_P + e]};
+                    g = geom_cost_p(a, qx, qy, v + 1, P);
                 }
                 const int pd = d0 + dd - 30;
                 if (a.lr_ncc && eval && !slow && pd >= -5 && pd <= 5) {

@@ -363,18 +363,24 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     exchange = None
-    if world > 1:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"  # nccl == RCCL on ROCm
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-        dist.init_process_group(backend)
-        exchange = Exchange(world, rank, f"cuda:{local}" if backend == "nccl" else None)
     on_device = torch.cuda.is_available()
-    run_fn = hip_run_fn(local, on_device)
+    # one GPU per rank; APD_SCAN_DEVICES=n maps the ranks onto n devices (rank r -> device r mod n: a test
+    # hook that runs several ranks on one GPU)
+    ndev = int(os.environ.get("APD_SCAN_DEVICES", "0")) or (torch.cuda.device_count() if on_device else 1)
+    dev_idx = local % max(1, ndev)
+    if world > 1:
+        # nccl == RCCL on ROCm; APD_SCAN_BACKEND=gloo exchanges the device tensors through gloo (test hook:
+        # RCCL refuses two ranks on one GPU)
+        backend = os.environ.get("APD_SCAN_BACKEND") or ("nccl" if on_device else "gloo")
+        if on_device:
+            torch.cuda.set_device(dev_idx)
+        dist.init_process_group(backend)
+        exchange = Exchange(world, rank, f"cuda:{dev_idx}" if on_device else None)
+    run_fn = hip_run_fn(dev_idx, on_device)
     run_scan(args.dense_folder, run_fn, rank, world, exchange, dataset=args.dataset,
              use_sa=args.use_sa.lower() in ("1", "true", "yes", "on"),
              use_impetus=args.use_impetus.lower() in ("1", "true", "yes", "on"), seed=args.seed,
-             device=f"cuda:{local}" if on_device else None)
+             device=f"cuda:{dev_idx}" if on_device else None)
     if exchange:
         dist.destroy_process_group()
     if rank == 0:

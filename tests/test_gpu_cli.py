@@ -147,3 +147,27 @@ def test_scan_runner_device_resident(scan, engine, tmp_path):
     SR.run_scan(folder, SR.hip_run_fn(0, on_device=True), 0, 1, None, device="cuda:0")
     expected = HS.run_schedule(folder, run_engine(engine), ordering="jacobi")
     check_outputs(folder, expected)
+
+
+def test_scan_runner_two_ranks_device_resident(scan, engine, tmp_path):
+    """Two scan_runner.py ranks (torch.distributed.run, both on GPU 0, states exchanged as device tensors
+    through gloo: RCCL refuses two ranks on one GPU) with the scan resident in HBM: the dynamic queue
+    splits every pass's views between the ranks, each problem's inputs are fresh torch / collective
+    outputs on the device (the library's stream waits for torch's), and the files equal the Jacobi
+    schedule restated on the host bit for bit."""
+    import shutil
+    import socket
+    import sys
+    folder = str(tmp_path / "run")
+    shutil.copytree(scan, folder)
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    env = dict(os.environ, APD_SCAN_BACKEND="gloo", APD_SCAN_DEVICES="1")
+    script = os.path.join(REPO, "apde-mvs_amd", "scan_runner.py")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), script, "--dense_folder", folder],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    expected = HS.run_schedule(folder, run_engine(engine), ordering="jacobi")
+    check_outputs(folder, expected)

@@ -13,7 +13,7 @@ extra = sys.argv[4:]
 sc = synth.make_scene(W, H, V - 1)
 print("scene generated", flush=True)
 folder = tempfile.mkdtemp(prefix="apd_scan_")
-HS.write_dense_folder(sc, folder, ext=".png", masks=True)
+HS.write_dense_folder(sc, folder, ext=".png", masks=os.environ.get("TIME_SCAN_SA", "1") == "1")  # TIME_SCAN_SA=0: no sa_masks/ (C3)
 from PIL import Image
 for f in sorted(os.listdir(os.path.join(folder, "images"))):  # re-encode as baseline JPEG
     p = os.path.join(folder, "images", f)
