@@ -1798,14 +1798,17 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
         const float4 cur = L.hyp[8 * VM_P + p1];
         float depth_now = depth_from_plane(cam0, cur, px1, py1);
         float4 pnow = cur;
+        bool taken = false;
         if ((L.flags[p1] >> mi) & 1u) {
             const float4 cnd = L.hyp[mi * VM_P + p1];
             const float db = depth_from_plane(cam0, cnd, px1, py1);
             if (db >= a.dmin && db <= a.dmax && fcm < cost_now) {
                 depth_now = db; pnow = cnd; cost_now = fcm;
                 a.sel[c1] = L.tsel[p1];
+                taken = true;
             }
         }
+        LANE_STAT(16, taken);  // (instrumented builds: pixels that take the best anchor hypothesis)
         L.pnow[p1] = pnow;
         L.st[0 * VM_P + p1] = depth_now;
         L.st[1 * VM_P + p1] = cost_now;
