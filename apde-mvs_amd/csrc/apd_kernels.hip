@@ -179,8 +179,10 @@ __global__ __launch_bounds__(BLOCK) void k_build_pairs(const float *__restrict__
 // Ordered compaction, one workgroup per image row.
 //   mode 0: colour `colour`, weak != WEAK, y < row_limit   (Strong sweep / filter pixel set)
 //   mode 1: colour `colour`, weak == WEAK, y < row_limit   (Weak sweep pixel set)
-//   mode 2: every pixel with weak == WEAK -> anchors_map (running row-major index, APD.cpp:627-640)
+//   mode 2: every pixel with weak == WEAK -> anchors_map (the WEAK index; see apd_stage_prepare)
+//   mode 3: every pixel with a WEAK index (the anchors export in the reference's row-major order)
 __device__ __forceinline__ bool list_pred(const Args &a, int mode, int colour, int x, int y) {
+    if (mode == 3) return a.amap[y * a.W + x] >= 0;
     const uint8_t w = a.weak[y * a.W + x];
     if (mode == 2) return w == APD_WEAK;
     if (y >= a.row_limit || (colour < 2 && ((x + y) & 1) != colour)) return false;  // colour 2: both
@@ -278,7 +280,37 @@ __global__ __launch_bounds__(BLOCK) void k_tile_fill(Args a, int mode, int colou
     __syncthreads();
     int wo = 0;
     for (int k = 0; k < wv; ++k) wo += wcnt[k];
-    if (p) out[offs[blockIdx.x] + wo + __popcll(m & ((1ull << lane) - 1ull))] = y * a.W + x;
+    const int pos = offs[blockIdx.x] + wo + __popcll(m & ((1ull << lane) - 1ull));
+    if (mode == 2) {  // a map: position in tile order, -1 elsewhere
+        if (x < a.W && y < a.H) out[y * a.W + x] = p ? pos : -1;
+    } else if (p) {
+        out[pos] = y * a.W + x;
+    }
+}
+// The anchors export (APD.cu:2614-2626 writes them by anchors_map, the row-major WEAK index): row y's
+// WEAK pixels in row order, from the row offsets of mode 3, copied from their tile-order slots.
+__global__ __launch_bounds__(BLOCK) void k_anchor_export(Args a, const int *__restrict__ row_off, short2 *__restrict__ dst) {
+    const int y = blockIdx.x;
+    __shared__ int wcnt[BLOCK / WAVE];
+    int off = row_off[y];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int x0 = 0; x0 < a.W; x0 += BLOCK) {
+        const int x = x0 + threadIdx.x;
+        const int wi = x < a.W ? a.amap[y * a.W + x] : -1;
+        const unsigned long long m = __ballot(wi >= 0);
+        if (lane == 0) wcnt[wv] = __popcll(m);
+        __syncthreads();
+        int wo = 0;
+        for (int k = 0; k < wv; ++k) wo += wcnt[k];
+        const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        if (wi >= 0) {
+            const int r = off + wo + __popcll(m & ((1ull << lane) - 1ull));
+#pragma unroll
+            for (int k = 0; k < 9; ++k) dst[(size_t)r * 9 + k] = a.anchors[(size_t)wi * 9 + k];
+        }
+        off += tot;
+        __syncthreads();
+    }
 }
 
 // XCD-aware workgroup order (cdna_hip_programming.md §5.5 T1): workgroups are dealt round-robin to
@@ -985,7 +1017,10 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     uint64_t defer[2] = {0, 0};  // up to 128 tasks per wave (9 * 31 / VM_WAVES)
     uint32_t issued = 0;         // NCC-Old evaluations of this lane (profiling count, a.evals)
     // tasks in view-major order, dealt round-robin over the waves (the 4 waves of a workgroup sample
-    // one source image around the same pixels at once: L1 sharing); (h, v) -> table index h * N + v
+    // one source image around the same pixels at once: L1 sharing); (h, v) -> table index h * N + v.
+    // (Measured and not kept: the current plane (h = 8) evaluated after the view selection for the
+    // weighted views only, as the Weak sweep does: fewer evaluations, but +3 % on the texture-rich C3
+    // pass -- the extra phase loses the hypotheses' shared source lines.)
     for (int u = wave, k = 0; u < 9 * N; u += VM_WAVES, ++k) {
         const int v = u / 9, h = u - 9 * v, t = h * N + v;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;  // float cost_array[8][32] = {2.0f} (APD.cu:1120)
@@ -1288,8 +1323,8 @@ __device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
 // this window (`live` false) run on a parked homography and discard the sums.
 // Reference taps: tap tk of the window at rb[tk * rs] (WvRefT: &rref[tap0 * VM_P + p], VM_P).
 // The IEEE statement of an NCC-New window's taps (lanes whose window fails window_rcp_ok).
-template <bool F16, int NW, int INC>
-__device__ __forceinline__ void ncc_new_window_slow(const Args &a, const typename std::conditional<F16, _Float16, float>::type *rb,
+template <bool F16, int NW, int INC, class RT>
+__device__ __forceinline__ void ncc_new_window_slow(const Args &a, const RT *rb,
                                                     int rs, uint64_t mask, const Hom &Hm, int ax, int ay, const SrcTex<F16> &Q,
                                                     float &ss, float &sss, float &srs) {
     const float Wm1 = (float)(a.W - 1), Hm1 = (float)(a.H - 1);
@@ -1316,8 +1351,10 @@ __device__ __forceinline__ void ncc_new_window_slow(const Args &a, const typenam
         }
     }
 }
-template <bool F16, int NW, int INC>
-__device__ __forceinline__ void ncc_new_window(const Args &a, const typename std::conditional<F16, _Float16, float>::type *rb,
+// RT: the reference taps' type in LDS -- fp16 (exact, see apd_set_problem) where LDS is tight, fp32
+// where it is not (one conversion less per tap)
+template <bool F16, int NW, int INC, class RT = typename std::conditional<F16, _Float16, float>::type>
+__device__ __forceinline__ void ncc_new_window(const Args &a, const RT *rb,
                                                int rs, uint64_t mask, const Hom &Hm, int ax, int ay, bool live,
                                                bool fast, const FastTex<F16, true> &T, const SrcTex<F16> &Q, float &ss,
                                                float &sss, float &srs) {
@@ -1387,7 +1424,7 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const typename std
             }
         }
     }
-    if (sm && live && !fast) ncc_new_window_slow<F16, NW, INC>(a, rb, rs, mask, Hm, ax, ay, Q, ss, sss, srs);
+    if (sm && live && !fast) ncc_new_window_slow<F16, NW, INC, RT>(a, rb, rs, mask, Hm, ax, ay, Q, ss, sss, srs);
 }
 
 
@@ -2453,6 +2490,7 @@ __device__ __forceinline__ float gp_combine(float cc, const float (&sc)[8]) {
 template <bool F16, bool SA>
 __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__restrict__ list, int count,
                                                           const uint8_t *__restrict__ cbw, float *__restrict__ out, int wc) {
+    // (fp16 reference taps when the images are: fp32 measured 6 % slower, profiles/r4_ab_cand_g_fp32_ref.txt)
     using RT = typename std::conditional<F16, _Float16, float>::type;
     __shared__ RT cref[36 * VM_P];
     __shared__ float csr[VM_P], csrr[VM_P];
@@ -2564,23 +2602,40 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
 // a thread per (pixel, candidate): few registers and many waves in flight for the pair-cost gathers.
 // `out` holds the centre cost (< 0: dead) and receives the candidate's cost in its place; the pixel's
 // used windows (wmw) say which of its 8 pair ids exist. Block = 4 candidates x 64 pixels of one group.
+// The block's pair ids ([WEAK index][window k][candidate h], 4 candidates = one 16-byte chunk per
+// (pixel, k)) are staged in LDS with 16-byte loads of whole chunks first: a thread's 8 ids lie 32 B
+// apart and the wave's 64 pixels 256 B apart, so loading them per thread issued 8 scattered 4-byte
+// gathers touching 64 lines each.
+#define COMB_STRIDE 33  // words per pixel slot in LDS (8 windows x 4 candidates, + 1 against bank conflicts)
 __global__ __launch_bounds__(BLOCK) void k_weak_cand_comb(Args a, const int *__restrict__ list, int count,
                                                           const uint8_t *__restrict__ cbw, const uint8_t *__restrict__ wmw,
                                                           const uint32_t *__restrict__ pidx,
                                                           const float *__restrict__ pcost, float *__restrict__ out, int wc) {
+    __shared__ uint32_t sid[VM_P * COMB_STRIDE];
     const int b = xcd_remap(blockIdx.x, gridDim.x);
-    const int h = ((b & 1) << 2) + (threadIdx.x >> 6);
-    const int i = (b >> 1) * VM_P + (threadIdx.x & (WAVE - 1));
+    const int h0 = (b & 1) << 2, hl = threadIdx.x >> 6, h = h0 + hl;
+    const int g0 = (b >> 1) * VM_P;
+    const int lane = threadIdx.x & (WAVE - 1);
+    for (int e = threadIdx.x; e < VM_P * 8; e += BLOCK) {
+        const int slot = e >> 3, k = e & 7;
+        if (g0 + slot < count) {
+            const int wi2 = a.amap[list[g0 + slot]];
+            const uint4 q = *reinterpret_cast<const uint4 *>(pidx + (size_t)wi2 * 64 + k * 8 + h0);
+            uint32_t *d = &sid[slot * COMB_STRIDE + k * 4];
+            d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
+        }
+    }
+    __syncthreads();
+    const int i = g0 + lane;
     if (i >= count) return;
     const int wi = a.amap[list[i]];
     if (!((cbw[wi] >> h) & 1u)) return;
     const int N = a.N, Np = (N + 3) & ~3;
     const uint32_t wm = wmw[wi];
-    const uint32_t *pp = pidx + (size_t)wi * 64 + h;  // [window k][candidate h]
     const float4 *pc4[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const uint32_t id = ((wm >> k) & 1u) ? pp[k * 8] : 0u;
+        const uint32_t id = ((wm >> k) & 1u) ? sid[lane * COMB_STRIDE + k * 4 + hl] : 0u;
         pc4[k] = reinterpret_cast<const float4 *>(pcost + (size_t)id * Np);
     }
     for (int v0 = 0; v0 < N; v0 += 4) {
@@ -3963,8 +4018,13 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
     ctx->gp_on = false;
     (void)hipEventRecord(ctx->ev[0], s);
     if (a.use_apd) {
-        // anchors_map from the input WEAK mask (APD.cpp:627-640)
-        if ((st = build_list(ctx, 2, 0, (int *)ctx->amap.p, (int *)ctx->totals.p + 4))) return st;
+        // anchors_map from the input WEAK mask (APD.cpp:627-640). The reference numbers the WEAK pixels
+        // row-major; here they are numbered in the sweep lists' tile order, so the per-WEAK-pixel
+        // arrays (anchors, the candidates' bits, pair ids and costs) are read and written in runs by
+        // the tile-ordered kernels (row-major, a 64-pixel list chunk scattered its 4-byte writes over
+        // 4 rows: k_weak_cand_comb wrote 2.2x its bytes). Only the anchors export sees the numbering,
+        // and apd_result restores the row-major order.
+        if ((st = build_tile_list(ctx, 2, 0, (int *)ctx->amap.p, (int *)ctx->totals.p + 4))) return st;
         if (ctx->near_levels) {
             hipLaunchKernelGGL(k_near_columns, dim3(blocks_for((size_t)ctx->near_levels * a.W, BLOCK)), dim3(BLOCK), 0, s, a,
                                ctx->near_levels, (uint8_t *)ctx->near_g.p);
@@ -4240,9 +4300,27 @@ int32_t apd_get_results(apd_ctx *ctx, const apd_outputs *out) {
     if (out->selected_views)
         HIP_OK(ctx, hipMemcpyAsync(out->selected_views, ctx->sel.p, HW * sizeof(uint32_t), hipMemcpyDefault, s));
     if (out->view_weights) HIP_OK(ctx, hipMemcpyAsync(out->view_weights, ctx->vw.p, HW * a.N, hipMemcpyDefault, s));
-    if (out->anchors && a.use_apd && ctx->weak_count > 0)
-        HIP_OK(ctx, hipMemcpyAsync(out->anchors, ctx->anchors.p, (size_t)ctx->weak_count * 9 * sizeof(short2),
-                                   hipMemcpyDefault, s));
+    if (out->anchors && a.use_apd && ctx->weak_count > 0) {
+        // the device keeps them by tile-order WEAK index: back to the row-major order of the export
+        const size_t nb = (size_t)ctx->weak_count * 9 * sizeof(short2);
+        void *tmp = nullptr;
+        if (hipMalloc(&tmp, nb) != hipSuccess) {
+            ctx->err = "hipMalloc(" + std::to_string(nb) + ") failed (anchors export)";
+            return APD_ENOMEM;
+        }
+        hipLaunchKernelGGL(k_list_count, dim3(a.H), dim3(BLOCK), 0, s, a, 3, 0, (int *)ctx->rowcnt.p);
+        hipLaunchKernelGGL(k_list_scan, dim3(1), dim3(1024), 0, s, (const int *)ctx->rowcnt.p, a.H, (int *)ctx->rowoff.p,
+                           (int *)ctx->totals.p + 6);
+        hipLaunchKernelGGL(k_anchor_export, dim3(a.H), dim3(BLOCK), 0, s, a, (const int *)ctx->rowoff.p, (short2 *)tmp);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(out->anchors, tmp, nb, hipMemcpyDefault, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        (void)hipFree(tmp);
+        if (e != hipSuccess) {
+            ctx->err = std::string("anchors export: ") + hipGetErrorString(e);
+            return APD_EDEVICE;
+        }
+    }
     if (out->reliable_curve && ctx->want_curve)
         HIP_OK(ctx, hipMemcpyAsync(out->reliable_curve, ctx->curve.p, HW * 61 * sizeof(float), hipMemcpyDefault, s));
     if (out->weak_count) *out->weak_count = ctx->weak_count;
