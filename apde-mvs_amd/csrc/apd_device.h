@@ -410,6 +410,16 @@ __device__ __forceinline__ float ncc_finalize(float sr, float srr, float ss, flo
     float vrs = sqrtf(var_ref * var_src);
     return fmaxf(0.0f, fminf(APD_COST_MAX, 1.0f - covar / vrs));
 }
+// ncc_finalize with its reference-side statements done beforehand (inv = 1 / wsum, srp = sr * inv,
+// var_ref = fmaf(-srp, srp, srr * inv)): the same values
+__device__ __forceinline__ float ncc_finalize_pre(float inv, float srp, float var_ref, float ss, float sss, float srs) {
+    ss *= inv; sss *= inv; srs *= inv;
+    float var_src = fmaf(-ss, ss, sss);
+    if (var_ref < 1e-5f || var_src < 1e-5f) return APD_COST_MAX;
+    float covar = fmaf(-srp, ss, srs);
+    float vrs = sqrtf(var_ref * var_src);
+    return fmaxf(0.0f, fminf(APD_COST_MAX, 1.0f - covar / vrs));
+}
 
 // Reference-side window of ComputeBilateralNCCOld (6x6, radius 5, step 2): fixed per pixel, so it is
 // gathered once per pixel into LDS (one copy per pixel, each of the pixel's N lanes fetching a share)

@@ -1277,7 +1277,9 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 template <bool F16>
 struct WvRefT {
     uint64_t tmask0[VM_P];       // SA tap masks (all ones without SA)
-    float wsr[9 * VM_P], wsrr[9 * VM_P];  // per window moments over its valid taps
+    // per window, the reference side of ncc_finalize over its valid taps, once per pixel instead of
+    // once per evaluation: 1 / wsum (0: empty window), sr / wsum, var_ref -- the same statements
+    float winv[9 * VM_P], wsrp[9 * VM_P], wvar[9 * VM_P];
     int anc[9 * VM_P];           // packed (x, y) of anchors 0..8, -1 = none
     uint32_t flags[VM_P];        // bits 0-8: hypothesis h present (anchor STRONG); 16-24: window k evaluated
                                  // (anchor present and SA label matches); 25-27: the best anchor
@@ -1286,7 +1288,6 @@ struct WvRefT {
     // the images are (exactly) fp16-representable, see apd_set_problem
     typename std::conditional<F16, _Float16, float>::type rref[108 * VM_P];
     uint16_t tmask[8 * VM_P];
-    uint8_t wsum[9 * VM_P];      // valid taps per window (<= 36)
     uint32_t box[2 * VM_P];      // bounding box of the anchors 0..8 (x0 | y0 << 16, x1 | y1 << 16)
 };
 // the Weak sweep's per-workgroup state: the reference side plus the hypotheses and per-pixel state
@@ -1301,9 +1302,10 @@ struct WvLdsT : WvRefT<F16> {
     int pxy[VM_P];               // packed (x, y) of pixel slot p (P5's packed items)
 };
 #define WV_CAND(L) ((L).hyp)
-// 53.2 KiB with the 9-slot cost table at N = 8 (fp16 reference taps): three workgroups per CU.
-static_assert(sizeof(WvLdsT<true>) + 9 * 8 * VM_P * sizeof(float) + 8 * VM_P <= 160 * 1024 / 3,
-              "k_sweep_weak_vm at N = 8 must fit three workgroups per CU (160 KiB LDS)");
+// 49.5 KiB with the direct 5-slot cost table at N = 10 (fp16 reference taps): three workgroups per CU.
+// (The sweep's own candidate path, a 9-slot table, runs two per CU from N = 8.)
+static_assert(sizeof(WvLdsT<true>) + 5 * 10 * VM_P * sizeof(float) + 10 * VM_P <= 160 * 1024 / 3,
+              "k_sweep_weak_vm (direct) at N = 10 must fit three workgroups per CU (160 KiB LDS)");
 // `direct` (the pair-table kernels handled every pixel): the sweep reads the anchor candidates'
 // costs from their buffer in P2 and its table holds [5][N][64] (current plane, fit plane,
 // refinement candidates) instead of [9][N][64]: 48 KiB at N = 10, three workgroups per CU instead of two.
@@ -1471,9 +1473,11 @@ __device__ __forceinline__ void wv_build_window(const Args &a, WvRefT<F16> &L, i
         srr = fmaf(r[tk], r[tk], srr);
         ws += 1.0f;
     }
-    L.wsr[k * VM_P + p1] = sr;
-    L.wsrr[k * VM_P + p1] = srr;
-    L.wsum[k * VM_P + p1] = (uint8_t)ws;
+    // (ncc_finalize's reference-side statements: inv = 1 / wsum, sr *= inv, srr *= inv, var_ref)
+    const float inv = 1.0f / ws, srp = sr * inv, srrp = srr * inv;
+    L.winv[k * VM_P + p1] = ws != 0.0f ? inv : 0.0f;
+    L.wsrp[k * VM_P + p1] = srp;
+    L.wvar[k * VM_P + p1] = fmaf(-srp, srp, srrp);
     if (k == 0) L.tmask0[p1] = mask;
     else L.tmask[(k - 1) * VM_P + p1] = (uint16_t)mask;
 }
@@ -1561,9 +1565,9 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
                                       SA ? (uint64_t)L.tmask[(k - 1) * VM_P + p] : 0x1FFull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
         if (!live) continue;
         if (nwc) { if (k == 0) ++*nwc; else ++*nwa; }  // (profiling: windows evaluated)
-        const float wsum = (float)L.wsum[k * VM_P + p];
-        if (wsum == 0.0f) continue;
-        const float c = ncc_finalize(L.wsr[k * VM_P + p], L.wsrr[k * VM_P + p], ss, sss, srs, wsum);
+        const float inv = L.winv[k * VM_P + p];
+        if (inv == 0.0f) continue;  // (empty window)
+        const float c = ncc_finalize_pre(inv, L.wsrp[k * VM_P + p], L.wvar[k * VM_P + p], ss, sss, srs);
         if (k == 0) {
             center_cost = c;
         } else {
