@@ -250,17 +250,39 @@ __global__ __launch_bounds__(BLOCK) void k_list_fill(Args a, int mode, int colou
 // List tiles: tw x th = 256 positions, visited in 4x4 micro-tiles (row-major inside the tile); a
 // sweep workgroup's 64 list entries are then a tw x th/2 region of one colour.
 #define TILE_POS 256
-__device__ __forceinline__ void tile_pixel(int tile, int tiles_x, int tw, int k, int &x, int &y) {
+// Tiles are visited in super-tiles of about TILE_SUPER_PX x TILE_SUPER_PX pixels (tiles row-major
+// inside, super-tiles row-major, partial ones at the right and bottom edges): the workgroups one XCD
+// runs at a time then cover a compact region instead of a strip of one tile row across the image, so
+// their windows in each source view stay within its L2 (XCD-aware dispatch gives each XCD a
+// contiguous run of the list). TILE_SUPER_PX 0: tiles row-major.
+#ifndef TILE_SUPER_PX
+#define TILE_SUPER_PX 128
+#endif
+__device__ __forceinline__ void tile_coords(int t, int tiles_x, int tiles_y, int tw, int &tx, int &ty) {
+    const int SX = TILE_SUPER_PX ? max(1, TILE_SUPER_PX / tw) : tiles_x;
+    const int SY = TILE_SUPER_PX ? max(1, TILE_SUPER_PX / (TILE_POS / tw)) : 1;
+    const int sy = t / (SY * tiles_x);                   // band of SY tile rows
+    const int rows = min(SY, tiles_y - SY * sy);         // tile rows in this band
+    const int r = t - sy * SY * tiles_x;
+    const int sx = r / (rows * SX);                      // super-tile within the band
+    const int cols = min(SX, tiles_x - SX * sx);
+    const int r2 = r - sx * rows * SX;
+    tx = SX * sx + r2 % cols;
+    ty = SY * sy + r2 / cols;
+}
+__device__ __forceinline__ void tile_pixel(int tile, int tiles_x, int tiles_y, int tw, int k, int &x, int &y) {
     const int micro = k >> 4, inner = k & 15, mx = tw >> 2;
     const int lx = ((micro % mx) << 2) + (inner & 3);
     const int ly = ((micro / mx) << 2) + (inner >> 2);
-    x = (tile % tiles_x) * tw + lx;
-    y = (tile / tiles_x) * (TILE_POS / tw) + ly;
+    int tx, ty;
+    tile_coords(tile, tiles_x, tiles_y, tw, tx, ty);
+    x = tx * tw + lx;
+    y = ty * (TILE_POS / tw) + ly;
 }
 __global__ __launch_bounds__(BLOCK) void k_tile_count(Args a, int mode, int colour, int tiles_x, int tw,
                                                     int *__restrict__ counts) {
     int x, y;
-    tile_pixel(blockIdx.x, tiles_x, tw, threadIdx.x, x, y);
+    tile_pixel(blockIdx.x, tiles_x, (int)gridDim.x / tiles_x, tw, threadIdx.x, x, y);
     const bool p = x < a.W && y < a.H && list_pred(a, mode, colour, x, y);
     __shared__ int wsum[BLOCK / WAVE];
     const int c = __popcll(__ballot(p));
@@ -271,7 +293,7 @@ __global__ __launch_bounds__(BLOCK) void k_tile_count(Args a, int mode, int colo
 __global__ __launch_bounds__(BLOCK) void k_tile_fill(Args a, int mode, int colour, int tiles_x, int tw,
                                                    const int *__restrict__ offs, int *__restrict__ out) {
     int x, y;
-    tile_pixel(blockIdx.x, tiles_x, tw, threadIdx.x, x, y);
+    tile_pixel(blockIdx.x, tiles_x, (int)gridDim.x / tiles_x, tw, threadIdx.x, x, y);
     const bool p = x < a.W && y < a.H && list_pred(a, mode, colour, x, y);
     __shared__ int wcnt[BLOCK / WAVE];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1310,8 +1332,11 @@ static_assert(sizeof(WvLdsT<true>) + 5 * 10 * VM_P * sizeof(float) + 10 * VM_P <
 // costs from their buffer in P2 and its table holds [5][N][64] (current plane, fit plane,
 // refinement candidates) instead of [9][N][64]: 48 KiB at N = 10, three workgroups per CU instead of two.
 template <bool F16>
+#ifndef APD_WV_LDS_PAD
+#define APD_WV_LDS_PAD 0  // experiments: extra LDS bytes per workgroup (fewer workgroups per CU)
+#endif
 static inline size_t wv_lds_bytes(int N, bool direct = false) {
-    return sizeof(WvLdsT<F16>) + (size_t)(direct ? 5 : 9) * N * VM_P * sizeof(float) + (size_t)N * VM_P;
+    return APD_WV_LDS_PAD + sizeof(WvLdsT<F16>) + (size_t)(direct ? 5 : 9) * N * VM_P * sizeof(float) + (size_t)N * VM_P;
 }
 __device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
     const long idx = (long)y * a.W + x;
@@ -1536,7 +1561,23 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
         bool live = has;
         if (has) {
             float asx, asy;
-            project(Hm, (float)ax, (float)ay, asx, asy);
+            if constexpr (BOX) {
+                // the anchor lies in the proven box: rcp_newton(Z) is the correctly rounded 1 / Z there,
+                // so X * it is project()'s value without the IEEE division (lanes outside the proof
+                // take the division)
+                const float X = fmaf(Hm.h[1], (float)ay, fmaf(Hm.h[0], (float)ax, Hm.h[2]));
+                const float Y = fmaf(Hm.h[4], (float)ay, fmaf(Hm.h[3], (float)ax, Hm.h[5]));
+                const float Z = fmaf(Hm.h[7], (float)ay, fmaf(Hm.h[6], (float)ax, Hm.h[8]));
+                float iz = rcp_newton(Z);
+                if (__builtin_amdgcn_ballot_w64(!box_ok)) {
+                    const float q = 1.0f / Z;
+                    if (!box_ok) iz = q;
+                }
+                asx = X * iz;
+                asy = Y * iz;
+            } else {
+                project(Hm, (float)ax, (float)ay, asx, asy);
+            }
             if (asx < 0 || asy < 0 || asx >= (float)W || asy >= (float)H) {
                 live = false;
                 if (k != 0) {
