@@ -97,6 +97,10 @@ struct Args {
     // RandomInitialization -> first Weak sweep (null = off): each WEAK pixel's NCC-New of its initial
     // plane per view, [N][H*W], NaN where it read an anchor's selected views
     APD_G float *wcur;
+    // anchor-window reference records (APD passes): per pixel q, [0] the 3x3 / step-5 window around q
+    // unfiltered, [1] filtered by q's own SA label (when the problem has labels): taps, tap mask and
+    // ncc_finalize's reference-side terms -- see AncRec in apd_kernels.hip
+    const APD_G uint4 *arec;
 };
 
 // ---------------------------------------------------------------------------------------------

@@ -1296,25 +1296,29 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 // ---------------------------------------------------------------------------------------------
 // NCC-New reference side of a pixel slot (anchors, window taps, SA tap masks, moments): shared by the
 // Weak sweep and RandomInitialization under APD
-template <bool F16>
+// NWIN: windows held in LDS -- 9 (RandomInitialization), or 1 (the Weak sweep: the centre window;
+// the anchor windows' reference side comes from the image-wide records AncRec, which depend on the
+// anchor alone, so 16 KiB less LDS per workgroup and four workgroups per CU instead of three)
+template <bool F16, int NWIN = 9>
 struct WvRefT {
     uint64_t tmask0[VM_P];       // SA tap masks (all ones without SA)
     // per window, the reference side of ncc_finalize over its valid taps, once per pixel instead of
     // once per evaluation: 1 / wsum (0: empty window), sr / wsum, var_ref -- the same statements
-    float winv[9 * VM_P], wsrp[9 * VM_P], wvar[9 * VM_P];
+    float winv[NWIN * VM_P], wsrp[NWIN * VM_P], wvar[NWIN * VM_P];
     int anc[9 * VM_P];           // packed (x, y) of anchors 0..8, -1 = none
     uint32_t flags[VM_P];        // bits 0-8: hypothesis h present (anchor STRONG); 16-24: window k evaluated
                                  // (anchor present and SA label matches); 25-27: the best anchor
-                                 // hypothesis (Weak sweep P2a); 31: refine (fit normal != 0)
+                                 // hypothesis (Weak sweep P2a); 29: the pixel has an SA label (its anchor
+                                 // windows are filtered); 31: refine (fit normal != 0)
     // [tap][p]: window 0 taps 0..35 (6x6, step 2), anchor k taps 36+9(k-1).. (3x3, step 5); fp16 when
     // the images are (exactly) fp16-representable, see apd_set_problem
-    typename std::conditional<F16, _Float16, float>::type rref[108 * VM_P];
-    uint16_t tmask[8 * VM_P];
+    typename std::conditional<F16, _Float16, float>::type rref[(36 + 9 * (NWIN - 1)) * VM_P];
+    uint16_t tmask[(NWIN > 1 ? NWIN - 1 : 1) * VM_P];
     uint32_t box[2 * VM_P];      // bounding box of the anchors 0..8 (x0 | y0 << 16, x1 | y1 << 16)
 };
 // the Weak sweep's per-workgroup state: the reference side plus the hypotheses and per-pixel state
 template <bool F16>
-struct WvLdsT : WvRefT<F16> {
+struct WvLdsT : WvRefT<F16, 1> {
     float4 hyp[9 * VM_P];        // [h][p]: anchor planes 1..8 (if STRONG) + current; P4 overwrites [0..4]
                                  // with the refinement candidates (WV_CAND) after P2's last read
     float4 pnow[VM_P];
@@ -1324,10 +1328,10 @@ struct WvLdsT : WvRefT<F16> {
     int pxy[VM_P];               // packed (x, y) of pixel slot p (P5's packed items)
 };
 #define WV_CAND(L) ((L).hyp)
-// 49.5 KiB with the direct 5-slot cost table at N = 10 (fp16 reference taps): three workgroups per CU.
-// (The sweep's own candidate path, a 9-slot table, runs two per CU from N = 8.)
-static_assert(sizeof(WvLdsT<true>) + 5 * 10 * VM_P * sizeof(float) + 10 * VM_P <= 160 * 1024 / 3,
-              "k_sweep_weak_vm (direct) at N = 10 must fit three workgroups per CU (160 KiB LDS)");
+// 33.5 KiB with the direct 5-slot cost table at N = 10 (fp16 reference taps): four workgroups per CU.
+// (The sweep's own candidate path, a 9-slot table, runs three per CU at N = 10.)
+static_assert(sizeof(WvLdsT<true>) + 5 * 10 * VM_P * sizeof(float) + 10 * VM_P <= 160 * 1024 / 4,
+              "k_sweep_weak_vm (direct) at N = 10 must fit four workgroups per CU (160 KiB LDS)");
 // `direct` (the pair-table kernels handled every pixel): the sweep reads the anchor candidates'
 // costs from their buffer in P2 and its table holds [5][N][64] (current plane, fit plane,
 // refinement candidates) instead of [9][N][64]: 48 KiB at N = 10, three workgroups per CU instead of two.
@@ -1351,16 +1355,18 @@ __device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
 // Reference taps: tap tk of the window at rb[tk * rs] (WvRefT: &rref[tap0 * VM_P + p], VM_P).
 // The IEEE statement of an NCC-New window's taps (lanes whose window fails window_rcp_ok).
 template <bool F16, int NW, int INC, class RT>
-__device__ __forceinline__ void ncc_new_window_slow(const Args &a, const RT *rb,
+__device__ __forceinline__ void ncc_new_window_slow(const Args &a, RT rb,
                                                     int rs, uint64_t mask, const Hom &Hm, int ax, int ay, const SrcTex<F16> &Q,
                                                     float &ss, float &sss, float &srs) {
     const float Wm1 = (float)(a.W - 1), Hm1 = (float)(a.H - 1);
     const uint32_t W1 = SrcTex<F16>::pitch(a.W);
+#pragma unroll (NW <= 3 ? NW : 1)  // (3x3: rb may be a register array)
     for (int i = 0; i < NW; ++i) {
         const float x = (float)(ax - 5 + INC * i);
         const float cx = fmaf(Hm.h[0], x, Hm.h[2]);
         const float cy = fmaf(Hm.h[3], x, Hm.h[5]);
         const float cz = fmaf(Hm.h[6], x, Hm.h[8]);
+#pragma unroll (NW <= 3 ? NW : 1)
         for (int j = 0; j < NW; ++j) {
             const int tk = i * NW + j;
             if (!((mask >> tk) & 1ull)) continue;
@@ -1378,10 +1384,11 @@ __device__ __forceinline__ void ncc_new_window_slow(const Args &a, const RT *rb,
         }
     }
 }
-// RT: the reference taps' type in LDS -- fp16 (exact, see apd_set_problem) where LDS is tight, fp32
-// where it is not (one conversion less per tap)
-template <bool F16, int NW, int INC, class RT = typename std::conditional<F16, _Float16, float>::type>
-__device__ __forceinline__ void ncc_new_window(const Args &a, const RT *rb,
+// RT: the reference taps' type (LDS or registers). PIPE: the centre window's columns software-
+// pipelined (more gathers in flight, ~30 more VGPRs; off in the Weak sweep, which runs four
+// workgroups per CU within 128 VGPRs)
+template <bool F16, int NW, int INC, bool PIPE = true, class RT = const typename std::conditional<F16, _Float16, float>::type *>
+__device__ __forceinline__ void ncc_new_window(const Args &a, RT rb,
                                                int rs, uint64_t mask, const Hom &Hm, int ax, int ay, bool live,
                                                bool fast, const FastTex<F16, true> &T, const SrcTex<F16> &Q, float &ss,
                                                float &sss, float &srs) {
@@ -1427,6 +1434,17 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const RT *rb,
                 for (int j = 0; j < NW; ++j) q[i][j] = T.load(t[i][j]);
 #pragma unroll
             for (int i = 0; i < NW; ++i) consume(i, t[i], q[i]);
+        } else if (!PIPE) {
+            // the centre window (6x6), one column of gathers at a time (fewer registers live)
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                typename TT::Tap t[NW];
+                typename TT::Raw q[NW];
+                column(i, t);
+#pragma unroll
+                for (int j = 0; j < NW; ++j) q[j] = T.load(t[j]);
+                consume(i, t, q);
+            }
         } else {
             // the centre window (6x6): column i+1's gathers in flight while column i is consumed
             typename TT::Tap ta[NW], tb[NW];
@@ -1459,8 +1477,8 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, const RT *rb,
 // masks and moments; wave w builds windows w, w + nwaves, ... (tap order = the reference's). Each
 // window's taps (and SA labels) are all loaded before the in-order moment sums, so a window costs one
 // memory round trip instead of one per tap.
-template <bool F16, int N1, int INC>
-__device__ __forceinline__ void wv_build_window(const Args &a, WvRefT<F16> &L, int p1, int k, int ax, int ay,
+template <bool F16, int N1, int INC, int NWIN>
+__device__ __forceinline__ void wv_build_window(const Args &a, WvRefT<F16, NWIN> &L, int p1, int k, int ax, int ay,
                                                 bool use_sa, int cid) {
     constexpr int NT = N1 * N1;
     const int tap0 = (k == 0) ? 0 : 36 + 9 * (k - 1);
@@ -1506,16 +1524,111 @@ __device__ __forceinline__ void wv_build_window(const Args &a, WvRefT<F16> &L, i
     if (k == 0) L.tmask0[p1] = mask;
     else L.tmask[(k - 1) * VM_P + p1] = (uint16_t)mask;
 }
-template <bool F16>
-__device__ __forceinline__ void wv_build_windows(const Args &a, WvRefT<F16> &L, int p, const APD_G short2 *anc, int cid,
+template <bool F16, int NWIN>
+__device__ __forceinline__ void wv_build_windows(const Args &a, WvRefT<F16, NWIN> &L, int p, const APD_G short2 *anc, int cid,
                                                  int wave, int nwaves) {
     const bool use_sa = cid != 0;
-    for (int k = wave; k < 9; k += nwaves) {
+    for (int k = wave; k < NWIN; k += nwaves) {
         const short2 ap = anc[k];
         if (ap.x == -1 || ap.y == -1) continue;
-        if (k == 0) wv_build_window<F16, 6, 2>(a, L, p, k, ap.x, ap.y, use_sa, cid);
-        else wv_build_window<F16, 3, 5>(a, L, p, k, ap.x, ap.y, use_sa, cid);
+        if (k == 0) wv_build_window<F16, 6, 2, NWIN>(a, L, p, k, ap.x, ap.y, use_sa, cid);
+        else wv_build_window<F16, 3, 5, NWIN>(a, L, p, k, ap.x, ap.y, use_sa, cid);
     }
+}
+
+// Anchor-window reference records: the reference side of an anchor window (k >= 1: 3x3 taps, step 5,
+// APD.cu:500-575) depends only on the anchor q and on whether it is SA-filtered -- by the pixel's
+// label, which for a used window is q's own (APD.cu:493-497) -- so it is built once per pixel q of
+// the image, in wv_build_window's statements: record [0] unfiltered, [1] filtered by q's label.
+// F16: 2 x uint4 = {taps 0..7 (fp16)}, {tap 8 | tap mask << 16, inv, srp, var}; fp32: 4 x uint4 =
+// {taps 0..3}, {taps 4..7}, {tap 8, mask, inv, srp}, {var, -, -, -}.
+template <bool F16> struct AncRec { static constexpr int U4 = F16 ? 2 : 4; };
+__device__ __forceinline__ size_t anc_rec_index(const Args &a, int q, int filt, int u4) {
+    return ((size_t)q * (a.sa_any ? 2 : 1) + (size_t)filt) * (size_t)u4;
+}
+template <bool F16>
+__global__ __launch_bounds__(BLOCK) void k_anchor_rec(Args a, uint4 *__restrict__ out) {
+    const int q = blockIdx.x * BLOCK + threadIdx.x;
+    if (q >= a.HW) return;
+    const int qy = q / a.W, qx = q - qy * a.W;
+    float r[9];
+#pragma unroll
+    for (int tk = 0; tk < 9; ++tk) r[tk] = tex_ref(a, qx - 5 + 5 * (tk / 3), qy - 5 + 5 * (tk % 3));
+    const int nvar = a.sa_any ? 2 : 1;
+    for (int filt = 0; filt < nvar; ++filt) {
+        const int cid = filt ? (int)a.sa[q] : 0;
+        bool in[9];
+#pragma unroll
+        for (int tk = 0; tk < 9; ++tk) {
+            in[tk] = true;
+            if (filt) {
+                const long idx = (long)(qy - 5 + 5 * (tk % 3)) * a.W + (qx - 5 + 5 * (tk / 3));
+                const bool inb = idx >= 0 && idx < a.HW;
+                const int lab = a.sa[inb ? idx : 0];
+                in[tk] = cid == 0 || (inb && lab == cid);
+            }
+        }
+        float sr = 0.0f, srr = 0.0f, ws = 0.0f, rv[9];
+        uint32_t mask = 0;
+#pragma unroll
+        for (int tk = 0; tk < 9; ++tk) {
+            rv[tk] = 0.0f;
+            if (!in[tk]) continue;
+            rv[tk] = r[tk];
+            mask |= 1u << tk;
+            sr += r[tk];
+            srr = fmaf(r[tk], r[tk], srr);
+            ws += 1.0f;
+        }
+        const float inv = 1.0f / ws, srp = sr * inv, srrp = srr * inv;
+        const float winv = ws != 0.0f ? inv : 0.0f, wvar = fmaf(-srp, srp, srrp);
+        uint4 *o = out + anc_rec_index(a, q, filt, AncRec<F16>::U4);
+        if constexpr (F16) {
+            uint32_t h[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const _Float16 lo = (_Float16)rv[2 * i];
+                const _Float16 hi = (i < 4) ? (_Float16)rv[2 * i + 1] : (_Float16)0.0f;
+                h[i] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+            }
+            o[0] = make_uint4(h[0], h[1], h[2], h[3]);
+            o[1] = make_uint4((h[4] & 0xFFFFu) | (mask << 16), __float_as_uint(winv), __float_as_uint(srp), __float_as_uint(wvar));
+        } else {
+            o[0] = make_uint4(__float_as_uint(rv[0]), __float_as_uint(rv[1]), __float_as_uint(rv[2]), __float_as_uint(rv[3]));
+            o[1] = make_uint4(__float_as_uint(rv[4]), __float_as_uint(rv[5]), __float_as_uint(rv[6]), __float_as_uint(rv[7]));
+            o[2] = make_uint4(__float_as_uint(rv[8]), mask, __float_as_uint(winv), __float_as_uint(srp));
+            o[3] = make_uint4(__float_as_uint(wvar), 0u, 0u, 0u);
+        }
+    }
+}
+// one record in registers, packed as loaded; r[tk] is tap tk (the reference-tap accessor of
+// ncc_new_window: rb[tk * rs] with rs = 1)
+template <bool F16>
+struct AncRecV {
+    uint4 u[AncRec<F16>::U4];
+    __device__ __forceinline__ static uint32_t comp(const uint4 &v, int i) {
+        return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+    }
+    __device__ __forceinline__ float operator[](int tk) const {  // (tk a compile-time constant after unrolling)
+        if constexpr (F16) {
+            const uint32_t h = tk < 8 ? comp(u[0], tk >> 1) : u[1].x;
+            return (float)__builtin_bit_cast(_Float16, (uint16_t)(h >> (16 * (tk & 1))));
+        } else {
+            return __uint_as_float(tk < 4 ? comp(u[0], tk) : tk < 8 ? comp(u[1], tk - 4) : u[2].x);
+        }
+    }
+    __device__ __forceinline__ uint32_t mask() const { return F16 ? (u[1].x >> 16) : u[2].y; }
+    __device__ __forceinline__ float inv() const { return __uint_as_float(F16 ? u[1].y : u[2].z); }
+    __device__ __forceinline__ float srp() const { return __uint_as_float(F16 ? u[1].z : u[2].w); }
+    __device__ __forceinline__ float var() const { return __uint_as_float(F16 ? u[1].w : u[3].x); }
+};
+template <bool F16>
+__device__ __forceinline__ AncRecV<F16> load_anc_rec(const Args &a, int q, int filt) {
+    const APD_G uint4 *src = a.arec + anc_rec_index(a, q, filt, AncRec<F16>::U4);
+    AncRecV<F16> R;
+#pragma unroll
+    for (int i = 0; i < AncRec<F16>::U4; ++i) R.u[i] = src[i];
+    return R;
 }
 
 // ComputeBilateralNCCNew + Softmax focal weighting (APD.cu:448-593, 431-446) for pixel slot p, source
@@ -1526,8 +1639,8 @@ __device__ __forceinline__ void wv_build_windows(const Args &a, WvRefT<F16> &L, 
 // SA = false: no SA masks in this problem, so every window's tap mask is full (compile-time constant:
 // no per-tap mask selects). BOX: L.box holds the pixel's anchor bounding box, and one
 // window_rcp_ok_box over it (taps included) stands for the per-window checks when it holds.
-template <bool F16, bool SA = true, bool BOX = false>
-__device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L, int p, int px, int py, int s, float4 pl,
+template <bool F16, bool SA = true, bool BOX = false, int NWIN>
+__device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWIN> &L, int p, int px, int py, int s, float4 pl,
                                             bool want, bool *seldep = nullptr, uint32_t *nwc = nullptr,
                                             uint32_t *nwa = nullptr) {
     const int W = a.W, H = a.H;
@@ -1599,16 +1712,26 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
         if (!BOX || __ballot(live && !box_ok))
             if (live && !box_ok) fast = window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
         float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-        if (k == 0)
-            ncc_new_window<F16, 6, 2>(a, &L.rref[p], VM_P, SA ? L.tmask0[p] : ~0ull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
-        else
+        float inv, srp, var;
+        if (k == 0) {
+            ncc_new_window<F16, 6, 2, NWIN == 9>(a, &L.rref[p], VM_P, SA ? L.tmask0[p] : ~0ull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            inv = L.winv[p]; srp = L.wsrp[p]; var = L.wvar[p];
+        } else if constexpr (NWIN > 1) {
             ncc_new_window<F16, 3, 5>(a, &L.rref[(36 + 9 * (k - 1)) * VM_P + p], VM_P,
                                       SA ? (uint64_t)L.tmask[(k - 1) * VM_P + p] : 0x1FFull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            inv = L.winv[k * VM_P + p]; srp = L.wsrp[k * VM_P + p]; var = L.wvar[k * VM_P + p];
+        } else {
+            // NWIN == 1: the anchor window's reference side from its record. Every lane loads (the
+            // window's code is converged); lanes without this anchor read pixel 0's record, as their
+            // (px, py) may be an unused slot's
+            const AncRecV<F16> R = load_anc_rec<F16>(a, has ? ax + ay * W : 0, (SA && has && ((L.flags[p] >> 29) & 1u)) ? 1 : 0);
+            ncc_new_window<F16, 3, 5>(a, R, 1, SA ? (uint64_t)R.mask() : 0x1FFull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            inv = R.inv(); srp = R.srp(); var = R.var();
+        }
         if (!live) continue;
         if (nwc) { if (k == 0) ++*nwc; else ++*nwa; }  // (profiling: windows evaluated)
-        const float inv = L.winv[k * VM_P + p];
         if (inv == 0.0f) continue;  // (empty window)
-        const float c = ncc_finalize_pre(inv, L.wsrp[k * VM_P + p], L.wvar[k * VM_P + p], ss, sss, srs);
+        const float c = ncc_finalize_pre(inv, srp, var, ss, sss, srs);
         if (k == 0) {
             center_cost = c;
         } else {
@@ -1641,7 +1764,7 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16> &L,
 // WvLdsT + the cost table take 52 KiB per workgroup at N = 8 (fp16 reference taps): 3 workgroups per
 // CU; the kernel needs ~110 VGPRs, well inside the 3-wave budget.
 #ifndef VM_WEAK_MINW
-#define VM_WEAK_MINW 3
+#define VM_WEAK_MINW 4  // waves per SIMD: four workgroups per CU (128 VGPRs)
 #endif
 #ifndef WV_WAVES
 #define WV_WAVES 4  // waves per Weak-sweep workgroup (64 pixels)
@@ -1714,7 +1837,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
                     L.hyp[(k - 1) * VM_P + p1] = hp[k];
                 }
             }
-            L.flags[p1] = hflag | (awin << 16);
+            L.flags[p1] = hflag | (awin << 16) | (use_sa ? (1u << 29) : 0u);
             L.hyp[8 * VM_P + p1] = cur;
             L.pxy[p1] = px1 | (py1 << 16);
             int bx0 = px1, by0 = py1, bx1 = px1, by1 = py1;  // anchors' bounding box (+ the pixel)
@@ -3453,7 +3576,7 @@ struct apd_ctx {
     std::string err;
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
-        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, lrs, wcur,
+        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, lrs, wcur, arec,
         wlist, gp_cb, gp_cnt, gp_cur, gp_refs, gp_ccnt, gp_cbase, gp_plist, gp_pidx, gp_pcost, gp_tmp;
     int n_near = 0;
     int host_stat[4] = {0, 0, 0, 0};  // apd_set_problem's read-back (see there)
@@ -3461,7 +3584,8 @@ struct apd_ctx {
     Args args{};
     bool loaded = false, prepared = false;
     int dw_tile_w = 8;             // DepthToWeak pixel tile width (64 / tile height); APD_DW_TILE_W
-    int tile_w = 8;                // sweep list tile width (tile = tile_w x 256/tile_w positions); APD_TILE_W
+    int tile_w = 16;               // sweep list tile width (tile = tile_w x 256/tile_w positions); APD_TILE_W
+                                   // (16 x 16: -1 % per C3 iteration against 8 x 32, profiles/r4_ab_tile_shape.txt)
     bool cand_pairs = true;        // Weak sweep candidates through the image-wide pair table; APD_NO_CAND_PAIRS=1
                                    // leaves them to the sweep
     bool gp_on = false;            // the pair table of the prepared problem is built (apd_stage_prepare)
@@ -3698,7 +3822,7 @@ void apd_destroy(apd_ctx *ctx) {
     DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
-                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand,
+                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand, &ctx->arec,
                       &ctx->lrs, &ctx->wcur, &ctx->wlist, &ctx->gp_cb, &ctx->gp_cnt, &ctx->gp_cur, &ctx->gp_refs, &ctx->gp_ccnt,
                       &ctx->gp_cbase, &ctx->gp_plist, &ctx->gp_pidx, &ctx->gp_pcost, &ctx->gp_tmp};
     for (DevBuf *b : bufs)
@@ -3825,6 +3949,8 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
         if ((st = ensure(ctx, ctx->reliable, HW))) return st;
         if ((st = ensure(ctx, ctx->nearest, HW * sizeof(short2)))) return st;
         if ((st = ensure(ctx, ctx->fit, HW * sizeof(float4)))) return st;
+        // anchor-window reference records (k_anchor_rec): 32 B (fp16 taps) or 64 B per pixel and variant
+        if ((st = ensure(ctx, ctx->arec, HW * (sa_any ? 2 : 1) * (tex_f16 ? 2 : 4) * sizeof(uint4)))) return st;
         HIP_OK(ctx, hipMemsetAsync(ctx->reliable.p, 0, HW, s));
         HIP_OK(ctx, hipMemsetAsync(ctx->fit.p, 0, HW * sizeof(float4), s));
         if ((st = build_near_offsets(ctx))) return st;
@@ -3877,6 +4003,7 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     a.nearest = devptr<decltype(a.nearest)>(P.use_APD ? ctx->nearest.p : nullptr);
     a.fit = devptr<decltype(a.fit)>(P.use_APD ? ctx->fit.p : nullptr);
     a.near_offsets = devptr<decltype(a.near_offsets)>(P.use_APD ? ctx->near_off.p : nullptr);
+    a.arec = devptr<decltype(a.arec)>(P.use_APD ? ctx->arec.p : nullptr);
     a.curve = nullptr;
     a.lr_ncc = nullptr;
     a.lr_geo = nullptr;
@@ -3899,6 +4026,12 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
             hipLaunchKernelGGL(k_build_quads, dim3(g), dim3(BLOCK), 0, s, (const float *)ctx->imgs.p,
                                (float4 *)ctx->quad.p, W, H, N, qstride);
         if ((st = check_launch(ctx, "k_build_quads"))) return st;
+    }
+    if (P.use_APD) {  // the anchor windows' reference side, once per problem (the Weak sweep reads it)
+        const unsigned g = blocks_for(HW, BLOCK);
+        if (tex_f16) hipLaunchKernelGGL(k_anchor_rec<true>, dim3(g), dim3(BLOCK), 0, s, a, (uint4 *)ctx->arec.p);
+        else hipLaunchKernelGGL(k_anchor_rec<false>, dim3(g), dim3(BLOCK), 0, s, a, (uint4 *)ctx->arec.p);
+        if ((st = check_launch(ctx, "k_anchor_rec"))) return st;
     }
     ctx->want_curve = pb->export_reliable_curve != 0;
     if (ctx->want_curve) {  // DepthToWeak cost curves (APD.cu:2188-2198, 2713-2724)
