@@ -2549,8 +2549,6 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
 static inline size_t gp_cost_lds_bytes(int N) { return GP_COST_STAGED ? (size_t)BLOCK * ((N + 3) & ~3) * sizeof(float) : 0; }
 template <bool F16, bool SA>
 __global__ __launch_bounds__(BLOCK) void k_gp_cost(Args a, const int2 *__restrict__ plist, int np, float *__restrict__ pcost) {
-    using RT = typename std::conditional<F16, _Float16, float>::type;
-    __shared__ RT rref[9 * BLOCK];
     float *crow = apd_dyn_lds;  // [BLOCK][Np]
     const int N = a.N, W = a.W, H = a.H, Np = (N + 3) & ~3;
     const int i0 = xcd_remap(blockIdx.x, gridDim.x) * BLOCK;
@@ -2560,30 +2558,10 @@ __global__ __launch_bounds__(BLOCK) void k_gp_cost(Args a, const int2 *__restric
     const int ax = pr.x & 0x7FFF, ay = pr.x >> 16;
     const bool filt = SA && (pr.x & 0x8000) != 0;  // SA-filtered window: taps with the anchor's label only
     const float4 pl = a.plane[pr.y];
-    float sr = 0.0f, srr = 0.0f, wsum = 9.0f;
-    uint64_t tm = 0x1FFull;
-    if (filt) {
-        // sa_at_dev's out-of-image -1 never equals the anchor's label (> 0); the anchor's own tap
-        // (t = 4) always matches, so wsum >= 1 (APD.cu:543's empty window cannot occur)
-        const int lab = a.sa[ax + ay * W];
-        tm = 0;
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-            const int ii = t / 3, jj = t - 3 * (t / 3);
-            if (sa_at_dev(a, ax - 5 + 5 * ii, ay - 5 + 5 * jj) == lab) tm |= 1ull << t;
-        }
-        wsum = (float)__builtin_popcountll(tm);
-    }
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-        const int ii = t / 3, jj = t - 3 * (t / 3);
-        const float r = tex_ref(a, ax - 5 + 5 * ii, ay - 5 + 5 * jj);
-        rref[t * BLOCK + threadIdx.x] = (RT)r;
-        if ((tm >> t) & 1ull) {
-            sr += r;
-            srr = fmaf(r, r, srr);
-        }
-    }
+    // the window's reference side from its record (k_anchor_rec: the same statements; a filtered
+    // window keeps the anchor's own tap, so its wsum >= 1 and APD.cu:543's empty window cannot occur)
+    const AncRecV<F16> R = load_anc_rec<F16>(a, ax + ay * W, filt ? 1 : 0);
+    const uint64_t tm = SA ? (uint64_t)R.mask() : 0x1FFull;
     const uint32_t selk = a.sel[ax + ay * W];
     uint32_t nlive = 0;
     for (int v = 0; v < N; ++v) {
@@ -2602,8 +2580,8 @@ __global__ __launch_bounds__(BLOCK) void k_gp_cost(Args a, const int2 *__restric
         if (__ballot(live)) {
             const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
             float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-            ncc_new_window<F16, 3, 5>(a, &rref[threadIdx.x], BLOCK, tm, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
-            if (live) res = ncc_finalize(sr, srr, ss, sss, srs, wsum);
+            ncc_new_window<F16, 3, 5>(a, R, 1, tm, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            if (live) res = ncc_finalize_pre(R.inv(), R.srp(), R.var(), ss, sss, srs);
         }
         nlive += live;
         if (GP_COST_STAGED) crow[threadIdx.x * Np + v] = res;
