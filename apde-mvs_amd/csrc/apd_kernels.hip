@@ -1316,9 +1316,11 @@ struct WvRefT {
     uint16_t tmask[(NWIN > 1 ? NWIN - 1 : 1) * VM_P];
     uint32_t box[2 * VM_P];      // bounding box of the anchors 0..8 (x0 | y0 << 16, x1 | y1 << 16)
 };
-// the Weak sweep's per-workgroup state: the reference side plus the hypotheses and per-pixel state
-template <bool F16>
-struct WvLdsT : WvRefT<F16, 1> {
+// the Weak sweep's per-workgroup state: the reference side plus the hypotheses and per-pixel state.
+// NWIN = 9: every window's reference side in LDS (the default); NWIN = 1: the centre window's only,
+// the anchor windows' from their records (APD_WEAK_REC=1, see k_sweep_weak_vm)
+template <bool F16, int NWIN = 9>
+struct WvLdsT : WvRefT<F16, NWIN> {
     float4 hyp[9 * VM_P];        // [h][p]: anchor planes 1..8 (if STRONG) + current; P4 overwrites [0..4]
                                  // with the refinement candidates (WV_CAND) after P2's last read
     float4 pnow[VM_P];
@@ -1328,19 +1330,22 @@ struct WvLdsT : WvRefT<F16, 1> {
     int pxy[VM_P];               // packed (x, y) of pixel slot p (P5's packed items)
 };
 #define WV_CAND(L) ((L).hyp)
-// 33.5 KiB with the direct 5-slot cost table at N = 10 (fp16 reference taps): four workgroups per CU.
-// (The sweep's own candidate path, a 9-slot table, runs three per CU at N = 10.)
-static_assert(sizeof(WvLdsT<true>) + 5 * 10 * VM_P * sizeof(float) + 10 * VM_P <= 160 * 1024 / 4,
-              "k_sweep_weak_vm (direct) at N = 10 must fit four workgroups per CU (160 KiB LDS)");
+// With the direct 5-slot cost table at N = 10 (fp16 reference taps): 49.5 KiB (three workgroups per
+// CU), or 33.5 KiB with the anchor records (four per CU). (The sweep's own candidate path, a 9-slot
+// table, runs one fewer per CU.)
+static_assert(sizeof(WvLdsT<true, 9>) + 5 * 10 * VM_P * sizeof(float) + 10 * VM_P <= 160 * 1024 / 3,
+              "k_sweep_weak_vm (direct) at N = 10 must fit three workgroups per CU (160 KiB LDS)");
+static_assert(sizeof(WvLdsT<true, 1>) + 5 * 10 * VM_P * sizeof(float) + 10 * VM_P <= 160 * 1024 / 4,
+              "k_sweep_weak_vm<REC> (direct) at N = 10 must fit four workgroups per CU (160 KiB LDS)");
 // `direct` (the pair-table kernels handled every pixel): the sweep reads the anchor candidates'
 // costs from their buffer in P2 and its table holds [5][N][64] (current plane, fit plane,
 // refinement candidates) instead of [9][N][64]: 48 KiB at N = 10, three workgroups per CU instead of two.
-template <bool F16>
 #ifndef APD_WV_LDS_PAD
 #define APD_WV_LDS_PAD 0  // experiments: extra LDS bytes per workgroup (fewer workgroups per CU)
 #endif
+template <bool F16, int NWIN>
 static inline size_t wv_lds_bytes(int N, bool direct = false) {
-    return APD_WV_LDS_PAD + sizeof(WvLdsT<F16>) + (size_t)(direct ? 5 : 9) * N * VM_P * sizeof(float) + (size_t)N * VM_P;
+    return APD_WV_LDS_PAD + sizeof(WvLdsT<F16, NWIN>) + (size_t)(direct ? 5 : 9) * N * VM_P * sizeof(float) + (size_t)N * VM_P;
 }
 __device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
     const long idx = (long)y * a.W + x;
@@ -1761,11 +1766,10 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
     return (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
 }
 
-// WvLdsT + the cost table take 52 KiB per workgroup at N = 8 (fp16 reference taps): 3 workgroups per
-// CU; the kernel needs ~110 VGPRs, well inside the 3-wave budget.
-#ifndef VM_WEAK_MINW
-#define VM_WEAK_MINW 4  // waves per SIMD: four workgroups per CU (128 VGPRs)
-#endif
+// Occupancy: REC = false (default) runs three workgroups per CU (LDS-bound, ~166 VGPRs); REC = true
+// (APD_WEAK_REC=1) four, within 128 VGPRs (the centre window without its column pipeline): -2 % on
+// the C3 headline pass but +11 % of Weak-sweep time over a whole C3-shaped scan, whose passes start
+// from converged priors (profiles/r4_scan_c3_26v_rec_vs_lds.txt) -- so the LDS variant is the default.
 #ifndef WV_WAVES
 #define WV_WAVES 4  // waves per Weak-sweep workgroup (64 pixels)
 #endif
@@ -1776,8 +1780,8 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
 #define WV_P5_CHUNKS 3  // P5 batches: whole views until at least this many 64-item chunks
 #endif
 #define WV_BLOCK (WV_WAVES * WAVE)
-template <bool F16, bool SA>
-__global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
+template <bool F16, bool SA, bool REC = false>
+__global__ __launch_bounds__(WV_BLOCK, REC ? 4 : 3) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
                                                                 int iter, const float *__restrict__ cand, int wc) {
     const int N = a.N, W = a.W;
     PHASE_BEGIN;
@@ -1786,7 +1790,7 @@ __global__ __launch_bounds__(WV_BLOCK, VM_WEAK_MINW) void k_sweep_weak_vm(Args a
     // without them (cand == nullptr: APD_NO_CAND_PAIRS=1 or a pair table that does not fit) P1
     // evaluates the candidates here
     const bool direct = cand != nullptr;
-    WvLdsT<F16> &L = *reinterpret_cast<WvLdsT<F16> *>(apd_dyn_lds);
+    WvLdsT<F16, REC ? 1 : 9> &L = *reinterpret_cast<WvLdsT<F16, REC ? 1 : 9> *>(apd_dyn_lds);
     float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64] (direct: [N][64]), later [5][N][64]
     uint8_t *wts = reinterpret_cast<uint8_t *>(costL + (direct ? 5 : 9) * N * VM_P);  // [N][64] view weights
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
@@ -3562,6 +3566,7 @@ struct apd_ctx {
     Args args{};
     bool loaded = false, prepared = false;
     int dw_tile_w = 8;             // DepthToWeak pixel tile width (64 / tile height); APD_DW_TILE_W
+    bool weak_rec = false;         // APD_WEAK_REC=1: the Weak sweep with anchor records (four workgroups per CU)
     int tile_w = 16;               // sweep list tile width (tile = tile_w x 256/tile_w positions); APD_TILE_W
                                    // (16 x 16: -1 % per C3 iteration against 8 x 32, profiles/r4_ab_tile_shape.txt)
     bool cand_pairs = true;        // Weak sweep candidates through the image-wide pair table; APD_NO_CAND_PAIRS=1
@@ -3695,6 +3700,18 @@ static inline T devptr(const void *p) { return reinterpret_cast<T>(reinterpret_c
     } while (0)
 
 // ... and of its SA-masked (SA quadrant windows on the fast taps) or unmasked form
+// (the same with a third template argument)
+#define LAUNCH_TEX_SA3(kern, t3, grid, block, lds, stream, ...)                                     \
+    do {                                                                                         \
+        const bool sa_ = ctx->args.sa_any != 0;                                                  \
+        if (ctx->args.tex_f16) {                                                                 \
+            if (sa_) hipLaunchKernelGGL((kern<true, true, t3>), grid, block, lds, stream, __VA_ARGS__); \
+            else hipLaunchKernelGGL((kern<true, false, t3>), grid, block, lds, stream, __VA_ARGS__);  \
+        } else {                                                                                 \
+            if (sa_) hipLaunchKernelGGL((kern<false, true, t3>), grid, block, lds, stream, __VA_ARGS__); \
+            else hipLaunchKernelGGL((kern<false, false, t3>), grid, block, lds, stream, __VA_ARGS__); \
+        }                                                                                        \
+    } while (0)
 #define LAUNCH_TEX_SA(kern, grid, block, lds, stream, ...)                                          \
     do {                                                                                         \
         const bool sa_ = ctx->args.sa_any != 0;                                                  \
@@ -3771,6 +3788,7 @@ apd_ctx *apd_create(int32_t device) {
         const int t = atoi(e);
         if (t == 1 || t == 2 || t == 4 || t == 8 || t == 16 || t == 32 || t == 64) ctx->dw_tile_w = t;
     }
+    ctx->weak_rec = getenv("APD_WEAK_REC") != nullptr && atoi(getenv("APD_WEAK_REC")) != 0;
     if (const char *e = getenv("APD_TILE_W")) {
         const int t = atoi(e);
         if (t == 4 || t == 8 || t == 16 || t == 32 || t == 64) ctx->tile_w = t;
@@ -3781,6 +3799,8 @@ apd_ctx *apd_create(int32_t device) {
         (const void *)k_sweep_strong_vm<true, true>, (const void *)k_sweep_strong_vm<false, true>,
         (const void *)k_sweep_weak_vm<true, false>, (const void *)k_sweep_weak_vm<false, false>,
         (const void *)k_sweep_weak_vm<true, true>, (const void *)k_sweep_weak_vm<false, true>,
+        (const void *)k_sweep_weak_vm<true, false, true>, (const void *)k_sweep_weak_vm<false, false, true>,
+        (const void *)k_sweep_weak_vm<true, true, true>, (const void *)k_sweep_weak_vm<false, true, true>,
         (const void *)k_depth_to_weak_vm<true, false>, (const void *)k_depth_to_weak_vm<false, false>,
         (const void *)k_depth_to_weak_vm<true, true>, (const void *)k_depth_to_weak_vm<false, true>,
         (const void *)k_local_refine_vm<true, false>, (const void *)k_local_refine_vm<false, false>,
@@ -4348,9 +4368,14 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             e0 = prof_begin(ctx);
             // k_sweep_weak_vm's small cost table when every pixel's candidates are in `cand`
             const bool direct = cand != nullptr;
-            LAUNCH_TEX_SA(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
-                       (ctx->args.tex_f16 ? wv_lds_bytes<true>(a.N, direct) : wv_lds_bytes<false>(a.N, direct)), s,
-                       aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
+            if (ctx->weak_rec)
+                LAUNCH_TEX_SA3(k_sweep_weak_vm, true, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
+                              (ctx->args.tex_f16 ? wv_lds_bytes<true, 1>(a.N, direct) : wv_lds_bytes<false, 1>(a.N, direct)), s,
+                              aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
+            else
+                LAUNCH_TEX_SA3(k_sweep_weak_vm, false, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
+                              (ctx->args.tex_f16 ? wv_lds_bytes<true, 9>(a.N, direct) : wv_lds_bytes<false, 9>(a.N, direct)), s,
+                              aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
             prof_end(ctx, e0, APD_PROF_WEAK_SWEEP, n);
         }
         if ((st = check_launch(ctx, "weak sweep"))) return st;
