@@ -163,8 +163,10 @@ struct Rng {
         uint32_t key0 = k0, key1 = k1;
 #pragma unroll
         for (int r = 0; r < 10; ++r) {
-            uint32_t lo0 = 0xD2511F53u * x0, hi0 = __umulhi(0xD2511F53u, x0);
-            uint32_t lo1 = 0xCD9E8D57u * x2, hi1 = __umulhi(0xCD9E8D57u, x2);
+            // (one 32x32 -> 64-bit product each: v_mad_u64_u32 instead of v_mul_lo + v_mul_hi)
+            const uint64_t p0 = (uint64_t)0xD2511F53u * x0, p1 = (uint64_t)0xCD9E8D57u * x2;
+            const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+            const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
             uint32_t n0 = hi1 ^ x1 ^ key0, n2 = hi0 ^ x3 ^ key1;
             x0 = n0; x1 = lo1; x2 = n2; x3 = lo0;
             key0 += 0x9E3779B9u; key1 += 0xBB67AE85u;
@@ -177,8 +179,10 @@ struct Rng {
         uint32_t key0 = k0, key1 = k1;
 #pragma unroll
         for (int r = 0; r < 10; ++r) {
-            uint32_t lo0 = 0xD2511F53u * x0, hi0 = __umulhi(0xD2511F53u, x0);
-            uint32_t lo1 = 0xCD9E8D57u * x2, hi1 = __umulhi(0xCD9E8D57u, x2);
+            // (one 32x32 -> 64-bit product each: v_mad_u64_u32 instead of v_mul_lo + v_mul_hi)
+            const uint64_t p0 = (uint64_t)0xD2511F53u * x0, p1 = (uint64_t)0xCD9E8D57u * x2;
+            const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+            const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
             uint32_t n0 = hi1 ^ x1 ^ key0, n2 = hi0 ^ x3 ^ key1;
             x0 = n0; x1 = lo1; x2 = n2; x3 = lo0;
             key0 += 0x9E3779B9u; key1 += 0xBB67AE85u;
