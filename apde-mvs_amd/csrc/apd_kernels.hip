@@ -1328,6 +1328,7 @@ struct WvLdsT : WvRefT<F16, NWIN> {
     uint32_t tsel[VM_P];         // views with weight > 0 (the selection the best anchor hypothesis brings)
     uint16_t rng_n[VM_P];
     int pxy[VM_P];               // packed (x, y) of pixel slot p (P5's packed items)
+    uint32_t asel[8 * VM_P];     // [k-1][p]: selected views of anchor k (P2a's priors; no launch writes them)
 };
 #define WV_CAND(L) ((L).hyp)
 // With the direct 5-slot cost table at N = 10 (fp16 reference taps): 49.5 KiB (three workgroups per
@@ -1820,13 +1821,17 @@ __global__ __launch_bounds__(WV_BLOCK, REC ? 4 : 3) void k_sweep_weak_vm(Args a,
             for (int k = 0; k < 9; ++k) ap[k] = anc[k];
             int lab[9], qk[9];
             uint8_t st[9];
+            uint32_t sl[9];
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
                 const bool ok = !(ap[k].x == -1 || ap[k].y == -1);
                 qk[k] = ok ? ap[k].x + ap[k].y * W : c1;  // anchors are in-image pixels
                 lab[k] = a.sa_any ? (int)a.sa[qk[k]] : cid;
                 st[k] = a.weak[qk[k]];
+                sl[k] = a.sel[qk[k]];
             }
+#pragma unroll
+            for (int k = 1; k < 9; ++k) L.asel[(k - 1) * VM_P + p1] = sl[k];
             float4 hp[9];
 #pragma unroll
             for (int k = 1; k < 9; ++k) hp[k] = a.plane[st[k] == APD_STRONG ? qk[k] : c1];
@@ -1899,7 +1904,7 @@ __global__ __launch_bounds__(WV_BLOCK, REC ? 4 : 3) void k_sweep_weak_vm(Args a,
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int pk = L.anc[(i + 1) * VM_P + p];  // anchor i+1's pixel, if any
-            if (pk >= 0) prior += ((a.sel[(pk & 0xFFFF) + (pk >> 16) * W] >> v) & 1u) ? 0.9f : 0.1f;
+            if (pk >= 0) prior += ((L.asel[i * VM_P + p] >> v) & 1u) ? 0.9f : 0.1f;
         }
         float ca[8];
         if (direct) {  // the candidates' costs from the pair-table kernels; absent ones as P1 sets them
