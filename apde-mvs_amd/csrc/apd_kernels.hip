@@ -3577,6 +3577,7 @@ struct apd_ctx {
     bool cand_pairs = true;        // Weak sweep candidates through the image-wide pair table; APD_NO_CAND_PAIRS=1
                                    // leaves them to the sweep
     bool gp_on = false;            // the pair table of the prepared problem is built (apd_stage_prepare)
+    bool rec_on = false;           // the anchor-window records of the prepared problem are built (k_anchor_rec)
     int gp_np = 0;                 // its distinct pairs
     bool lr_handover = true;       // LocalRefine reads DepthToWeak's samples; APD_NO_LR_HANDOVER=1 disables
     bool wcur_on = true;           // RandomInit keeps WEAK current-plane costs for iteration 0; APD_NO_WCUR=1 disables
@@ -3952,8 +3953,6 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
         if ((st = ensure(ctx, ctx->reliable, HW))) return st;
         if ((st = ensure(ctx, ctx->nearest, HW * sizeof(short2)))) return st;
         if ((st = ensure(ctx, ctx->fit, HW * sizeof(float4)))) return st;
-        // anchor-window reference records (k_anchor_rec): 32 B (fp16 taps) or 64 B per pixel and variant
-        if ((st = ensure(ctx, ctx->arec, HW * (sa_any ? 2 : 1) * (tex_f16 ? 2 : 4) * sizeof(uint4)))) return st;
         HIP_OK(ctx, hipMemsetAsync(ctx->reliable.p, 0, HW, s));
         HIP_OK(ctx, hipMemsetAsync(ctx->fit.p, 0, HW * sizeof(float4), s));
         if ((st = build_near_offsets(ctx))) return st;
@@ -4006,7 +4005,7 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     a.nearest = devptr<decltype(a.nearest)>(P.use_APD ? ctx->nearest.p : nullptr);
     a.fit = devptr<decltype(a.fit)>(P.use_APD ? ctx->fit.p : nullptr);
     a.near_offsets = devptr<decltype(a.near_offsets)>(P.use_APD ? ctx->near_off.p : nullptr);
-    a.arec = devptr<decltype(a.arec)>(P.use_APD ? ctx->arec.p : nullptr);
+    a.arec = nullptr;  // (apd_stage_prepare, when a kernel reads the records)
     a.curve = nullptr;
     a.lr_ncc = nullptr;
     a.lr_geo = nullptr;
@@ -4029,12 +4028,6 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
             hipLaunchKernelGGL(k_build_quads, dim3(g), dim3(BLOCK), 0, s, (const float *)ctx->imgs.p,
                                (float4 *)ctx->quad.p, W, H, N, qstride);
         if ((st = check_launch(ctx, "k_build_quads"))) return st;
-    }
-    if (P.use_APD) {  // the anchor windows' reference side, once per problem (the Weak sweep reads it)
-        const unsigned g = blocks_for(HW, BLOCK);
-        if (tex_f16) hipLaunchKernelGGL(k_anchor_rec<true>, dim3(g), dim3(BLOCK), 0, s, a, (uint4 *)ctx->arec.p);
-        else hipLaunchKernelGGL(k_anchor_rec<false>, dim3(g), dim3(BLOCK), 0, s, a, (uint4 *)ctx->arec.p);
-        if ((st = check_launch(ctx, "k_anchor_rec"))) return st;
     }
     ctx->want_curve = pb->export_reliable_curve != 0;
     if (ctx->want_curve) {  // DepthToWeak cost curves (APD.cu:2188-2198, 2713-2724)
@@ -4247,10 +4240,31 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
             (void)hipEventRecord(ctx->ev[14], s);
             // (the table's keys hold a pixel index below 2^25 and x below 2^15; else the sweep
             // evaluates the candidates itself)
-            if ((size_t)a.HW < (1u << 25) && a.W < 32768 && (st = build_global_pairs(ctx, ctx->cnt[2] + ctx->cnt[3])))
+            // (a pair packs x | filtered << 15 | y << 16 into an int: H < 32768 is also apd_set_problem's limit)
+            if ((size_t)a.HW < (1u << 25) && a.W < 32768 && a.H < 32768 &&
+                (st = build_global_pairs(ctx, ctx->cnt[2] + ctx->cnt[3])))
                 return st;
         } else {
             (void)hipEventRecord(ctx->ev[14], s);
+        }
+        // the anchor windows' reference side (k_anchor_rec: taps, tap mask, finalisation terms; 32 B
+        // with fp16 taps, else 64 B, per pixel and SA variant), built only when a kernel reads it --
+        // k_gp_cost, or the APD_WEAK_REC sweep. Optional: without room the pair table is dropped (the
+        // sweep evaluates the candidates itself) and the sweep runs its LDS variant.
+        ctx->rec_on = false;
+        a.arec = nullptr;
+        if (a.use_apd && ((ctx->gp_on && ctx->gp_np > 0) || ctx->weak_rec)) {
+            const size_t rb = (size_t)a.HW * (a.sa_any ? 2 : 1) * (a.tex_f16 ? 2 : 4) * sizeof(uint4);
+            if (try_ensure(ctx, ctx->arec, rb)) {
+                a.arec = devptr<decltype(a.arec)>(ctx->arec.p);
+                const unsigned g = blocks_for((size_t)a.HW, BLOCK);
+                if (a.tex_f16) hipLaunchKernelGGL(k_anchor_rec<true>, dim3(g), dim3(BLOCK), 0, s, a, (uint4 *)ctx->arec.p);
+                else hipLaunchKernelGGL(k_anchor_rec<false>, dim3(g), dim3(BLOCK), 0, s, a, (uint4 *)ctx->arec.p);
+                if ((st = check_launch(ctx, "k_anchor_rec"))) return st;
+                ctx->rec_on = true;
+            } else if (ctx->gp_on && ctx->gp_np > 0) {
+                ctx->gp_on = false;
+            }
         }
     }
     (void)hipEventRecord(ctx->ev[2], s);
@@ -4373,7 +4387,7 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             e0 = prof_begin(ctx);
             // k_sweep_weak_vm's small cost table when every pixel's candidates are in `cand`
             const bool direct = cand != nullptr;
-            if (ctx->weak_rec)
+            if (ctx->weak_rec && ctx->rec_on)
                 LAUNCH_TEX_SA3(k_sweep_weak_vm, true, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
                               (ctx->args.tex_f16 ? wv_lds_bytes<true, 1>(a.N, direct) : wv_lds_bytes<false, 1>(a.N, direct)), s,
                               aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
@@ -4613,6 +4627,13 @@ int32_t apd_device_copy(apd_ctx *ctx, void *dst, const void *src, size_t bytes) 
     (void)hipSetDevice(ctx->device);
     HIP_OK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, ctx->stream));
     HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+    return APD_OK;
+}
+
+int32_t apd_device_mem_info(apd_ctx *ctx, size_t *free_bytes, size_t *total_bytes) {
+    if (!ctx || !free_bytes || !total_bytes) return APD_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    HIP_OK(ctx, hipMemGetInfo(free_bytes, total_bytes));
     return APD_OK;
 }
 

@@ -292,11 +292,19 @@ struct DevStore {
         for (auto &kv : ms) release(kv.second);
         ms.clear();
     }
-    const float *image(const std::string &key, const ImageCache::Scaled &s) {
+    // the round image in HBM; nullptr with *failed false: no room (the caller uploads it per problem),
+    // with *failed true: the copy itself failed (an error, the buffer is released)
+    const float *image(const std::string &key, const ImageCache::Scaled &s, bool *failed) {
+        *failed = false;
         Map &m = images[key];
         if (!m.p) {
             const size_t b = (size_t)s.w * s.h * sizeof(float);
-            if (!reserve(m, b) || apd_device_copy(ctx, m.p, s.img.data(), b) != APD_OK) return nullptr;
+            if (!reserve(m, b)) return nullptr;
+            if (apd_device_copy(ctx, m.p, s.img.data(), b) != APD_OK) {
+                release(m);
+                *failed = true;
+                return nullptr;
+            }
             m.w = s.w;
             m.h = s.h;
             uploaded += (long)b;
@@ -506,7 +514,9 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     bool dev_priors = false;
     if (dev) {
         for (int i = 0; i < NI; ++i) {
-            img_ptrs[i] = dev->image(dense + "/images/" + format_index(ids[i]) + pb.img_ext, *scaled[i]);
+            bool failed = false;
+            img_ptrs[i] = dev->image(dense + "/images/" + format_index(ids[i]) + pb.img_ext, *scaled[i], &failed);
+            if (failed) { SAY("device upload failed: " << apd_last_error(ctx)); return false; }
             if (!img_ptrs[i]) {  // no room in HBM: this image is uploaded per problem, as the reference does
                 dev->images.erase(dense + "/images/" + format_index(ids[i]) + pb.img_ext);
                 img_ptrs[i] = scaled[i]->img.data();
@@ -630,11 +640,23 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     prob.seed = seed ^ ((uint64_t)(uint32_t)job.iteration << 32) ^ (uint64_t)(uint32_t)pb.ref_image_id;
     prob.export_reliable_curve = job.export_curve ? 1 : 0;
     int st = apd_set_problem(ctx, &prob);
-    if (st != APD_OK) { SAY("apd_set_problem failed: " << apd_last_error(ctx)); return false; }
-    const auto t0 = std::chrono::steady_clock::now();
-    st = apd_run_patchmatch(ctx);
+    auto t0 = std::chrono::steady_clock::now();
+    if (st == APD_OK) {
+        t0 = std::chrono::steady_clock::now();
+        st = apd_run_patchmatch(ctx);
+    }
     const auto t1 = std::chrono::steady_clock::now();
-    if (st != APD_OK) { SAY("apd_run_patchmatch failed: " << apd_last_error(ctx)); return false; }
+    if (st == APD_ENOMEM && dev) {
+        // the library's own per-problem buffers did not fit next to the device-resident store: the
+        // store is released (its maps hold the same values as the files, pending ones are committed
+        // from the host side at the pass end) and the run continues on the host store, starting with
+        // this problem
+        SAY("device memory exhausted (" << apd_last_error(ctx) << "): device-resident state released, "
+                                         "the run continues from the host store");
+        dev.reset();
+        return process(ctx, job);
+    }
+    if (st != APD_OK) { SAY("RunPatchMatch failed: " << apd_last_error(ctx)); return false; }
     const long ms = (long)std::chrono::duration_cast<std::chrono::milliseconds>(t1 - t0).count();
     {
         std::lock_guard<std::mutex> g(g_print);
@@ -869,6 +891,14 @@ int main(int argc, char **argv) {
     if (ctxs.size() == 1 && !(getenv("APD_DEVICE_STATE") && std::string(getenv("APD_DEVICE_STATE")) == "0")) {
         drv.dev = std::make_unique<DevStore>();
         drv.dev->ctx = ctxs[0];
+        // default cap: the device's free memory less room for the library's per-problem buffers
+        // (≈ 40 GB at C3 with the pair table and the DepthToWeak hand-over; a quarter of the free
+        // memory, at least 16 GiB); a problem that still runs out releases the store (process())
+        size_t fb = 0, tb = 0;
+        if (apd_device_mem_info(ctxs[0], &fb, &tb) == APD_OK) {
+            const size_t room = std::max<size_t>((size_t)16 << 30, fb / 4);
+            drv.dev->cap = fb > room ? fb - room : 0;
+        }
         if (const char *e = getenv("APD_DEVICE_STATE_CAP_MB")) drv.dev->cap = (size_t)std::max(0L, atol(e)) << 20;
     }
     std::vector<Job> jobs(problems.size());

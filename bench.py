@@ -15,10 +15,18 @@ no step repeats an iteration on an already-converged view. Each block is bracket
 a device synchronisation, and the blocks' times are summed; inputs are resident in HBM throughout.
 value = W*H*steps summed over ranks / max-over-ranks time.
 
-Multi-GPU (weak scaling): one process per GPU (torch.distributed.run); each rank runs its own
-reference view (rank mod #views) with its own priors. Within a pass the reference views are
-independent given the previous pass's depth maps, so the only collectives are the
-timing barriers and a max-reduction of the elapsed time (no data-path collective).
+Multi-GPU (weak scaling): one process per GPU. `python3 bench.py --gpus N` outside a
+torch.distributed launch starts its N ranks itself (a torch.distributed.run child on 127.0.0.1,
+before anything in this process touches the GPU) and exits with the child's status; under the
+driver's own torch.distributed.run it runs as one rank. Each rank runs its own reference view
+(rank mod #views) of the same final-round pass with its own priors. Within a pass the reference
+views are independent given the previous pass's view states (APD.cpp:592-610), and
+the scan runner (apde-mvs_amd/scan_runner.py) ends every pass with ONE all-gather of the
+new states ([6, H, W] fp32 per view: depth, normal xyz, pixel state, confidence). The bench does the
+same inside the timed region: every block of fresh iterations (one pass's loop body) ends with that
+all-gather over RCCL (xGMI), so `value` at N > 1 pays the exchange; `exchange_ms` is the median of
+separately timed all-gathers (barrier, then the collective alone) and `rank_ms_per_step` the ranks'
+own per-step times (the value uses the max over ranks).
 
 Besides the headline the JSON line carries:
   roofline      the dominant kernels of the step, the Weak sweep (the anchor candidates -- k_gp_cost +
@@ -123,10 +131,12 @@ def final_round_problem(sc, priors, ref, N, sa=False):
     return arr
 
 
-def timed_fresh_iterations(eng, arr, steps, warmup, barrier):
+def timed_fresh_iterations(eng, arr, steps, warmup, barrier, exchange=None):
     """Warm-up, then `steps` loop-body iterations taken in blocks of one fresh run's iterations
     0..max_iterations-1; each block re-uploads and re-initialises the problem untimed, and is timed
-    between a barrier + device synchronisation on both sides. Returns (summed seconds, per-step ms)."""
+    between a barrier + device synchronisation on both sides. `exchange` (N > 1): the pass's
+    all-gather of the view states, run at the end of every block inside the timed region.
+    Returns (summed seconds, per-step ms)."""
     iters = max(1, arr.params.max_iterations)
     done = 0
     while done < warmup:
@@ -153,6 +163,9 @@ def timed_fresh_iterations(eng, arr, steps, warmup, barrier):
             t = time.perf_counter()
             step_ms.append((t - t_prev) * 1e3)
             t_prev = t
+        if exchange is not None:
+            exchange()
+            t_prev = time.perf_counter()
         elapsed += t_prev - t_block
         barrier()
         done += n
@@ -267,21 +280,25 @@ def depth_to_weak_roofline(eng, W, N):
 
 def end_to_end(eng, arr, sc, ref, W, H, N):
     """One full RunPatchMatch (the main.cpp:157-161 bracket), after an untimed one (first-use
-    allocations and code loading out of the way); the timed run is profiled (HIP events around the
-    loop-body kernels and DepthToWeak), which also gives DepthToWeak's roofline."""
+    allocations and code loading out of the way). The timed run is unprofiled (only the phase events
+    of apd_timing); a third, profiled run (HIP events around the loop-body kernels and DepthToWeak,
+    device counters) gives DepthToWeak's roofline."""
     eng.set_problem(arr)
     eng.run()
     eng.set_problem(arr)
-    eng.profile_reset(True)
+    eng.profile_reset(False)
     t1 = time.perf_counter()
     eng.run()
     t2 = time.perf_counter()
     tm = eng.timing()
+    eng.set_problem(arr)
+    eng.profile_reset(True)
+    eng.run()
     dtw = depth_to_weak_roofline(eng, W, N)
     eng.profile_reset(False)
     iters = tm.iterations
     parts = tm.anchors_ms + tm.lists_ms + tm.pairs_ms + tm.init_ms + tm.sweep_ms + tm.post_ms
-    r = {"run_patchmatch_ms": round(tm.total_ms, 3), "host_wall_ms": round((t2 - t1) * 1e3, 3),
+    r = {"run_patchmatch_ms": round(tm.total_ms, 3), "host_wall_ms": round((t2 - t1) * 1e3, 3), "profiled": False,
          "mpix_s_end_to_end": round(W * H * iters / (tm.total_ms * 1e-3) / 1e6, 3),
          "anchors_ms": round(tm.anchors_ms, 3), "lists_ms": round(tm.lists_ms, 3), "pairs_ms": round(tm.pairs_ms, 3),
          "init_ms": round(tm.init_ms, 3), "sweep_ms": round(tm.sweep_ms, 3),
@@ -324,6 +341,9 @@ def c2_first_init(eng, steps, warmup):
                         "(geom off, APD off), Strong sweep B + R per step, fresh runs",
             "value": round(W * H * len(step_ms) / el / 1e6, 3), "unit": "Mpix/s", "steps": len(step_ms),
             "ms_per_step": round(el / len(step_ms) * 1e3, 4),
+            "mpix_s_iter_amortised": (round(W * H / (elapsed / args.steps + e2e["pairs_ms"] * 1e-3 / 3) / 1e6 * n_gpus, 3)
+                                      if e2e else None),
+            "multi_gpu": exch,
             "iter_ms_median": round(statistics.median(step_ms), 3), "roofline": roof, "end_to_end": e2e}
 
 
@@ -351,6 +371,50 @@ def cpu_baseline(eng, texture, N, w, h, threads):
                       f"(t_iter={t_iter:.2f}s; anchors/RandomInit {times[0]:.2f}s untimed)"}
 
 
+def self_launch_cmd(argv, gpus, env):
+    """The torch.distributed.run command that starts `gpus` ranks of this script with the same
+    arguments, or None when no launch is needed (one GPU, or already a rank of a distributed launch:
+    WORLD_SIZE set by the driver's own torch.distributed.run). Built and run before anything in this
+    process touches the GPU; the ranks rendezvous on 127.0.0.1 at a free port (APD_BENCH_PORT
+    overrides it)."""
+    if gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    port = env.get("APD_BENCH_PORT")
+    if not port:
+        import socket
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+            so.bind(("127.0.0.1", 0))
+            port = str(so.getsockname()[1])
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def state_exchange(tdist, torch, state, world):
+    """The scan runner's per-pass step (scan_runner.Exchange.all_gather_state): every
+    rank's new view state [6, H, W] fp32 to every rank, device to device (RCCL over xGMI; gloo in the
+    one-GPU rehearsal). Returns (exchange, timed): exchange() runs one all-gather and waits for it;
+    timed(reps) is the median ms of `reps` all-gathers, each after a barrier (the collective alone,
+    without the ranks' load imbalance)."""
+    outs = [torch.empty_like(state) for _ in range(world)]
+
+    def exchange():
+        tdist.all_gather(outs, state)
+        if state.is_cuda:
+            torch.cuda.synchronize()
+
+    def timed(reps):
+        ms = []
+        for _ in range(reps):
+            tdist.barrier()
+            if state.is_cuda:
+                torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            exchange()
+            ms.append((time.perf_counter() - t0) * 1e3)
+        return statistics.median(ms)
+    return exchange, timed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -368,6 +432,11 @@ def main():
     ap.add_argument("--sa", type=int, default=1, help="also measure the headline pass with SA labels (C5's pass) (0/1)")
     args = ap.parse_args()
     t_start_all = time.time()
+    cmd = self_launch_cmd(sys.argv[1:], args.gpus, os.environ)
+    if cmd is not None:
+        # `python3 bench.py --gpus N`: start the N ranks as a child (nothing here has touched the GPU)
+        import subprocess
+        sys.exit(subprocess.call(cmd))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -403,6 +472,10 @@ def main():
 
     lib = A.load_library()
     device = local_rank % max(1, lib.apd_device_count())
+    if dist and dist[2] != "nccl":
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.set_device(device)
     eng = A.Engine(device, lib)
     t0 = time.time()
     priors = first_init_priors(eng, sc, ids, N)
@@ -411,16 +484,44 @@ def main():
     del priors
     weak_frac = float((arr.weak_info == A.WEAK).mean())
 
-    elapsed, step_ms = timed_fresh_iterations(eng, arr, args.steps, args.warmup, barrier)
+    exchange = exchange_timed = None
+    if dist:
+        # this rank's view state as the scan runner packs it (depth, normal xyz, state, confidence),
+        # from a finished run of its problem, on its device
+        import scan_runner
+        torch, tdist, backend = dist
+        eng.set_problem(arr)
+        eng.run()
+        o = eng.results_device(W, H, f"cuda:{device}")
+        state = scan_runner._pack(o.planes[..., 3], o.planes[..., :3], o.weak_info, o.confidence).contiguous()
+        del o
+        exchange, exchange_timed = state_exchange(tdist, torch, state, world)
+        exchange()  # (first use: communicator setup out of the timed region)
+    elapsed, step_ms = timed_fresh_iterations(eng, arr, args.steps, args.warmup, barrier, exchange)
     roof = weak_roofline(eng, args.steps, W, N)
     roof_strong_apd = strong_roofline(eng, W, N)
     eng.profile_reset(False)
+    exch = None
     if dist:
         torch, tdist, backend = dist
+        ex_ms = exchange_timed(5)
         dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        mine = torch.tensor([elapsed, statistics.median(step_ms), ex_ms], dtype=torch.float64, device=dev)
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        tdist.all_gather(every, mine)
+        every = [e.cpu().tolist() for e in every]
+        elapsed = max(e[0] for e in every)
+        blocks = -(-args.steps // max(1, arr.params.max_iterations))
+        exch = {"exchange_ms": round(max(e[2] for e in every), 3),
+                "exchange_bytes_per_rank": int(state.numel() * state.element_size()),
+                "exchanges_in_timed_region": blocks,
+                "exchange_backend": backend,
+                "rank_ms_per_step": [round(e[0] / args.steps * 1e3, 3) for e in every],
+                "rank_iter_ms_median": [round(e[1], 3) for e in every],
+                "note": "one all-gather of the [6, H, W] fp32 view states per block of fresh iterations (one "
+                        "pass's loop body) inside the timed region, as scan_runner.py ends every pass; "
+                        "exchange_ms = median of 5 barrier-separated all-gathers, max over ranks"}
+        del state
 
     n_gpus = world if dist else 1
     value = n_gpus * W * H * args.steps / elapsed / 1e6
@@ -469,6 +570,9 @@ def main():
                        "width": W, "height": H, "n_src": N, "texture": args.texture,
                        "weak_frac": round(weak_frac, 4), "global_batch": n_gpus,
                        "parallelism": f"views{n_gpus}"},
+            "mpix_s_iter_amortised": (round(W * H / (elapsed / args.steps + e2e["pairs_ms"] * 1e-3 / 3) / 1e6 * n_gpus, 3)
+                                      if e2e else None),
+            "multi_gpu": exch,
             "iter_ms_median": round(statistics.median(step_ms), 3),
             "iter_ms": [round(x, 2) for x in step_ms],
             "roofline": roof,

@@ -248,6 +248,9 @@ int32_t apd_profile_evaluations(apd_ctx *ctx, int64_t *ncc_evaluations);
 int32_t apd_device_alloc(apd_ctx *ctx, size_t bytes, void **ptr);
 int32_t apd_device_free(apd_ctx *ctx, void *ptr);
 int32_t apd_device_copy(apd_ctx *ctx, void *dst, const void *src, size_t bytes);
+/* Free and total bytes of the ctx's device (hipMemGetInfo): the `apd` binary sizes its
+   device-resident store from it, leaving room for the library's per-problem buffers. */
+int32_t apd_device_mem_info(apd_ctx *ctx, size_t *free_bytes, size_t *total_bytes);
 /* cv::resize INTER_NEAREST (the priors' resize, APD.cpp:605-672) from a device buffer of sw x sh
    elements of elem_bytes to one of dw x dh, with the host library's index arithmetic. */
 int32_t apd_device_resize_nearest(apd_ctx *ctx, const void *src, int32_t sw, int32_t sh, void *dst,

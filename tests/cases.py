@@ -1,6 +1,7 @@
 """Seeded parity cases shared by the CPU (oracle/golden) and GPU (HIP vs oracle) tests.
 
-Every case is a small synthetic scene (≤160x120, N≤8) so the oracle finishes in seconds. The
+Every case is a small synthetic scene (≤160x120, N≤31; C1's 640x480 N=4 FIRST_INIT with two
+iterations) so the oracle finishes in seconds. The
 prior-dependent states (REFINE_INIT / REFINE_ITER, geometric consistency, APD anchors, SA masks)
 take their priors from an oracle FIRST_INIT pass over the neighbouring views, exactly the data flow
 of main.cpp:306-367 (depths.bin / normals.bin / weak.bin / confidence.bin of the previous pass).
@@ -110,6 +111,8 @@ CASES = {
     # config C5's pass (final round with SAM edge priors): SA labels with a label-0 band, N = 10,
     # rotate_time 4 -- the image-wide pair table keyed by (window anchor, SA-filtered)
     "refine_iter_sa_n10_apd_geom_rt4": (144, 88, 10, "apd_geom_sa_rt4"),
+    # config C1 (BASELINE configs[0]): 640x480, 1 ref + 4 src views, 2 iterations, FIRST_INIT
+    "c1_first_n4_iter2": (640, 480, 4, "first_c1"),
 }
 
 
@@ -127,6 +130,8 @@ def make_case(name, oracle_run):
     sc = scene(w, h, max(n, 4), texture="rich" if rich else "smooth")
     if kind in ("first", "first_rich"):
         return base_problem(sc, 0, n)
+    if kind == "first_c1":
+        return base_problem(sc, 0, n, max_iterations=2)
     if kind == "first_sa0":
         arr = base_problem(sc, 0, n)
         arr.sa_mask = sc.labels[0].copy()

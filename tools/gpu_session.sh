@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU-box session of chained steps (run from the repo root): bash tools/gpu_session.sh OUT STEP...
-# Steps: parity | fullsize | ab:<AB env>:<libA>,<libB>,... | bench[:args] | pmc:<kernel-regex>:<last>:<bench args> | prof[:args]
+# Steps: parity | tests:<file,file,...> | gputests | smoke | ab:<AB env>:<libA>,<libB>,... | bench[:args] | pmc:<kernel-regex>:<last>:<bench args> | prof[:args]
 # Each GPU step has its own time limit; the script stops at the first failure.
 set -e
 OUT=$1; shift
@@ -13,6 +13,7 @@ for step in "$@"; do
   echo "[$(date +%T)] step $n: $step"
   case $kind in
     parity) timeout -k 10 420 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread > "$OUT/s$n.parity.log" 2>&1 ;;
+    tests) timeout -k 10 900 python3 -u -m pytest ${rest//,/ } -m gpu -x -v --timeout 500 --timeout-method thread > "$OUT/s$n.tests.log" 2>&1 ;;
     gputests) timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 500 --timeout-method thread > "$OUT/s$n.gputests.log" 2>&1 ;;
     smoke) timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/s$n.smoke.log" 2>&1 ;;
     ab) env_=${rest%%:*}; libs=${rest#*:}
