@@ -745,6 +745,15 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
                ms_(start, t_img), ms_(t_img, t_pri), ms_(t_pri, t_run), ms, ms_(t_run, t_get), ms_(t_get, t_epi),
                ms_(t_epi, end));
     }
+    if (getenv("APD_PHASE_TIMING")) {  // the library's phase split of this RunPatchMatch (device events, ms)
+        apd_timing tm{};
+        if (apd_get_timing(ctx, &tm) == APD_OK) {
+            std::lock_guard<std::mutex> g(g_print);
+            printf("PhaseTiming %d %d iters %d weak %d total %.3f anchors %.3f lists %.3f pairs %.3f init %.3f "
+                   "sweep %.3f post %.3f\n", width, height, tm.iterations, weak_count, tm.total_ms, tm.anchors_ms,
+                   tm.lists_ms, tm.pairs_ms, tm.init_ms, tm.sweep_ms, tm.post_ms);
+        }
+    }
     {
         std::lock_guard<std::mutex> g(g_print);
         std::cout << "Processing image: " << format_index(pb.ref_image_id) << " done!" << std::endl;

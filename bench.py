@@ -341,9 +341,6 @@ def c2_first_init(eng, steps, warmup):
                         "(geom off, APD off), Strong sweep B + R per step, fresh runs",
             "value": round(W * H * len(step_ms) / el / 1e6, 3), "unit": "Mpix/s", "steps": len(step_ms),
             "ms_per_step": round(el / len(step_ms) * 1e3, 4),
-            "mpix_s_iter_amortised": (round(W * H / (elapsed / args.steps + e2e["pairs_ms"] * 1e-3 / 3) / 1e6 * n_gpus, 3)
-                                      if e2e else None),
-            "multi_gpu": exch,
             "iter_ms_median": round(statistics.median(step_ms), 3), "roofline": roof, "end_to_end": e2e}
 
 

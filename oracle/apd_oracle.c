@@ -53,6 +53,38 @@
 
 typedef struct { float x, y, z, w; } f4;
 
+/* Float division and square roots of the restated arithmetic. In the parity build these are the IEEE
+   operations of the contract above. ORACLE_FASTMATH (liboracle_fm.so, the numerics-sensitivity study
+   tools/numerics_sensitivity.py; NOT the parity contract) restates the reference's own build flags,
+   nvcc --use_fast_math (CMakeLists.txt:26), in spirit: the file is compiled with -ffp-contract=fast
+   (every a*b+c the source writes may become a fused multiply-add, as nvcc --fmad=true does), a/b is
+   a * rcp(b) and 1/sqrt(x) is rsqrt(x) with ~1-2 ulp approximations (the SSE 12-bit estimate plus one
+   Newton step, as -prec-div=false / -prec-sqrt=false allow), sqrt(x) = x * rsqrt(x), exp is __expf's
+   exp2 of a rounded x * log2(e), sin/cos come from libm instead of the contract's polynomials, and
+   denormals are flushed to zero (FTZ/DAZ, -ftz=true). */
+#ifdef ORACLE_FASTMATH
+#include <immintrin.h>
+static inline float fm_rcp(float x) {
+    const float ax = fabsf(x);
+    if (!(ax > 1e-36f && ax < 1e36f)) return 1.0f / x; /* zero, denormal, huge, inf, NaN */
+    float r = _mm_cvtss_f32(_mm_rcp_ss(_mm_set_ss(x)));
+    return r * (2.0f - x * r);
+}
+static inline float fm_rsqrt(float x) {
+    if (!(x > 1e-36f && x < 1e36f)) return 1.0f / sqrtf(x);
+    float r = _mm_cvtss_f32(_mm_rsqrt_ss(_mm_set_ss(x)));
+    return r * (1.5f - 0.5f * x * r * r);
+}
+static inline float fm_sqrt(float x) { return (x > 1e-36f && x < 1e36f) ? x * fm_rsqrt(x) : sqrtf(x); }
+#define FDIV(a, b) ((a) * fm_rcp(b))
+#define FRSQRT(x) fm_rsqrt(x)
+#define FSQRT(x) fm_sqrt(x)
+#else
+#define FDIV(a, b) ((a) / (b))
+#define FRSQRT(x) (1.0f / sqrtf(x))
+#define FSQRT(x) sqrtf(x)
+#endif
+
 #define WEAK APD_WEAK
 #define STRONG APD_STRONG
 #define UNKNOWN APD_UNKNOWN
@@ -80,6 +112,9 @@ static inline float bits_f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 /* exp(x): Cody-Waite reduction + degree-7 Taylor/Horner (|r| <= ln2/2), 2^k by two exact scalings.
    Restates expf at APD.cu:440 (Softmax), 1340/1347/1358 (view selection). */
 float o_expf(float x) {
+#ifdef ORACLE_FASTMATH
+    return (float)exp2((double)(x * 1.44269504f)); /* __expf: ex2.approx(x * log2e) */
+#endif
     if (x != x) return x;
     if (x > 88.7228394f) return INFINITY;
     if (x < -103.972084f) return 0.0f;
@@ -103,6 +138,9 @@ float o_expf(float x) {
 
 /* sin/cos for |x| <= 0.8 (arguments are the +-0.01*pi perturbation angles, APD.cu:274-283). */
 float o_sinf(float x) {
+#ifdef ORACLE_FASTMATH
+    return (float)sin((double)x);
+#endif
     float s2 = x * x;
     float p = -2.50521084e-08f;
     p = fmaf(p, s2, 2.75573192e-06f);
@@ -112,6 +150,9 @@ float o_sinf(float x) {
     return fmaf(x * s2, p, x);
 }
 float o_cosf(float x) {
+#ifdef ORACLE_FASTMATH
+    return (float)cos((double)x);
+#endif
     float s2 = x * x;
     float p = 2.08767570e-09f;
     p = fmaf(p, s2, -2.75573192e-07f);
@@ -292,7 +333,7 @@ static inline void homography(const octx *o, int s, f4 pl, float Hm[9]) {
     float m0 = pl.x * o->ikx;
     float m1 = pl.y * o->iky;
     float m2 = fmaf(-pl.y, o->cyk, fmaf(-pl.x, o->cxk, pl.z));
-    float iw = 1.0f / pl.w;
+    float iw = FDIV(1.0f, pl.w);
     m0 *= iw; m1 *= iw; m2 *= iw;
     const float *A = o->A[s], *b = o->b[s];
     Hm[0] = fmaf(-b[0], m0, A[0]); Hm[1] = fmaf(-b[0], m1, A[1]); Hm[2] = fmaf(-b[0], m2, A[2]);
@@ -305,7 +346,7 @@ static inline void project(const float Hm[9], float x, float y, float *ox, float
     float X = fmaf(Hm[1], y, fmaf(Hm[0], x, Hm[2]));
     float Y = fmaf(Hm[4], y, fmaf(Hm[3], x, Hm[5]));
     float Z = fmaf(Hm[7], y, fmaf(Hm[6], x, Hm[8]));
-    float iz = 1.0f / Z;
+    float iz = FDIV(1.0f, Z);
     *ox = X * iz;
     *oy = Y * iz;
 }
@@ -343,24 +384,24 @@ static inline int trunc_clamp(float x, int n) {
  * ----------------------------------------------------------------------------------------------*/
 static inline void normalize3(f4 *v) { /* NormalizeVec3, APD.cu:157-164 */
     float ns = v->x * v->x + v->y * v->y + v->z * v->z;
-    float inv = 1.0f / sqrtf(ns);
+    float inv = FRSQRT(ns);
     v->x *= inv; v->y *= inv; v->z *= inv;
 }
 static inline void normalize2(float *x, float *y) { /* NormalizeVec2, APD.cu:166-172 */
     float ns = *x * *x + *y * *y;
-    float inv = 1.0f / sqrtf(ns);
+    float inv = FRSQRT(ns);
     *x *= inv; *y *= inv;
 }
 static inline void get3d(const apd_camera *c, float px, float py, float depth, float X[3]) { /* APD.cu:190-202 */
-    X[0] = depth * (px - c->K[2]) / c->K[0];
-    X[1] = depth * (py - c->K[5]) / c->K[4];
+    X[0] = FDIV(depth * (px - c->K[2]), c->K[0]);
+    X[1] = FDIV(depth * (py - c->K[5]), c->K[4]);
     X[2] = depth;
 }
 static inline f4 view_dir(const apd_camera *c, int px, int py, float depth) { /* APD.cu:204-216 */
     float X[3];
     get3d(c, (float)px, (float)py, depth, X);
-    float norm = sqrtf(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
-    f4 v = {X[0] / norm, X[1] / norm, X[2] / norm, 0.0f};
+    float norm = FSQRT(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
+    f4 v = {FDIV(X[0], norm), FDIV(X[1], norm), FDIV(X[2], norm), 0.0f};
     return v;
 }
 static inline float dist2origin(const apd_camera *c, int px, int py, float depth, f4 n) { /* APD.cu:218-223 */
@@ -369,8 +410,8 @@ static inline float dist2origin(const apd_camera *c, int px, int py, float depth
     return -(n.x * X[0] + n.y * X[1] + n.z * X[2]);
 }
 static inline float depth_from_plane(const apd_camera *c, f4 pl, int px, int py) { /* APD.cu:237-240 */
-    return -pl.w * c->K[0] /
-           (((float)px - c->K[2]) * pl.x + (c->K[0] / c->K[4]) * ((float)py - c->K[5]) * pl.y + c->K[0] * pl.z);
+    return FDIV(-pl.w * c->K[0],
+                (((float)px - c->K[2]) * pl.x + FDIV(c->K[0], c->K[4]) * ((float)py - c->K[5]) * pl.y + c->K[0] * pl.z));
 }
 static f4 random_normal(const apd_camera *c, int px, int py, orng *g, float depth) { /* APD.cu:242-268 */
     float q1 = 1.0f, q2 = 1.0f, s = 2.0f;
@@ -379,7 +420,7 @@ static f4 random_normal(const apd_camera *c, int px, int py, orng *g, float dept
         q2 = 2.0f * orng_uniform(g) - 1.0f;
         s = q1 * q1 + q2 * q2;
     }
-    float sq = sqrtf(1.0f - s);
+    float sq = FSQRT(1.0f - s);
     f4 n = {2.0f * q1 * sq, 2.0f * q2 * sq, 1.0f - 2.0f * s, 0.0f};
     f4 vd = view_dir(c, px, py, depth);
     float dot = n.x * vd.x + n.y * vd.y + n.z * vd.z;
@@ -421,8 +462,8 @@ static inline f4 to_ref(const apd_camera *c, f4 p) { /* TransformNormal2RefCam, 
     return r;
 }
 static inline void world_point(const apd_camera *c, float x, float y, float depth, float P[3]) { /* APD.cu:831-851 */
-    float X0 = depth * (x - c->K[2]) / c->K[0];
-    float X1 = depth * (y - c->K[5]) / c->K[4];
+    float X0 = FDIV(depth * (x - c->K[2]), c->K[0]);
+    float X1 = FDIV(depth * (y - c->K[5]), c->K[4]);
     float X2 = depth;
     float t0 = c->R[0] * X0 + c->R[3] * X1 + c->R[6] * X2;
     float t1 = c->R[1] * X0 + c->R[4] * X1 + c->R[7] * X2;
@@ -443,14 +484,14 @@ static inline void project_cam(const float P[3], const apd_camera *c, float *px,
  * matching costs
  * ----------------------------------------------------------------------------------------------*/
 static inline float ncc_finalize(float sr, float srr, float ss, float sss, float srs, float wsum) {
-    float inv = 1.0f / wsum;
+    float inv = FDIV(1.0f, wsum);
     sr *= inv; srr *= inv; ss *= inv; sss *= inv; srs *= inv;
     float var_ref = fmaf(-sr, sr, srr);
     float var_src = fmaf(-ss, ss, sss);
     if (var_ref < 1e-5f || var_src < 1e-5f) return COST_MAX;
     float covar = fmaf(-sr, ss, srs);
-    float vrs = sqrtf(var_ref * var_src);
-    return fmaxf(0.0f, fminf(COST_MAX, 1.0f - covar / vrs));
+    float vrs = FSQRT(var_ref * var_src);
+    return fmaxf(0.0f, fminf(COST_MAX, 1.0f - FDIV(covar, vrs)));
 }
 
 /* ComputeBilateralNCCOld, APD.cu:596-721 */
@@ -595,7 +636,7 @@ float o_geom_cost(const octx *o, int px, int py, int s, f4 pl) {
     float bx, by, rd;
     project_cam(Q, rc, &bx, &by, &rd);
     float dx = (float)px - bx, dy = (float)py - by;
-    float e = sqrtf(dx * dx + dy * dy);
+    float e = FSQRT(dx * dx + dy * dy);
     return fminf(3.0f, e);
 }
 
@@ -650,7 +691,7 @@ static void k_random_init(octx *o, int px, int py) {
         uint32_t sv = 0;
         for (int i = 0; i < N; ++i) if (cv[i] <= thr) sv |= (1u << i);
         WR(o, sel_next, c) = sv;
-        WR(o, cost, c) = cost / (float)top_k;
+        WR(o, cost, c) = FDIV(cost, (float)top_k);
     } else {
         WR(o, cost, c) = COST_MAX;
     }
@@ -659,25 +700,25 @@ static void k_random_init(octx *o, int px, int py) {
 /* Multi-hypothesis joint view selection shared by the Strong/Weak sweeps, APD.cu:1339-1374 / 1505-1540 */
 static void view_selection(const octx *o, float ca[8][32], const float *prior, int iter, orng *g, uint8_t *vw) {
     const int N = o->N;
-    float thr = (float)(0.8 * (double)o_expf((float)(iter * iter) / (-90.0f)));
+    float thr = (float)(0.8 * (double)o_expf(FDIV((float)(iter * iter), (-90.0f))));
     float sp[32];
     for (int i = 0; i < N; ++i) {
         float count = 0.0f, tmpw = 0.0f;
         int cf = 0;
         for (int j = 0; j < 8; ++j) {
             float c = ca[j][i];
-            if (c < thr) { tmpw += o_expf(c * c / (-0.18f)); count += 1.0f; }
+            if (c < thr) { tmpw += o_expf(FDIV(c * c, (-0.18f))); count += 1.0f; }
             if (c > 1.2f) cf++;
         }
         float p = 0.0f;
-        if (count > 2 && cf < 3) p = tmpw / count;
-        else if (cf < 3) p = o_expf(thr * thr / (-0.32f));
+        if (count > 2 && cf < 3) p = FDIV(tmpw, count);
+        else if (cf < 3) p = o_expf(FDIV(thr * thr, (-0.32f)));
         sp[i] = p * prior[i];
     }
     /* TransformPDFToCDF, APD.cu:174-188 */
     float sum = 0.0f;
     for (int i = 0; i < N; ++i) sum += sp[i];
-    float inv = 1.0f / sum, cum = 0.0f;
+    float inv = FDIV(1.0f, sum), cum = 0.0f;
     for (int i = 0; i < N; ++i) { cum = fmaf(sp[i], inv, cum); sp[i] = cum; }
     for (int i = 0; i < APD_MAX_IMAGES; ++i) vw[i] = 0;
     for (int smp = 0; smp < 15; ++smp) {
@@ -801,7 +842,7 @@ static void k_sweep_strong(octx *o, int px, int py, int iter) {
     for (int j = 0; j < 8; ++j) {
         float acc = 0.0f;
         for (int i = 0; i < N; ++i) if (vw[i] > 0) acc = fmaf((float)vw[i], ca[j][i], acc);
-        fc[j] = acc / wn;
+        fc[j] = FDIV(acc, wn);
     }
     int mi = 0; /* FindMinCostIndex, APD.cu:60-71 */
     { float m = fc[0]; for (int j = 1; j < 8; ++j) if (fc[j] <= m) { m = fc[j]; mi = j; } }
@@ -911,19 +952,19 @@ static void weak_stats(const octx *o, int px, int py, f4 t, const uint8_t *vw, f
     int stop = 0;
     for (int i = 0; i < N; ++i) {
         if (!vw[i]) continue;
-        if (!stop) { st[2]++; P = fmaf((float)vw[i], full[i], P); if (P / wn >= thr) stop = 1; }
+        if (!stop) { st[2]++; P = fmaf((float)vw[i], full[i], P); if (FDIV(P, wn) >= thr) stop = 1; }
         Pg = fmaf((float)vw[i], lbg[i], Pg);
         Pc = fmaf((float)vw[i], lbc[i], Pc);
     }
-    if (Pg / wn >= thr) st[3] = 1;
-    if (Pc / wn >= thr) st[4] = 1;
+    if (FDIV(Pg, wn) >= thr) st[3] = 1;
+    if (FDIV(Pc, wn) >= thr) st[4] = 1;
     else {  /* survivors: anchor windows with the prefix exit */
         float Q = 0.0f;
         for (int i = 0; i < N; ++i) {
             if (!vw[i]) continue;
             st[5]++;
             Q = fmaf((float)vw[i], full[i], Q);
-            if (Q / wn >= thr) break;
+            if (FDIV(Q, wn) >= thr) break;
         }
     }
     if (!stop) st[6] = 1;
@@ -975,7 +1016,7 @@ static void k_sweep_weak(octx *o, int px, int py, int iter) {
                 acc = fmaf((float)vw[i], v, acc);
             }
         }
-        fc[j] = acc / wn;
+        fc[j] = FDIV(acc, wn);
     }
     int mi = 0;
     { float m = fc[0]; for (int j = 1; j < 8; ++j) if (fc[j] <= m) { m = fc[j]; mi = j; } }
@@ -1055,7 +1096,7 @@ static int point_in_triangle(int ax, int ay, int bx, int by, int cx, int cy, int
     float ABx = (float)(bx - ax), ABy = (float)(by - ay);
     float BCx = (float)(cx - bx), BCy = (float)(cy - by);
     float CAx = (float)(ax - cx), CAy = (float)(ay - cy);
-    float AB = sqrtf(ABx * ABx + ABy * ABy), BC = sqrtf(BCx * BCx + BCy * BCy), CA = sqrtf(CAx * CAx + CAy * CAy);
+    float AB = FSQRT(ABx * ABx + ABy * ABy), BC = FSQRT(BCx * BCx + BCy * BCy), CA = FSQRT(CAx * CAx + CAy * CAy);
     if (AB <= 2 || BC <= 2 || CA <= 2) return 0;
     if (!(AB + BC > CA && BC + CA > AB && AB + CA > BC)) return 0;
     float PAx = (float)(ax - px), PAy = (float)(ay - py);
@@ -1085,7 +1126,7 @@ static void k_find_nearest(octx *o, int px, int py) {
                 int t = tx + ty * W;
                 if (RD(o, weak, t) != STRONG) continue;
                 if (RD(o, conf, t) < cc) continue;
-                float d = sqrtf((float)(x * x + y * y));
+                float d = FSQRT((float)(x * x + y * y));
                 if (d < md) { md = d; bx = tx; by = ty; bc = RD(o, conf, t); }
                 else if (d == md) { if (RD(o, conf, t) > bc) { bx = tx; by = ty; bc = RD(o, conf, t); } }
             }
@@ -1100,7 +1141,7 @@ static void k_find_nearest(octx *o, int px, int py) {
 typedef struct { float cos_a, sin_a, thr; int shift; } anchor_consts;
 static anchor_consts make_anchor_consts(int rotate_time) {
     anchor_consts k;
-    float angle = 45.0f / (float)rotate_time;
+    float angle = FDIV(45.0f, (float)rotate_time);
     k.cos_a = (float)cos((double)angle * M_PI_D / 180.0f);
     k.sin_a = (float)sin((double)angle * M_PI_D / 180.0f);
     k.thr = (float)cos((double)(angle / 2.0f) * M_PI_D / 180.0f);
@@ -1204,7 +1245,7 @@ static void k_gen_anchors(octx *o, int px, int py, anchor_consts K) {
         float sd = 0.0f;
         for (int k = 0; k < vc; ++k) {
             float d = fabsf(cr.x * v3[k][0] + cr.y * v3[k][1] + cr.z * v3[k][2] + cr.w);
-            if (d / depth_diff < o->P.ransac_threshold) { tcnt++; sd += d; }
+            if (FDIV(d, depth_diff) < o->P.ransac_threshold) { tcnt++; sd += d; }
         }
         if (tcnt < 6) continue;
         if (tcnt > max_count) {
@@ -1220,7 +1261,7 @@ static void k_gen_anchors(octx *o, int px, int py, anchor_consts K) {
     float wgt[32];
     for (int i = 0; i < vc; ++i) {
         float d = fabsf(best.x * v3[i][0] + best.y * v3[i][1] + best.z * v3[i][2] + best.w);
-        if (d / depth_diff >= o->P.ransac_threshold) { vx[i] = -1; vy[i] = -1; wgt[i] = FLT_MAX; continue; }
+        if (FDIV(d, depth_diff) >= o->P.ransac_threshold) { vx[i] = -1; vy[i] = -1; wgt[i] = FLT_MAX; continue; }
         if (i == ua || i == ub || i == uc) d -= 1;
         wgt[i] = d;
     }
@@ -1360,7 +1401,7 @@ static int o_classify_curve(const float *pc, int weak_peak_radius) {
     for (int i = 2; i < 59; ++i) {
         if (is_peak[i] && i != min_peak) { float d = pc[i] - min_cost; var = fmaf(d, d, var); }
     }
-    var = sqrtf(var);
+    var = FSQRT(var);
     var /= (float)(count - 1);
     return (var > 0.2f) ? STRONG : WEAK;
 }
@@ -1380,18 +1421,18 @@ static void k_depth_to_weak(octx *o, int px, int py) {
         if (is_set(sv, s - 1)) {
             wn += (float)RD(o, vw, (size_t)(s - 1) * o->HW + c);
             float d0 = cam->c[0] - o->cam[s].c[0], d1 = cam->c[1] - o->cam[s].c[1], d2 = cam->c[2] - o->cam[s].c[2];
-            base += sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+            base += FSQRT(d0 * d0 + d1 * d1 + d2 * d2);
             valid++;
         }
     }
     if (valid == 0) { WR(o, weak, c) = UNKNOWN; return; }
     base /= (float)valid;
-    float disp = cam->K[0] * base / od;
+    float disp = FDIV(cam->K[0] * base, od);
     float pc[61];
     const int geom = o->P.geom_consistency;
     const float gf = o->P.geom_factor;
     for (int pd = -30; pd <= 30; ++pd) {
-        float pdepth = cam->K[0] * base / (disp + (float)pd);
+        float pdepth = FDIV(cam->K[0] * base, (disp + (float)pd));
         if (pdepth < o->P.depth_min || pdepth > o->P.depth_max) { pc[pd + 30] = 2.0f; continue; }
         f4 t = pl;
         t.w = dist2origin(cam, px, py, pdepth, t);
@@ -1438,8 +1479,8 @@ static void k_confidence(octx *o, int px, int py) {
         float bx, by, refd;
         project_cam(Q, rc, &bx, &by, &refd);
         float dx = (float)px - bx, dy = (float)py - by;
-        if (sqrtf(dx * dx + dy * dy) <= 2.0f) nc += 2;
-        if (fabsf(rd - refd) / rd <= 0.02f) nc += 2;
+        if (FSQRT(dx * dx + dy * dy) <= 2.0f) nc += 2;
+        if (FDIV(fabsf(rd - refd), rd) <= 0.02f) nc += 2;
     }
     if (nc > 255) nc = 255;
     WR(o, conf, c) = (uint8_t)nc;
@@ -1467,17 +1508,17 @@ static void k_local_refine(octx *o, int px, int py) {
             cost_now = fmaf(tc, w, cost_now);
             wn += w;
             float d0 = cam->c[0] - o->cam[s].c[0], d1 = cam->c[1] - o->cam[s].c[1], d2 = cam->c[2] - o->cam[s].c[2];
-            base += sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+            base += FSQRT(d0 * d0 + d1 * d1 + d2 * d2);
             valid++;
         }
     }
     if (wn == 0 || valid == 0) return;
     cost_now /= wn;
     base /= (float)valid;
-    float disp = cam->K[0] * base / od;
+    float disp = FDIV(cam->K[0] * base, od);
     float min_cost = 2.0f, best = od;
     for (int pd = -5; pd <= 5; ++pd) {
-        float pdepth = cam->K[0] * base / (disp + (float)pd);
+        float pdepth = FDIV(cam->K[0] * base, (disp + (float)pd));
         if (pdepth < o->P.depth_min || pdepth > o->P.depth_max) continue;
         f4 t = pl;
         t.w = dist2origin(cam, px, py, pdepth, t);
@@ -1663,6 +1704,14 @@ int oracle_run_patchmatch(const apd_problem *pb, const apd_outputs *out, int nth
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #else
     (void)nthreads;
+#endif
+#ifdef ORACLE_FASTMATH
+    /* flush denormals in this thread and in every pool thread (libgomp keeps its pool) */
+    _mm_setcsr(_mm_getcsr() | 0x8040u);
+#ifdef _OPENMP
+#pragma omp parallel
+    _mm_setcsr(_mm_getcsr() | 0x8040u);
+#endif
 #endif
     octx *o = (octx *)malloc(sizeof(octx));
     if (!o) return APD_ENOMEM;

@@ -12,11 +12,15 @@ ORACLE_DIR = os.path.join(REPO, "oracle")
 ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
 
 
-def load():
-    # APD_ORACLE_SO: a mutated oracle build (tools/mutate_oracle.py checks that the KATs reject it)
-    path = os.environ.get("APD_ORACLE_SO") or ORACLE_SO
-    if path == ORACLE_SO and not os.path.exists(ORACLE_SO):
-        subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
+ORACLE_FM_SO = os.path.join(ORACLE_DIR, "liboracle_fm.so")
+
+
+def load(path=None):
+    # APD_ORACLE_SO: a mutated oracle build (tools/mutate_oracle.py checks that the KATs reject it);
+    # path=ORACLE_FM_SO: the fast-math variant of the numerics-sensitivity study (numerics_sensitivity.py)
+    path = path or os.environ.get("APD_ORACLE_SO") or ORACLE_SO
+    if path in (ORACLE_SO, ORACLE_FM_SO) and not os.path.exists(path):
+        subprocess.run(["make", "-C", ORACLE_DIR, os.path.basename(path)], check=True, capture_output=True)
     lib = C.CDLL(path)
     lib.oracle_run_patchmatch.restype = C.c_int
     lib.oracle_run_patchmatch.argtypes = [C.POINTER(A.ApdProblem), C.POINTER(A.ApdOutputs), C.c_int,
