@@ -11,31 +11,42 @@ sys.path[:0] = [os.path.join(REPO, "apde-mvs_amd"), os.path.join(REPO, "tests")]
 import numpy as np
 import synth, host_schedule as HS
 
+PARSE = sys.argv[1] == "--parse" if len(sys.argv) > 1 else False  # --parse LOG W H V: summarise an apd log
+if PARSE:
+    parse_log = sys.argv[2]
+    del sys.argv[1:3]
 W, H, V = (int(x) for x in sys.argv[1:4]) if len(sys.argv) >= 4 else (3024, 2016, 9)
 extra = sys.argv[4:]
-sc = synth.make_scene(W, H, V - 1)
-NSRC = int(os.environ.get("TIME_SCAN_NSRC", "10"))
-if NSRC > 0:
-    sc.pairs = [pl[:NSRC] for pl in sc.pairs]
-print(f"scene generated ({NSRC or V - 1} sources per view)", flush=True)
-folder = tempfile.mkdtemp(prefix="apd_scan_")
-HS.write_dense_folder(sc, folder, ext=".png", masks=os.environ.get("TIME_SCAN_SA", "1") == "1")  # TIME_SCAN_SA=0: no sa_masks/ (C3)
-from PIL import Image
-for f in sorted(os.listdir(os.path.join(folder, "images"))):  # re-encode as baseline JPEG
-    p = os.path.join(folder, "images", f)
-    Image.open(p).save(p[:-4] + ".jpg", quality=95)
-    print("jpeg", f, flush=True)
-    os.remove(p)
 apd = os.path.join(REPO, "apde-mvs_amd", "host", "build", "apd")
-cmd = [apd, "-d", folder, "--dataset", "ETH3D", "--no_fuse", "true"] + extra
-# the apd stdout goes to a file as it runs (TIME_SCAN_LOG, default under /tmp): a long scan keeps
-# writing, so a watchdog on the output directory sees progress
-log = os.environ.get("TIME_SCAN_LOG", os.path.join(folder, "apd_stdout.log"))
-print(f"scene written ({W}x{H}, {V} views); apd log: {log}", flush=True)
-t0 = time.time()
-with open(log, "w") as lf:
-    rc = subprocess.run(cmd, stdout=lf, stderr=subprocess.STDOUT, env=dict(os.environ, APD_PHASE_TIMING="1")).returncode
-wall = time.time() - t0
+if PARSE:
+    wall, rc, log = float("nan"), 0, parse_log
+else:
+    sc = synth.make_scene(W, H, V - 1)
+    NSRC = int(os.environ.get("TIME_SCAN_NSRC", "10"))
+    if NSRC > 0:
+        sc.pairs = [pl[:NSRC] for pl in sc.pairs]
+    print(f"scene generated ({NSRC or V - 1} sources per view)", flush=True)
+    folder = os.environ.get("TIME_SCAN_FOLDER") or tempfile.mkdtemp(prefix="apd_scan_")
+    os.makedirs(folder, exist_ok=True)
+    HS.write_dense_folder(sc, folder, ext=".png", masks=os.environ.get("TIME_SCAN_SA", "1") == "1")  # TIME_SCAN_SA=0: no sa_masks/ (C3)
+    from PIL import Image
+    for f in sorted(os.listdir(os.path.join(folder, "images"))):  # re-encode as baseline JPEG
+        p = os.path.join(folder, "images", f)
+        Image.open(p).save(p[:-4] + ".jpg", quality=95)
+        print("jpeg", f, flush=True)
+        os.remove(p)
+    cmd = [apd, "-d", folder, "--dataset", "ETH3D", "--no_fuse", "true"] + extra
+    # the apd stdout goes to a file as it runs (TIME_SCAN_LOG, default under /tmp): a long scan keeps
+    # writing, so a watchdog on the output directory sees progress
+    log = os.environ.get("TIME_SCAN_LOG", os.path.join(folder, "apd_stdout.log"))
+    print(f"scene written ({W}x{H}, {V} views); apd log: {log}", flush=True)
+    if os.environ.get("TIME_SCAN_RUN", "1") == "0":  # scene only (the caller runs apd, e.g. under rocprofv3)
+        print("command:", " ".join(cmd), flush=True)
+        sys.exit(0)
+    t0 = time.time()
+    with open(log, "w") as lf:
+        rc = subprocess.run(cmd, stdout=lf, stderr=subprocess.STDOUT, env=dict(os.environ, APD_PHASE_TIMING="1")).returncode
+    wall = time.time() - t0
 
 
 class _Out:
