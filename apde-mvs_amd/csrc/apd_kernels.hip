@@ -1781,8 +1781,11 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
 #define WV_P5_CHUNKS 3  // P5 batches: whole views until at least this many 64-item chunks
 #endif
 #define WV_BLOCK (WV_WAVES * WAVE)
+#ifndef WV_LDS_OCC
+#define WV_LDS_OCC 3  // workgroups per CU the LDS variant's registers are bounded for
+#endif
 template <bool F16, bool SA, bool REC = false>
-__global__ __launch_bounds__(WV_BLOCK, REC ? 4 : 3) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
+__global__ __launch_bounds__(WV_BLOCK, REC ? 4 : WV_LDS_OCC) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
                                                                 int iter, const float *__restrict__ cand, int wc) {
     const int N = a.N, W = a.W;
     PHASE_BEGIN;

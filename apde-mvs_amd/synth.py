@@ -59,10 +59,10 @@ class _Texture:
 
     SIZE = 512
 
-    def __init__(self, rng, base_freq=6.0, flat_patches=(), detail=None):
+    def __init__(self, rng, base_freq=6.0, flat_patches=(), detail=None, scale=1.0):
         n = self.SIZE
         self.tex = self._noise(rng, n, 24.0)  # keep ~24 cycles per tile
-        self.k = base_freq * n / 24.0 / (2 * np.pi) * 2.0  # texels per world unit
+        self.k = base_freq * n / 24.0 / (2 * np.pi) * 2.0 / scale  # texels per world unit
         self.flat = list(flat_patches)  # (u0, v0, u1, v1, value)
         self.mean = rng.uniform(90, 160)
         self.scale = rng.uniform(28, 40)
@@ -149,12 +149,17 @@ TEXTURES = ("smooth", "rich")
 
 
 def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=True, depth=6.0,
-               workers: int = 0, texture: str = "smooth", detail_period_px: float = 5.0) -> Scene:
+               workers: int = 0, texture: str = "smooth", detail_period_px: float = 5.0,
+               texture_scale: float = 1.0) -> Scene:
     """texture="smooth": band-limited textures fixed in world units, so they get smoother per pixel
     as the resolution grows (90-94 % of the pixels end WEAK at 3024x2016 and 6048x4032).
     texture="rich": the same scene plus a fine detail octave of `detail_period_px` pixels at the
     reference view, and two more textureless patches: a resolution-independent, texture-rich
-    variant whose WEAK fraction is set by the textureless area."""
+    variant whose WEAK fraction is set by the textureless area.
+    texture_scale: the smooth textures' world wavelengths times this factor. A scene rendered at
+    1/s of a resolution with texture_scale s has that resolution's texture per pixel (its WEAK
+    fraction): bench.py's CPU baseline samples the C3 workload that way. The random draws do not
+    change, so texture_scale = 1 is the scene of every other caller."""
     if texture not in TEXTURES:
         raise ValueError(f"texture must be one of {TEXTURES}")
     rng = np.random.default_rng(seed)
@@ -179,10 +184,10 @@ def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=Tru
         flat += [(1.45 * half_w, 0.1 * half_h, 2.0 * half_w, 1.5 * half_h, 112.0)]
         floor_flat = [(0.2 * half_w, 0.0, 1.1 * half_w, 0.35 * depth, 96.0)]
     quads.append(_Quad([-half_w, -half_h, depth], [2 * half_w, 0, 0.35 * depth], [0, 2 * half_h, 0],
-                       _Texture(rng, base_freq=4.0, flat_patches=flat, detail=detail())))  # slanted back wall
+                       _Texture(rng, base_freq=4.0, flat_patches=flat, detail=detail(), scale=texture_scale)))  # slanted back wall
     quads.append(_Quad([-half_w, 0.55 * half_h, 0.45 * depth], [2 * half_w, 0, 0],
                        [0, 0.45 * half_h, 0.9 * depth],
-                       _Texture(rng, base_freq=5.0, flat_patches=floor_flat, detail=detail())))  # floor
+                       _Texture(rng, base_freq=5.0, flat_patches=floor_flat, detail=detail(), scale=texture_scale)))  # floor
     for b in range(3):
         cx = rng.uniform(-0.6, 0.6) * half_w
         cy = rng.uniform(-0.5, 0.3) * half_h
@@ -192,7 +197,7 @@ def make_scene(width=160, height=120, num_src=4, seed=20251114, weak_patches=Tru
         eu = np.array([np.cos(ang), 0, np.sin(ang)]) * sz
         ev = np.array([0, 1.0, rng.uniform(-0.3, 0.3)]) * sz
         bflat = [(0.1 * sz, 0.1 * sz, 0.7 * sz, 0.7 * sz, rng.uniform(60, 200))] if (weak_patches and b == 0) else []
-        quads.append(_Quad([cx, cy, cz], eu, ev, _Texture(rng, base_freq=7.0, flat_patches=bflat, detail=detail())))
+        quads.append(_Quad([cx, cy, cz], eu, ev, _Texture(rng, base_freq=7.0, flat_patches=bflat, detail=detail(), scale=texture_scale)))
 
     # cameras: ref at origin, sources on an arc around the scene centre
     target = np.array([0.0, 0.0, 0.8 * depth])

@@ -37,8 +37,10 @@ Besides the headline the JSON line carries:
                 HIP events on the engine stream, against the FP32 vector peak; HBM bytes per launch from
                 the newest rocprofv3 PMC summary of k_sweep_weak_vm at this shape under profiles/.
   cpu_baseline  the C oracle (oracle/liboracle.so) on a bounded sample of the same workload: the
-                same scene rendered at 756x504 with N = 10, one APD iteration of the same pass, at
-                --cpu-threads cores; plus the same at 1 core on 378x252 (cpu_baseline_1core).
+                same scene rendered at W/4 x H/4 (1512x1008) with its textures scaled 4x in world
+                units (the headline's texture per pixel and WEAK fraction), N = 10, one APD iteration
+                of the same pass, at --cpu-threads cores; plus the same at 1 core on W/16 x H/16
+                (378x252, textures scaled 16x: cpu_baseline_1core).
   end_to_end    one full RunPatchMatch of the headline problem (main.cpp:157-161 bracket).
   c2_first_init configs[1] (3024x2016, N = 8, FIRST_INIT, Strong sweep only): the round-1/2 headline,
                 same fresh-run timing, with the Strong sweep's NCC-Old roofline.
@@ -92,9 +94,9 @@ def latest_pmc(kernel: str, W: int, n_src: int):
     return None
 
 
-def make_scene(W, H, N, world, texture):
+def make_scene(W, H, N, world, texture, texture_scale=1.0):
     import synth
-    return synth.make_scene(W, H, max(N, world), seed=20251114, texture=texture)
+    return synth.make_scene(W, H, max(N, world), seed=20251114, texture=texture, texture_scale=texture_scale)
 
 
 def first_init_priors(eng, sc, ids, N):
@@ -344,12 +346,15 @@ def c2_first_init(eng, steps, warmup):
             "iter_ms_median": round(statistics.median(step_ms), 3), "roofline": roof, "end_to_end": e2e}
 
 
-def cpu_baseline(eng, texture, N, w, h, threads):
+def cpu_baseline(eng, texture, N, w, h, threads, W, H):
     """The C oracle on one APD iteration of the headline pass, on the same scene rendered at w x h
-    (priors from FIRST_INIT runs on the device, which are bit-identical to the oracle's)."""
+    with its smooth textures scaled by W / w in world units, so that the sample has the headline's
+    texture per pixel and WEAK fraction (synth texture_scale); priors from FIRST_INIT runs on the
+    device, which are bit-identical to the oracle's."""
     import ctypes as C
     import oracle_lib
-    sc = make_scene(w, h, N, 1, texture)
+    scale = W / w if texture == "smooth" else 1.0
+    sc = make_scene(w, h, N, 1, texture, texture_scale=scale)
     ids = [0] + [j for j, _ in sc.pairs[0]][:N]
     priors = first_init_priors(eng, sc, ids, N)
     arr = final_round_problem(sc, priors, 0, N)
@@ -364,7 +369,8 @@ def cpu_baseline(eng, texture, N, w, h, threads):
             "weak_frac": round(float((arr.weak_info == 0).mean()), 4),
             "sample": f"oracle (C restatement{', OpenMP' if threads > 1 else ', 1 thread'}) on the headline "
                       f"pass (REFINE_ITER, APD + focal + geom + impetus, final-round params) of the same "
-                      f"synthetic scan rendered at {w}x{h}, N={N}, one loop-body iteration "
+                      f"synthetic scan rendered at {w}x{h} with texture_scale {scale:g} (the headline's texture "
+                      f"per pixel), N={N}, one loop-body iteration "
                       f"(t_iter={t_iter:.2f}s; anchors/RandomInit {times[0]:.2f}s untimed)"}
 
 
@@ -542,8 +548,8 @@ def main():
             del rsc
         cpu = cpu1 = None
         if not args.no_cpu_baseline and single:
-            cpu = cpu_baseline(eng, args.texture, N, 756, 504, args.cpu_threads)
-            cpu1 = cpu_baseline(eng, args.texture, N, 378, 252, 1)
+            cpu = cpu_baseline(eng, args.texture, N, W // 4, H // 4, args.cpu_threads, W, H)
+            cpu1 = cpu_baseline(eng, args.texture, N, W // 16, H // 16, 1, W, H)
         name = workload_name(W, H, N, True)
         line = {
             "metric": METRIC,
