@@ -640,6 +640,11 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     prob.seed = seed ^ ((uint64_t)(uint32_t)job.iteration << 32) ^ (uint64_t)(uint32_t)pb.ref_image_id;
     prob.export_reliable_curve = job.export_curve ? 1 : 0;
     int st = apd_set_problem(ctx, &prob);
+    if (dev && st == APD_OK) {  // test hook: the k-th problem with the device store finds HBM exhausted
+        static std::atomic<int> n_dev_problems{0};
+        const char *e = getenv("APD_TEST_ENOMEM_AT");
+        if (e && ++n_dev_problems == atoi(e)) st = APD_ENOMEM;
+    }
     auto t0 = std::chrono::steady_clock::now();
     if (st == APD_OK) {
         t0 = std::chrono::steady_clock::now();

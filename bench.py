@@ -94,6 +94,19 @@ def latest_pmc(kernel: str, W: int, n_src: int):
     return None
 
 
+def fetch_calibration():
+    """The measured FETCH_SIZE correction for this repo's gather widths (tools/fetch_calib.hip): HBM bytes
+    = factor x FETCH_SIZE + WRITE_SIZE, the factor the PMC summaries' hbm_bytes_per_launch applies."""
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*fetch_calibration*.json")), reverse=True):
+        try:
+            c = json.load(open(f))
+        except Exception:
+            continue
+        c["_file"] = os.path.relpath(f, REPO)
+        return c
+    return None
+
+
 def make_scene(W, H, N, world, texture, texture_scale=1.0):
     import synth
     return synth.make_scene(W, H, max(N, world), seed=20251114, texture=texture, texture_scale=texture_scale)
@@ -198,6 +211,7 @@ def weak_roofline(eng, steps, W, N):
     achieved_issued = flop_issued / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     pmc = latest_pmc("k_sweep_weak_vm", W, N)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    cal = fetch_calibration()
     return {
         "bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
@@ -227,6 +241,8 @@ def weak_roofline(eng, steps, W, N):
         "launches": {"k_gp_cost+k_weak_cand_g+k_weak_cand_comb": cand["launches"], "k_sweep_weak_vm": sweep["launches"],
                      "k_sweep_strong_vm": strong["launches"], "k_ransac_fit": ransac["launches"]},
         "pmc_file": pmc.get("_file") if pmc else None,
+        "traffic_correction_factor": cal.get("correction_factor") if cal else None,
+        "traffic_calibration": cal.get("_file") if cal else None,
     }
 
 

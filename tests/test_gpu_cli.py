@@ -71,14 +71,18 @@ def check_outputs(folder, expected):
     ("jacobi", "0,0", "1"),     # two contexts: host-side state (the device store is single-context)
     ("sequential", "0", "cap"),  # device store capped (APD_DEVICE_STATE_CAP_MB): views that do not fit
     ("jacobi", "0", "cap"),      # ... fall back to the host store, same outputs
+    ("sequential", "0", "oom"),  # a problem finds HBM exhausted (APD_TEST_ENOMEM_AT): the store is released
+    ("jacobi", "0", "oom"),      # and the run continues from the host store, same outputs
 ])
 def test_cli_matches_schedule(scan, engine, ordering, gpus, device_state, tmp_path):
     import shutil
     folder = str(tmp_path / "run")
     shutil.copytree(scan, folder)
-    env = dict(os.environ, APD_DEVICE_STATE="1" if device_state == "cap" else device_state)
+    env = dict(os.environ, APD_DEVICE_STATE="1" if device_state in ("cap", "oom") else device_state)
     if device_state == "cap":  # room for the round's images and a few views' maps, not for all of them
         env["APD_DEVICE_STATE_CAP_MB"] = "40"
+    if device_state == "oom":  # the 13th problem (second round, maps and images resident) runs out
+        env["APD_TEST_ENOMEM_AT"] = "13"
     r = subprocess.run([APD_BIN, "--dense_folder", folder, "--dataset", "ETH3D", "--no_fuse", "true",
                         "--memory_cache", "false", "--gpus", gpus, "--ordering", ordering],
                        capture_output=True, text=True, timeout=600, env=env)
@@ -87,6 +91,8 @@ def test_cli_matches_schedule(scan, engine, ordering, gpus, device_state, tmp_pa
     resident = device_state in ("1", "cap") and "," not in gpus
     if device_state == "cap":
         assert "falls back to the host store" in r.stdout
+    if device_state == "oom":
+        assert "device-resident state released" in r.stdout
     assert ("Device-resident state:" in r.stdout) == resident
     assert r.stdout.count("RunPatchMatch time:") == 5 * 8
     expected = HS.run_schedule(folder, run_engine(engine), ordering=ordering)

@@ -2,8 +2,9 @@
 counters of one kernel and the HBM traffic estimate bench.py reports as roofline.traffic.
     python tools/pmc_json.py <pmc dir> <out.json> [--kernel k_sweep_strong] [--width 3024 --height 2016
                              --n-src 8] [--stats kernel_stats.csv] [--source "..."]
-HBM bytes per launch = 2 x FETCH_SIZE (gfx950 reports half of wide reads, MI355X_MICROARCH.md §HBM)
-+ WRITE_SIZE, both in KiB from rocprofv3; the per-width calibration of narrow gathers is open."""
+HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE, both in KiB from rocprofv3: gfx950 tallies each
+128-B line fill as one 64-B request for every access width these kernels use (4-, 8- and 16-byte
+loads, one or both line halves: profiles/r5_fetch_calibration.json, tools/fetch_calib.hip)."""
 import argparse, csv, glob, json, os, collections
 ap = argparse.ArgumentParser()
 ap.add_argument("src")
@@ -39,7 +40,9 @@ if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
     out["fetch_bytes_raw"] = m["FETCH_SIZE"] * 1024
     out["write_bytes"] = m["WRITE_SIZE"] * 1024
     out["hbm_bytes_per_launch"] = 2 * m["FETCH_SIZE"] * 1024 + m["WRITE_SIZE"] * 1024
-    out["correction"] = "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes); narrow-gather widths uncalibrated"
+    out["correction"] = "2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes)"
+    out["correction_factor"] = 2.0
+    out["correction_calibration"] = "profiles/r5_fetch_calibration.json"
 if "SQ_WAVE_CYCLES" in m:
     w = m["SQ_WAVE_CYCLES"]
     g = lambda k: m.get(k)
