@@ -101,6 +101,9 @@ struct Args {
     // unfiltered, [1] filtered by q's own SA label (when the problem has labels): taps, tap mask and
     // ncc_finalize's reference-side terms -- see AncRec in apd_kernels.hip
     const APD_G uint4 *arec;
+    // DepthToWeak's pre-differenced fp16 texels (tex_f16 problems; null = off, see FastTexD): per padded
+    // pair position k, {pairs[k], (pairs[k + 1] - pairs[k]) / 256}, same stride as pairs
+    const APD_G uint2 *dpairs;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -670,6 +673,59 @@ struct FastTex {
     __device__ __forceinline__ float sample(const Tap &t) const { return finish(t, load(t)); }
 };
 
+// FastTex over pre-differenced fp16 texels (F16 problems; DepthToWeak): the 8-byte record at the tap's
+// base position holds the vertical pair {T(ix,iy), T(ix,iy+1)} and the horizontal differences
+// {(T(ix+1,iy) - T(ix,iy)) / 256, (T(ix+1,iy+1) - T(ix,iy+1)) / 256}, all exact in fp16 (quarter-
+// integer texels in [0, 256): the differences are multiples of 2^-10 below 1 in magnitude, normal
+// fp16). The lerp takes the x fraction as the integer 256 * ax: fma(256 ax, dd / 256, T00) has the
+// exact product ax * dd of fma(ax, dd, T00), hence the same single rounding -- bit-identical to
+// FastTex<true>::finish -- without FastTex's per-tap v_pk_add_f16 for the differences (and the x
+// fraction's 1/256 multiply). Twice the bytes per texel position; for the VALU-bound kernels.
+template <bool UNI>
+struct FastTexD {
+    const APD_G char *base;
+    uint32_t vbase;
+    uint32_t W1;
+    float Wm1, Hm1;
+    static constexpr uint32_t SHIFT = 3u;
+    template <class AT>
+    __device__ __forceinline__ FastTexD(const AT &a, int s) {
+        W1 = SrcTex<true>::pitch(a.W);
+        const int64_t off = ((int64_t)(s - 1) * (int64_t)a.qstride - (int64_t)W1 - 1) * (1 << SHIFT);
+        if constexpr (UNI) {
+            base = (const APD_G char *)a.dpairs + off;
+            vbase = 0u;
+        } else {
+            base = (const APD_G char *)a.dpairs;
+            vbase = (uint32_t)off;
+        }
+        Wm1 = (float)(a.W - 1);
+        Hm1 = (float)(a.H - 1);
+    }
+    struct Tap { uint32_t off; apd_f2 f; };  // f = {256 ax, ay}
+    __device__ __forceinline__ Tap tap(apd_f2 XY, float iz) const {
+        apd_f2 p = XY * iz;
+        p.x = __builtin_amdgcn_fmed3f(p.x, -1.0f, Wm1);
+        p.y = __builtin_amdgcn_fmed3f(p.y, -1.0f, Hm1);
+        const apd_f2 q = pk_fma(p, (apd_f2){256.0f, 256.0f}, (apd_f2){512.5f, 512.5f});
+        const int qx = (int)q.x, qy = (int)q.y;
+        Tap t;
+        t.off = ((__umul24((uint32_t)qy >> 8, W1) + ((uint32_t)qx >> 8)) << SHIFT) + vbase;
+        t.f = (apd_f2){(float)(qx & 255), (float)(qy & 255) * 0.00390625f};
+        return t;
+    }
+    using Raw = uint2;
+    __device__ __forceinline__ Raw load(const Tap &t) const { return *(const APD_G uint2 *)(base + t.off); }
+    __device__ __forceinline__ float finish(const Tap &t, const Raw &v) const {
+        const apd_h2 c0 = __builtin_bit_cast(apd_h2, v.x);  // {T00, T01}
+        const apd_h2 dd = __builtin_bit_cast(apd_h2, v.y);  // {(T10 - T00) / 256, (T11 - T01) / 256}
+        const float top = fma_mix_lo(t.f.x, dd, c0);      // fma(ax, T10 - T00, T00)
+        const float bot = fma_mix_hi(t.f.x, dd, c0);      // fma(ax, T11 - T01, T01)
+        return fmaf(t.f.y, bot - top, top);
+    }
+    __device__ __forceinline__ float sample(const Tap &t) const { return finish(t, load(t)); }
+};
+
 // The 36 taps of a ComputeBilateralNCCOld window (6x6, step 2) and their moments, for a texel source
 // TT with the FastTex interface (tap / load / finish). Accumulation order = the reference's (i outer,
 // j inner). (Factored out of ncc_old_fast; the Strong sweep measured 3 % faster with this form.)
@@ -854,9 +910,11 @@ __device__ __noinline__ float ncc_old_slow(const APD_G Args *ap, int px, int py,
 // is then meaningless (the taps ran on a dummy homography that keeps every address in bounds).
 // RS = LDS stride of the reference window (1: per-pixel contiguous; 64: [k][pixel] layout).
 // (ncc_old_fast_h: the same with the window's homography given, e.g. from precomputed plane_terms)
-template <bool F16, int RS = 1>
+template <bool F16, int RS = 1, bool DP = false>
 __device__ __forceinline__ float ncc_old_fast_h(const Args &a, int px, int py, int s, Hom Hm, const RefWin &rw,
                                                 bool &slow) {
+    // DP: the taps over the pre-differenced texels (FastTexD, F16 problems with a.dpairs)
+    using TT = typename std::conditional<DP && F16, FastTexD<(RS > 1)>, FastTex<F16, (RS > 1)>>::type;
     const int W = a.W, H = a.H;
     float ptx, pty;
     project(Hm, (float)px, (float)py, ptx, pty);
@@ -879,21 +937,21 @@ __device__ __forceinline__ float ncc_old_fast_h(const Args &a, int px, int py, i
         for (int k = 0; k < 9; ++k) Hm.h[k] = (k == 8) ? 1.0f : 0.0f;  // every tap -> texel (0, 0)
     }
     float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-    const FastTex<F16, (RS > 1)> T(a, s);
+    const TT T(a, s);
     if constexpr (RS > 1) {
         if (rw.sa != nullptr) {
             // each branch runs only if some lane of the wave needs it
-            if (__builtin_amdgcn_ballot_w64(!sa_win)) ncc_old_taps<FastTex<F16, true>, RS>(T, Hm, px, py, rw, ss, sss, srs);
+            if (__builtin_amdgcn_ballot_w64(!sa_win)) ncc_old_taps<TT, RS>(T, Hm, px, py, rw, ss, sss, srs);
             if (__builtin_amdgcn_ballot_w64(sa_win)) {
                 const SaWin w = *rw.sa;
                 float s2 = 0.0f, ss2 = 0.0f, rs2 = 0.0f;
-                ncc_old_sa_taps<FastTex<F16, true>, RS>(T, Hm, px, py, rw.r, w, s2, ss2, rs2);
+                ncc_old_sa_taps<TT, RS>(T, Hm, px, py, rw.r, w, s2, ss2, rs2);
                 if (sa_win) return ncc_finalize(w.sr, w.srr, s2, ss2, rs2, (float)(__popc(w.mlo) + __popc(w.mhi)));
             }
             return ncc_old_finish(ss, sss, srs, rw.mean, rw.var);
         }
     }
-    ncc_old_taps<FastTex<F16, (RS > 1)>, RS>(T, Hm, px, py, rw, ss, sss, srs);
+    ncc_old_taps<TT, RS>(T, Hm, px, py, rw, ss, sss, srs);
     return ncc_old_finish(ss, sss, srs, rw.mean, rw.var);
 }
 template <bool F16, int RS = 1>

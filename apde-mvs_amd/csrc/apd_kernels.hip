@@ -176,6 +176,27 @@ __global__ __launch_bounds__(BLOCK) void k_build_pairs(const float *__restrict__
     }
 }
 
+// fp16 vertical pairs -> DepthToWeak's pre-differenced records D[k] = {P[k], (P[k + 1] - P[k]) / 256}
+// (FastTexD in apd_device.h): padded columns 0..W read their right neighbour in the same row; the last
+// padded column (never a tap's base) gets zero differences.
+__global__ __launch_bounds__(BLOCK) void k_build_dpairs(const uint32_t *__restrict__ pairs, uint2 *__restrict__ dpairs,
+                                                      int W, int H, int N, size_t pstride) {
+    const size_t per = (size_t)(W + 2) * (H + 1);
+    const size_t total = per * N;
+    for (size_t i = blockIdx.x * (size_t)BLOCK + threadIdx.x; i < total; i += (size_t)gridDim.x * BLOCK) {
+        const int v = (int)(i / per);
+        const size_t r = i - (size_t)v * per;
+        const int c = (int)(r % (W + 2));
+        const size_t k = (size_t)v * pstride + r;
+        const uint32_t cur = pairs[k], nxt = c < W + 1 ? pairs[k + 1] : cur;
+        const apd_h2 a0 = __builtin_bit_cast(apd_h2, cur), a1 = __builtin_bit_cast(apd_h2, nxt);
+        apd_h2 d;  // exact: quarter-integer texels in [0, 256) (apd_set_problem's fp16 eligibility)
+        d.x = (_Float16)(((float)a1.x - (float)a0.x) * 0.00390625f);
+        d.y = (_Float16)(((float)a1.y - (float)a0.y) * 0.00390625f);
+        dpairs[k] = make_uint2(cur, __builtin_bit_cast(uint32_t, d));
+    }
+}
+
 // Ordered compaction, one workgroup per image row.
 //   mode 0: colour `colour`, weak != WEAK, y < row_limit   (Strong sweep / filter pixel set)
 //   mode 1: colour `colour`, weak == WEAK, y < row_limit   (Weak sweep pixel set)
@@ -2907,7 +2928,7 @@ static inline int dw_chunk(int N, bool geom, size_t extra) {
 static inline size_t dw_lds_bytes(int N, bool geom, int chunk) {
     return sizeof(DwLds) + (size_t)2 * N * VM_P + (size_t)chunk * dw_per_disp(N, geom);
 }
-template <bool F16, bool SA>
+template <bool F16, bool SA, bool DP = false>
 __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, int chunk, int tw) {
     const int N = a.N, W = a.W, H = a.H;
     DwLds &L = *reinterpret_cast<DwLds *>(apd_dyn_lds);
@@ -3048,7 +3069,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
                 bool slow = false;
                 if (eval) {
                     const float3 m = make_float3(ptm[e], ptm[chunk * VM_P + e], ptm[2 * chunk * VM_P + e]);
-                    tc = ncc_old_fast_h<F16, VM_P>(a, qx, qy, v + 1, homography_terms(a, v + 1, m), rwq, slow);
+                    tc = ncc_old_fast_h<F16, VM_P, DP>(a, qx, qy, v + 1, homography_terms(a, v + 1, m), rwq, slow);
                     if (slow) defer |= 1ull << k;
                 }
                 float g = 0.0f;
@@ -3567,7 +3588,7 @@ struct apd_ctx {
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
         fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, lrs, wcur, arec,
-        wlist, gp_cb, gp_cnt, gp_cur, gp_refs, gp_ccnt, gp_cbase, gp_plist, gp_pidx, gp_pcost, gp_tmp;
+        wlist, gp_cb, gp_cnt, gp_cur, gp_refs, gp_ccnt, gp_cbase, gp_plist, gp_pidx, gp_pcost, gp_tmp, dpairs;
     int n_near = 0;
     int host_stat[4] = {0, 0, 0, 0};  // apd_set_problem's read-back (see there)
     int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
@@ -3581,6 +3602,7 @@ struct apd_ctx {
                                    // leaves them to the sweep
     bool gp_on = false;            // the pair table of the prepared problem is built (apd_stage_prepare)
     bool rec_on = false;           // the anchor-window records of the prepared problem are built (k_anchor_rec)
+    bool dtex = true;              // DepthToWeak over pre-differenced fp16 texels (FastTexD); APD_NO_DTEX=1 disables
     int gp_np = 0;                 // its distinct pairs
     bool lr_handover = true;       // LocalRefine reads DepthToWeak's samples; APD_NO_LR_HANDOVER=1 disables
     bool wcur_on = true;           // RandomInit keeps WEAK current-plane costs for iteration 0; APD_NO_WCUR=1 disables
@@ -3792,6 +3814,7 @@ apd_ctx *apd_create(int32_t device) {
     ctx->cand_pairs = getenv("APD_NO_CAND_PAIRS") == nullptr;
     ctx->lr_handover = getenv("APD_NO_LR_HANDOVER") == nullptr;
     ctx->wcur_on = getenv("APD_NO_WCUR") == nullptr;
+    ctx->dtex = getenv("APD_NO_DTEX") == nullptr;
     // tile_pix needs the tile width to divide the 64-pixel tile (otherwise two workgroups share pixels)
     if (const char *e = getenv("APD_DW_TILE_W")) {
         const int t = atoi(e);
@@ -3812,6 +3835,7 @@ apd_ctx *apd_create(int32_t device) {
         (const void *)k_sweep_weak_vm<true, true, true>, (const void *)k_sweep_weak_vm<false, true, true>,
         (const void *)k_depth_to_weak_vm<true, false>, (const void *)k_depth_to_weak_vm<false, false>,
         (const void *)k_depth_to_weak_vm<true, true>, (const void *)k_depth_to_weak_vm<false, true>,
+        (const void *)k_depth_to_weak_vm<true, false, true>, (const void *)k_depth_to_weak_vm<true, true, true>,
         (const void *)k_local_refine_vm<true, false>, (const void *)k_local_refine_vm<false, false>,
         (const void *)k_local_refine_vm<true, true>, (const void *)k_local_refine_vm<false, true>,
         (const void *)k_random_init_vm<true, false, false>, (const void *)k_random_init_vm<false, false, false>,
@@ -3831,7 +3855,7 @@ void apd_destroy(apd_ctx *ctx) {
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
                       &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand, &ctx->arec,
                       &ctx->lrs, &ctx->wcur, &ctx->wlist, &ctx->gp_cb, &ctx->gp_cnt, &ctx->gp_cur, &ctx->gp_refs, &ctx->gp_ccnt,
-                      &ctx->gp_cbase, &ctx->gp_plist, &ctx->gp_pidx, &ctx->gp_pcost, &ctx->gp_tmp};
+                      &ctx->gp_cbase, &ctx->gp_plist, &ctx->gp_pidx, &ctx->gp_pcost, &ctx->gp_tmp, &ctx->dpairs};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
@@ -4436,8 +4460,22 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
         const int dwc = dw_chunk(a.N, a.geom != 0, sa_lds_bytes(a));
         Args ad = a;
         ad.evals = (ctx->prof && ctx->evals.p) ? (APD_G unsigned long long *)ctx->evals.p : nullptr;
+        // fp16 problems: DepthToWeak's taps over pre-differenced texels (FastTexD; optional buffer,
+        // 8 B per padded texel position and view, built from the pairs here)
+        const size_t dpn = a.qstride * (size_t)a.N;
+        const bool dp = a.tex_f16 && ctx->dtex && try_ensure(ctx, ctx->dpairs, dpn * sizeof(uint2));
+        if (dp)
+            hipLaunchKernelGGL(k_build_dpairs, dim3((unsigned)std::min<size_t>(blocks_for(dpn, BLOCK), 65535u * 8u)), dim3(BLOCK), 0, s,
+                               (const uint32_t *)ctx->quad.p, (uint2 *)ctx->dpairs.p, a.W, a.H, a.N, a.qstride);
         hipEvent_t e0 = prof_begin(ctx);
-        LAUNCH_TEX_SA(k_depth_to_weak_vm, dim3(nb), dim3(VM_BLOCK), dw_lds_bytes(a.N, a.geom != 0, dwc) + sa_lds_bytes(a), s, ad, dwc, tw);
+        if (dp) {
+            ad.dpairs = devptr<decltype(ad.dpairs)>(ctx->dpairs.p);
+            const size_t lds = dw_lds_bytes(a.N, a.geom != 0, dwc) + sa_lds_bytes(a);
+            if (a.sa_any) hipLaunchKernelGGL((k_depth_to_weak_vm<true, true, true>), dim3(nb), dim3(VM_BLOCK), lds, s, ad, dwc, tw);
+            else hipLaunchKernelGGL((k_depth_to_weak_vm<true, false, true>), dim3(nb), dim3(VM_BLOCK), lds, s, ad, dwc, tw);
+        } else {
+            LAUNCH_TEX_SA(k_depth_to_weak_vm, dim3(nb), dim3(VM_BLOCK), dw_lds_bytes(a.N, a.geom != 0, dwc) + sa_lds_bytes(a), s, ad, dwc, tw);
+        }
         prof_end(ctx, e0, APD_PROF_DEPTH_TO_WEAK, a.HW);
     }
     if (a.geom || a.use_apd) hipLaunchKernelGGL(k_confidence, dim3(gpx), dim3(BLOCK), 0, s, a);
