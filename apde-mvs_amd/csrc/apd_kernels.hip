@@ -1317,9 +1317,11 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 // ---------------------------------------------------------------------------------------------
 // NCC-New reference side of a pixel slot (anchors, window taps, SA tap masks, moments): shared by the
 // Weak sweep and RandomInitialization under APD
-// NWIN: windows held in LDS -- 9 (RandomInitialization), or 1 (the Weak sweep: the centre window;
-// the anchor windows' reference side comes from the image-wide records AncRec, which depend on the
-// anchor alone, so 16 KiB less LDS per workgroup and four workgroups per CU instead of three)
+// NWIN: windows held in LDS (9: the centre window and the 8 anchor windows). (Round 4's variant with
+// only the centre window in LDS and the anchor windows' reference side read from k_anchor_rec's
+// image-wide records at four workgroups per CU measured equal over the whole C3 N = 10 scan --
+// profiles/r5_scan_c3_n10_rec_vs_lds.txt -- and +11 % at N = 25, since its record loads scale with the
+// evaluations per pixel while this layout builds each window once per pixel; it was retired in round 5.)
 template <bool F16, int NWIN = 9>
 struct WvRefT {
     uint64_t tmask0[VM_P];       // SA tap masks (all ones without SA)
@@ -1334,12 +1336,10 @@ struct WvRefT {
     // [tap][p]: window 0 taps 0..35 (6x6, step 2), anchor k taps 36+9(k-1).. (3x3, step 5); fp16 when
     // the images are (exactly) fp16-representable, see apd_set_problem
     typename std::conditional<F16, _Float16, float>::type rref[(36 + 9 * (NWIN - 1)) * VM_P];
-    uint16_t tmask[(NWIN > 1 ? NWIN - 1 : 1) * VM_P];
+    uint16_t tmask[(NWIN - 1) * VM_P];
     uint32_t box[2 * VM_P];      // bounding box of the anchors 0..8 (x0 | y0 << 16, x1 | y1 << 16)
 };
-// the Weak sweep's per-workgroup state: the reference side plus the hypotheses and per-pixel state.
-// NWIN = 9: every window's reference side in LDS (the default); NWIN = 1: the centre window's only,
-// the anchor windows' from their records (APD_WEAK_REC=1, see k_sweep_weak_vm)
+// the Weak sweep's per-workgroup state: the reference side plus the hypotheses and per-pixel state
 template <bool F16, int NWIN = 9>
 struct WvLdsT : WvRefT<F16, NWIN> {
     float4 hyp[9 * VM_P];        // [h][p]: anchor planes 1..8 (if STRONG) + current; P4 overwrites [0..4]
@@ -1353,12 +1353,9 @@ struct WvLdsT : WvRefT<F16, NWIN> {
 };
 #define WV_CAND(L) ((L).hyp)
 // With the direct 5-slot cost table at N = 10 (fp16 reference taps): 49.5 KiB (three workgroups per
-// CU), or 33.5 KiB with the anchor records (four per CU). (The sweep's own candidate path, a 9-slot
-// table, runs one fewer per CU.)
+// CU). (The sweep's own candidate path, a 9-slot table, runs one fewer per CU.)
 static_assert(sizeof(WvLdsT<true, 9>) + 5 * 10 * VM_P * sizeof(float) + 10 * VM_P <= 160 * 1024 / 3,
               "k_sweep_weak_vm (direct) at N = 10 must fit three workgroups per CU (160 KiB LDS)");
-static_assert(sizeof(WvLdsT<true, 1>) + 5 * 10 * VM_P * sizeof(float) + 10 * VM_P <= 160 * 1024 / 4,
-              "k_sweep_weak_vm<REC> (direct) at N = 10 must fit four workgroups per CU (160 KiB LDS)");
 // `direct` (the pair-table kernels handled every pixel): the sweep reads the anchor candidates'
 // costs from their buffer in P2 and its table holds [5][N][64] (current plane, fit plane,
 // refinement candidates) instead of [9][N][64]: 48 KiB at N = 10, three workgroups per CU instead of two.
@@ -1411,9 +1408,8 @@ __device__ __forceinline__ void ncc_new_window_slow(const Args &a, RT rb,
         }
     }
 }
-// RT: the reference taps' type (LDS or registers). PIPE: the centre window's columns software-
-// pipelined (more gathers in flight, ~30 more VGPRs; off in the Weak sweep, which runs four
-// workgroups per CU within 128 VGPRs)
+// RT: the reference taps' type (LDS, or registers: k_gp_cost's anchor records). PIPE: the centre
+// window's columns software-pipelined (more gathers in flight, ~30 more VGPRs)
 template <bool F16, int NW, int INC, bool PIPE = true, class RT = const typename std::conditional<F16, _Float16, float>::type *>
 __device__ __forceinline__ void ncc_new_window(const Args &a, RT rb,
                                                int rs, uint64_t mask, const Hom &Hm, int ax, int ay, bool live,
@@ -1741,19 +1737,12 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
         float ss = 0.0f, sss = 0.0f, srs = 0.0f;
         float inv, srp, var;
         if (k == 0) {
-            ncc_new_window<F16, 6, 2, NWIN == 9>(a, &L.rref[p], VM_P, SA ? L.tmask0[p] : ~0ull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            ncc_new_window<F16, 6, 2>(a, &L.rref[p], VM_P, SA ? L.tmask0[p] : ~0ull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
             inv = L.winv[p]; srp = L.wsrp[p]; var = L.wvar[p];
-        } else if constexpr (NWIN > 1) {
+        } else {
             ncc_new_window<F16, 3, 5>(a, &L.rref[(36 + 9 * (k - 1)) * VM_P + p], VM_P,
                                       SA ? (uint64_t)L.tmask[(k - 1) * VM_P + p] : 0x1FFull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
             inv = L.winv[k * VM_P + p]; srp = L.wsrp[k * VM_P + p]; var = L.wvar[k * VM_P + p];
-        } else {
-            // NWIN == 1: the anchor window's reference side from its record. Every lane loads (the
-            // window's code is converged); lanes without this anchor read pixel 0's record, as their
-            // (px, py) may be an unused slot's
-            const AncRecV<F16> R = load_anc_rec<F16>(a, has ? ax + ay * W : 0, (SA && has && ((L.flags[p] >> 29) & 1u)) ? 1 : 0);
-            ncc_new_window<F16, 3, 5>(a, R, 1, SA ? (uint64_t)R.mask() : 0x1FFull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
-            inv = R.inv(); srp = R.srp(); var = R.var();
         }
         if (!live) continue;
         if (nwc) { if (k == 0) ++*nwc; else ++*nwa; }  // (profiling: windows evaluated)
@@ -1788,10 +1777,8 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
     return (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
 }
 
-// Occupancy: REC = false (default) runs three workgroups per CU (LDS-bound, ~166 VGPRs); REC = true
-// (APD_WEAK_REC=1) four, within 128 VGPRs (the centre window without its column pipeline): -2 % on
-// the C3 headline pass but +11 % of Weak-sweep time over a whole C3-shaped scan, whose passes start
-// from converged priors (profiles/r4_scan_c3_26v_rec_vs_lds.txt) -- so the LDS variant is the default.
+// Occupancy: three workgroups per CU (LDS-bound at 49.5 KiB, ~161 VGPRs). Four would need both the
+// LDS below 40 KiB and the registers within 128 (124 B per lane of spills today).
 #ifndef WV_WAVES
 #define WV_WAVES 4  // waves per Weak-sweep workgroup (64 pixels)
 #endif
@@ -1803,10 +1790,10 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
 #endif
 #define WV_BLOCK (WV_WAVES * WAVE)
 #ifndef WV_LDS_OCC
-#define WV_LDS_OCC 3  // workgroups per CU the LDS variant's registers are bounded for
+#define WV_LDS_OCC 3  // workgroups per CU the registers are bounded for
 #endif
-template <bool F16, bool SA, bool REC = false>
-__global__ __launch_bounds__(WV_BLOCK, REC ? 4 : WV_LDS_OCC) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
+template <bool F16, bool SA>
+__global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
                                                                 int iter, const float *__restrict__ cand, int wc) {
     const int N = a.N, W = a.W;
     PHASE_BEGIN;
@@ -1815,7 +1802,7 @@ __global__ __launch_bounds__(WV_BLOCK, REC ? 4 : WV_LDS_OCC) void k_sweep_weak_v
     // without them (cand == nullptr: APD_NO_CAND_PAIRS=1 or a pair table that does not fit) P1
     // evaluates the candidates here
     const bool direct = cand != nullptr;
-    WvLdsT<F16, REC ? 1 : 9> &L = *reinterpret_cast<WvLdsT<F16, REC ? 1 : 9> *>(apd_dyn_lds);
+    WvLdsT<F16, 9> &L = *reinterpret_cast<WvLdsT<F16, 9> *>(apd_dyn_lds);
     float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64] (direct: [N][64]), later [5][N][64]
     uint8_t *wts = reinterpret_cast<uint8_t *>(costL + (direct ? 5 : 9) * N * VM_P);  // [N][64] view weights
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
@@ -3595,7 +3582,6 @@ struct apd_ctx {
     Args args{};
     bool loaded = false, prepared = false;
     int dw_tile_w = 8;             // DepthToWeak pixel tile width (64 / tile height); APD_DW_TILE_W
-    bool weak_rec = false;         // APD_WEAK_REC=1: the Weak sweep with anchor records (four workgroups per CU)
     int tile_w = 16;               // sweep list tile width (tile = tile_w x 256/tile_w positions); APD_TILE_W
                                    // (16 x 16: -1 % per C3 iteration against 8 x 32, profiles/r4_ab_tile_shape.txt)
     bool cand_pairs = true;        // Weak sweep candidates through the image-wide pair table; APD_NO_CAND_PAIRS=1
@@ -3732,17 +3718,6 @@ static inline T devptr(const void *p) { return reinterpret_cast<T>(reinterpret_c
 
 // ... and of its SA-masked (SA quadrant windows on the fast taps) or unmasked form
 // (the same with a third template argument)
-#define LAUNCH_TEX_SA3(kern, t3, grid, block, lds, stream, ...)                                     \
-    do {                                                                                         \
-        const bool sa_ = ctx->args.sa_any != 0;                                                  \
-        if (ctx->args.tex_f16) {                                                                 \
-            if (sa_) hipLaunchKernelGGL((kern<true, true, t3>), grid, block, lds, stream, __VA_ARGS__); \
-            else hipLaunchKernelGGL((kern<true, false, t3>), grid, block, lds, stream, __VA_ARGS__);  \
-        } else {                                                                                 \
-            if (sa_) hipLaunchKernelGGL((kern<false, true, t3>), grid, block, lds, stream, __VA_ARGS__); \
-            else hipLaunchKernelGGL((kern<false, false, t3>), grid, block, lds, stream, __VA_ARGS__); \
-        }                                                                                        \
-    } while (0)
 #define LAUNCH_TEX_SA(kern, grid, block, lds, stream, ...)                                          \
     do {                                                                                         \
         const bool sa_ = ctx->args.sa_any != 0;                                                  \
@@ -3820,7 +3795,6 @@ apd_ctx *apd_create(int32_t device) {
         const int t = atoi(e);
         if (t == 1 || t == 2 || t == 4 || t == 8 || t == 16 || t == 32 || t == 64) ctx->dw_tile_w = t;
     }
-    ctx->weak_rec = getenv("APD_WEAK_REC") != nullptr && atoi(getenv("APD_WEAK_REC")) != 0;
     if (const char *e = getenv("APD_TILE_W")) {
         const int t = atoi(e);
         if (t == 4 || t == 8 || t == 16 || t == 32 || t == 64) ctx->tile_w = t;
@@ -3831,8 +3805,6 @@ apd_ctx *apd_create(int32_t device) {
         (const void *)k_sweep_strong_vm<true, true>, (const void *)k_sweep_strong_vm<false, true>,
         (const void *)k_sweep_weak_vm<true, false>, (const void *)k_sweep_weak_vm<false, false>,
         (const void *)k_sweep_weak_vm<true, true>, (const void *)k_sweep_weak_vm<false, true>,
-        (const void *)k_sweep_weak_vm<true, false, true>, (const void *)k_sweep_weak_vm<false, false, true>,
-        (const void *)k_sweep_weak_vm<true, true, true>, (const void *)k_sweep_weak_vm<false, true, true>,
         (const void *)k_depth_to_weak_vm<true, false>, (const void *)k_depth_to_weak_vm<false, false>,
         (const void *)k_depth_to_weak_vm<true, true>, (const void *)k_depth_to_weak_vm<false, true>,
         (const void *)k_depth_to_weak_vm<true, false, true>, (const void *)k_depth_to_weak_vm<true, true, true>,
@@ -4275,12 +4247,11 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
             (void)hipEventRecord(ctx->ev[14], s);
         }
         // the anchor windows' reference side (k_anchor_rec: taps, tap mask, finalisation terms; 32 B
-        // with fp16 taps, else 64 B, per pixel and SA variant), built only when a kernel reads it --
-        // k_gp_cost, or the APD_WEAK_REC sweep. Optional: without room the pair table is dropped (the
-        // sweep evaluates the candidates itself) and the sweep runs its LDS variant.
+        // with fp16 taps, else 64 B, per pixel and SA variant), built only when k_gp_cost reads it.
+        // Optional: without room the pair table is dropped (the sweep evaluates the candidates itself).
         ctx->rec_on = false;
         a.arec = nullptr;
-        if (a.use_apd && ((ctx->gp_on && ctx->gp_np > 0) || ctx->weak_rec)) {
+        if (a.use_apd && ctx->gp_on && ctx->gp_np > 0) {
             const size_t rb = (size_t)a.HW * (a.sa_any ? 2 : 1) * (a.tex_f16 ? 2 : 4) * sizeof(uint4);
             if (try_ensure(ctx, ctx->arec, rb)) {
                 a.arec = devptr<decltype(a.arec)>(ctx->arec.p);
@@ -4289,7 +4260,7 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
                 else hipLaunchKernelGGL(k_anchor_rec<false>, dim3(g), dim3(BLOCK), 0, s, a, (uint4 *)ctx->arec.p);
                 if ((st = check_launch(ctx, "k_anchor_rec"))) return st;
                 ctx->rec_on = true;
-            } else if (ctx->gp_on && ctx->gp_np > 0) {
+            } else {
                 ctx->gp_on = false;
             }
         }
@@ -4414,14 +4385,9 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             e0 = prof_begin(ctx);
             // k_sweep_weak_vm's small cost table when every pixel's candidates are in `cand`
             const bool direct = cand != nullptr;
-            if (ctx->weak_rec && ctx->rec_on)
-                LAUNCH_TEX_SA3(k_sweep_weak_vm, true, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
-                              (ctx->args.tex_f16 ? wv_lds_bytes<true, 1>(a.N, direct) : wv_lds_bytes<false, 1>(a.N, direct)), s,
-                              aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
-            else
-                LAUNCH_TEX_SA3(k_sweep_weak_vm, false, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
-                              (ctx->args.tex_f16 ? wv_lds_bytes<true, 9>(a.N, direct) : wv_lds_bytes<false, 9>(a.N, direct)), s,
-                              aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
+            LAUNCH_TEX_SA(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
+                          (ctx->args.tex_f16 ? wv_lds_bytes<true, 9>(a.N, direct) : wv_lds_bytes<false, 9>(a.N, direct)), s,
+                          aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
             prof_end(ctx, e0, APD_PROF_WEAK_SWEEP, n);
         }
         if ((st = check_launch(ctx, "weak sweep"))) return st;

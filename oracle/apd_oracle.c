@@ -1706,8 +1706,10 @@ int oracle_run_patchmatch(const apd_problem *pb, const apd_outputs *out, int nth
     (void)nthreads;
 #endif
 #ifdef ORACLE_FASTMATH
-    /* flush denormals in this thread and in every pool thread (libgomp keeps its pool) */
-    _mm_setcsr(_mm_getcsr() | 0x8040u);
+    /* flush denormals (FTZ | DAZ) in this thread and in the OpenMP team, restored before returning:
+       the process's other code (the parity oracle, numpy) shares the thread pool */
+    const unsigned csr0 = _mm_getcsr();
+    _mm_setcsr(csr0 | 0x8040u);
 #ifdef _OPENMP
 #pragma omp parallel
     _mm_setcsr(_mm_getcsr() | 0x8040u);
@@ -1729,6 +1731,13 @@ int oracle_run_patchmatch(const apd_problem *pb, const apd_outputs *out, int nth
     if (out) ctx_output(o, out);
     ctx_free(o);
     free(o);
+#ifdef ORACLE_FASTMATH
+#ifdef _OPENMP
+#pragma omp parallel
+    _mm_setcsr(_mm_getcsr() & ~0x8040u);
+#endif
+    _mm_setcsr(csr0);
+#endif
     return APD_OK;
 }
 
