@@ -1410,16 +1410,17 @@ __device__ __forceinline__ void ncc_new_window_slow(const Args &a, RT rb,
 }
 // RT: the reference taps' type (LDS, or registers: k_gp_cost's anchor records). PIPE: the centre
 // window's columns software-pipelined (more gathers in flight, ~30 more VGPRs)
-template <bool F16, int NW, int INC, bool PIPE = true, class RT = const typename std::conditional<F16, _Float16, float>::type *>
+template <bool F16, int NW, int INC, bool PIPE = true, class RT = const typename std::conditional<F16, _Float16, float>::type *,
+          class TT = FastTex<F16, true>>
 __device__ __forceinline__ void ncc_new_window(const Args &a, RT rb,
                                                int rs, uint64_t mask, const Hom &Hm, int ax, int ay, bool live,
-                                               bool fast, const FastTex<F16, true> &T, const SrcTex<F16> &Q, float &ss,
+                                               bool fast, const TT &T, const SrcTex<F16> &Q, float &ss,
                                                float &sss, float &srs) {
     const uint64_t sm = __ballot(live && !fast);
     // only the lanes whose window is evaluated issue its gathers (the gather path's cost is per
-    // active lane); the others are exec-masked off instead of sampling a parked homography
+    // active lane); the others are exec-masked off instead of sampling a parked homography.
+    // TT: FastTex, or FastTexD (pre-differenced fp16 texels, the same values)
     if (live && fast) {
-        using TT = FastTex<F16, true>;
         auto column = [&](int i, typename TT::Tap *t) {
             const float x = (float)(ax - 5 + INC * i);
             const apd_f2 cxy = {fmaf(Hm.h[0], x, Hm.h[2]), fmaf(Hm.h[3], x, Hm.h[5])};
@@ -1662,16 +1663,18 @@ __device__ __forceinline__ AncRecV<F16> load_anc_rec(const Args &a, int q, int f
 // SA = false: no SA masks in this problem, so every window's tap mask is full (compile-time constant:
 // no per-tap mask selects). BOX: L.box holds the pixel's anchor bounding box, and one
 // window_rcp_ok_box over it (taps included) stands for the per-window checks when it holds.
-template <bool F16, bool SA = true, bool BOX = false, int NWIN>
+template <bool F16, bool SA = true, bool BOX = false, int NWIN, bool DP = false>
 __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWIN> &L, int p, int px, int py, int s, float4 pl,
                                             bool want, bool *seldep = nullptr, uint32_t *nwc = nullptr,
                                             uint32_t *nwa = nullptr) {
+    // DP: the windows' taps over the pre-differenced fp16 texels (FastTexD, a.dpairs)
+    using TT = typename std::conditional<DP && F16, FastTexD<true>, FastTex<F16, true>>::type;
     const int W = a.W, H = a.H;
     const Hom Hm = homography(a, s, pl);
     float ptx, pty;
     project(Hm, (float)px, (float)py, ptx, pty);
     bool alive = want && !(ptx >= (float)W || ptx < 0.0f || pty >= (float)H || pty < 0.0f);
-    const FastTex<F16, true> T(a, s);
+    const TT T(a, s);
     const SrcTex<F16> Q(a, s);
     const uint32_t awin = (L.flags[p] >> 16) & 0x1FFu;
     float sc[9];
@@ -1792,7 +1795,7 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
 #ifndef WV_LDS_OCC
 #define WV_LDS_OCC 3  // workgroups per CU the registers are bounded for
 #endif
-template <bool F16, bool SA>
+template <bool F16, bool SA, bool DP = false>
 __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
                                                                 int iter, const float *__restrict__ cand, int wc) {
     const int N = a.N, W = a.W;
@@ -1886,7 +1889,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
         const bool want = pv1 && ((L.flags[p1] >> h) & 1u);
         const float4 pl = L.hyp[h * VM_P + p1];
-        const float nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
+        const float nv = ncc_new_vm<F16, SA, true, 9, DP>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
         if (want) val = nv;
         costL[t * VM_P + p1] = val;
     }
@@ -1998,7 +2001,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
             if (iter == 0 && a.wcur && !__ballot(want && __builtin_isnan(kept)))
                 nv = kept;
             else
-                nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
+                nv = ncc_new_vm<F16, SA, true, 9, DP>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
             if (want) {
                 val = nv;
                 if (geom) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
@@ -2090,7 +2093,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
             const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[p1];
             LANE_STAT(22, want);
             const float4 fit = fit1;
-            const float nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, fit, want, nullptr, &nwc, &nwa);
+            const float nv = ncc_new_vm<F16, SA, true, 9, DP>(a, L, p1, px1, py1, v + 1, fit, want, nullptr, &nwc, &nwa);
             if (want) {
                 cv = nv;
                 if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, fit), cv);
@@ -2188,7 +2191,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
                     const int px = pxy & 0xFFFF, py = pxy >> 16;
                     const float4 tp = WV_CAND(L)[k * VM_P + p];
                     LANE_STAT(20, want);
-                    const float nv = ncc_new_vm<F16, SA, true>(a, L, p, px, py, v + 1, tp, want, nullptr, &nwc, &nwa);
+                    const float nv = ncc_new_vm<F16, SA, true, 9, DP>(a, L, p, px, py, v + 1, tp, want, nullptr, &nwc, &nwa);
                     if (want) {
                         float cv = nv;
                         if (geom) cv = fmaf(gf, geom_cost(a, px, py, v + 1, tp), cv);
@@ -2230,7 +2233,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
             const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[(1 + k) * VM_P + p1];
             LANE_STAT(20, want);
             const float4 tp = WV_CAND(L)[k * VM_P + p1];
-            const float nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, tp, want, nullptr, &nwc, &nwa);
+            const float nv = ncc_new_vm<F16, SA, true, 9, DP>(a, L, p1, px1, py1, v + 1, tp, want, nullptr, &nwc, &nwa);
             if (want) {
                 cv = nv;
                 if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
@@ -2653,9 +2656,11 @@ __device__ __forceinline__ float gp_combine(float cc, const float (&sc)[8]) {
 // anchor 0 projected out of frame). With an SA label at the pixel the centre window is used only
 // when anchor 0 carries the label (else center_cost stays 0, APD.cu:493-497) and its taps are
 // filtered by it (APD.cu:526-530); an empty window leaves center_cost 0 (APD.cu:543).
-template <bool F16, bool SA>
+template <bool F16, bool SA, bool DP = false>
 __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__restrict__ list, int count,
                                                           const uint8_t *__restrict__ cbw, float *__restrict__ out, int wc) {
+    // DP: the centre windows' taps over the pre-differenced fp16 texels (FastTexD, a.dpairs)
+    using TT = typename std::conditional<DP && F16, FastTexD<true>, FastTex<F16, true>>::type;
     // (fp16 reference taps when the images are: fp32 measured 6 % slower, profiles/r4_ab_cand_g_fp32_ref.txt)
     using RT = typename std::conditional<F16, _Float16, float>::type;
     __shared__ RT cref[36 * VM_P];
@@ -2734,7 +2739,7 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
     uint32_t nlive = 0;
     for (int v = 0; v < N; ++v) {
         const int s = v + 1;
-        const FastTex<F16, true> T(a, s);
+        const TT T(a, s);
         const SrcTex<F16> Q(a, s);
         const Hom Hm = homography(a, s, pl);
         float ptx, pty;
@@ -3588,7 +3593,9 @@ struct apd_ctx {
                                    // leaves them to the sweep
     bool gp_on = false;            // the pair table of the prepared problem is built (apd_stage_prepare)
     bool rec_on = false;           // the anchor-window records of the prepared problem are built (k_anchor_rec)
-    bool dtex = true;              // DepthToWeak over pre-differenced fp16 texels (FastTexD); APD_NO_DTEX=1 disables
+    bool dtex = true;              // pre-differenced fp16 texels (FastTexD) for the VALU-bound kernels; APD_NO_DTEX=1 disables
+    bool dtex_cand = true;         // ... in k_weak_cand_g (APD_NO_DTEX_CAND=1: the plain pairs there only)
+    bool dtex_sweep = false;       // ... in k_sweep_weak_vm (APD_DTEX_SWEEP=1; A/B)
     int gp_np = 0;                 // its distinct pairs
     bool lr_handover = true;       // LocalRefine reads DepthToWeak's samples; APD_NO_LR_HANDOVER=1 disables
     bool wcur_on = true;           // RandomInit keeps WEAK current-plane costs for iteration 0; APD_NO_WCUR=1 disables
@@ -3790,6 +3797,8 @@ apd_ctx *apd_create(int32_t device) {
     ctx->lr_handover = getenv("APD_NO_LR_HANDOVER") == nullptr;
     ctx->wcur_on = getenv("APD_NO_WCUR") == nullptr;
     ctx->dtex = getenv("APD_NO_DTEX") == nullptr;
+    ctx->dtex_cand = getenv("APD_NO_DTEX_CAND") == nullptr;
+    ctx->dtex_sweep = getenv("APD_DTEX_SWEEP") != nullptr;
     // tile_pix needs the tile width to divide the 64-pixel tile (otherwise two workgroups share pixels)
     if (const char *e = getenv("APD_DW_TILE_W")) {
         const int t = atoi(e);
@@ -3805,6 +3814,7 @@ apd_ctx *apd_create(int32_t device) {
         (const void *)k_sweep_strong_vm<true, true>, (const void *)k_sweep_strong_vm<false, true>,
         (const void *)k_sweep_weak_vm<true, false>, (const void *)k_sweep_weak_vm<false, false>,
         (const void *)k_sweep_weak_vm<true, true>, (const void *)k_sweep_weak_vm<false, true>,
+        (const void *)k_sweep_weak_vm<true, false, true>, (const void *)k_sweep_weak_vm<true, true, true>,
         (const void *)k_depth_to_weak_vm<true, false>, (const void *)k_depth_to_weak_vm<false, false>,
         (const void *)k_depth_to_weak_vm<true, true>, (const void *)k_depth_to_weak_vm<false, true>,
         (const void *)k_depth_to_weak_vm<true, false, true>, (const void *)k_depth_to_weak_vm<true, true, true>,
@@ -3838,6 +3848,14 @@ void apd_destroy(apd_ctx *ctx) {
 }
 
 const char *apd_last_error(const apd_ctx *ctx) { return ctx ? ctx->err.c_str() : g_global_err; }
+
+// ensure() for optional buffers: a failed allocation leaves no error behind (the caller falls back)
+static bool try_ensure(apd_ctx *ctx, DevBuf &b, size_t bytes) {
+    if (ensure(ctx, b, bytes) == APD_OK) return true;
+    (void)hipGetLastError();
+    ctx->err.clear();
+    return false;
+}
 
 int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     if (!ctx || !pb) return APD_EINVAL;
@@ -4028,6 +4046,16 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
                                (float4 *)ctx->quad.p, W, H, N, qstride);
         if ((st = check_launch(ctx, "k_build_quads"))) return st;
     }
+    // fp16 problems: the pre-differenced texel records (FastTexD) of DepthToWeak and the anchor
+    // candidates' centre windows, 8 B per padded texel position and view (2 GB at C3); optional
+    a.dpairs = nullptr;
+    if (tex_f16 && ctx->dtex && try_ensure(ctx, ctx->dpairs, qstride * (size_t)N * sizeof(uint2))) {
+        const size_t dpn = qstride * (size_t)N;
+        hipLaunchKernelGGL(k_build_dpairs, dim3((unsigned)std::min<size_t>(blocks_for(dpn, BLOCK), 65535u * 8u)), dim3(BLOCK), 0, s,
+                           (const uint32_t *)ctx->quad.p, (uint2 *)ctx->dpairs.p, W, H, N, qstride);
+        if ((st = check_launch(ctx, "k_build_dpairs"))) return st;
+        a.dpairs = devptr<decltype(a.dpairs)>(ctx->dpairs.p);
+    }
     ctx->want_curve = pb->export_reliable_curve != 0;
     if (ctx->want_curve) {  // DepthToWeak cost curves (APD.cu:2188-2198, 2713-2724)
         if ((st = ensure(ctx, ctx->curve, HW * 61 * sizeof(float)))) return st;
@@ -4104,13 +4132,6 @@ static int *list_ptr(apd_ctx *ctx, int which) {
     return base + off;
 }
 
-// ensure() for optional buffers: a failed allocation leaves no error behind (the caller falls back)
-static bool try_ensure(apd_ctx *ctx, DevBuf &b, size_t bytes) {
-    if (ensure(ctx, b, bytes) == APD_OK) return true;
-    (void)hipGetLastError();
-    ctx->err.clear();
-    return false;
-}
 
 // exclusive prefix sum of n ints (rocPRIM) on the ctx stream
 static int exclusive_scan_int(apd_ctx *ctx, const int *in, int *out, size_t n) {
@@ -4364,8 +4385,15 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
                                (const int2 *)ctx->gp_plist.p, ctx->gp_np, (float *)ctx->gp_pcost.p);
                 prof_end(ctx, e1, APD_PROF_GP_COST, ctx->gp_np);
                 e1 = prof_begin(ctx);
-                LAUNCH_TEX_SA(k_weak_cand_g, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), 0, s, ac, (const int *)ctx->wlist.p, nw,
-                           (const uint8_t *)ctx->gp_cb.p, (float *)ctx->wcand.p, wc);
+                if (a.dpairs && ctx->dtex_cand) {
+                    if (a.sa_any) hipLaunchKernelGGL((k_weak_cand_g<true, true, true>), dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), 0, s,
+                                                     ac, (const int *)ctx->wlist.p, nw, (const uint8_t *)ctx->gp_cb.p, (float *)ctx->wcand.p, wc);
+                    else hipLaunchKernelGGL((k_weak_cand_g<true, false, true>), dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), 0, s,
+                                            ac, (const int *)ctx->wlist.p, nw, (const uint8_t *)ctx->gp_cb.p, (float *)ctx->wcand.p, wc);
+                } else {
+                    LAUNCH_TEX_SA(k_weak_cand_g, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), 0, s, ac, (const int *)ctx->wlist.p, nw,
+                                  (const uint8_t *)ctx->gp_cb.p, (float *)ctx->wcand.p, wc);
+                }
                 prof_end(ctx, e1, APD_PROF_WEAK_CAND_G, nw);
                 e1 = prof_begin(ctx);
                 hipLaunchKernelGGL(k_weak_cand_comb, dim3(2 * blocks_for((size_t)nw, VM_P)), dim3(BLOCK), 0, s, ac,
@@ -4385,9 +4413,17 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             e0 = prof_begin(ctx);
             // k_sweep_weak_vm's small cost table when every pixel's candidates are in `cand`
             const bool direct = cand != nullptr;
-            LAUNCH_TEX_SA(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
-                          (ctx->args.tex_f16 ? wv_lds_bytes<true, 9>(a.N, direct) : wv_lds_bytes<false, 9>(a.N, direct)), s,
-                          aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
+            if (a.dpairs && ctx->dtex_sweep) {
+                const size_t lds = wv_lds_bytes<true, 9>(a.N, direct);
+                if (a.sa_any) hipLaunchKernelGGL((k_sweep_weak_vm<true, true, true>), dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), lds, s,
+                                                 aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
+                else hipLaunchKernelGGL((k_sweep_weak_vm<true, false, true>), dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), lds, s,
+                                        aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
+            } else {
+                LAUNCH_TEX_SA(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
+                              (ctx->args.tex_f16 ? wv_lds_bytes<true, 9>(a.N, direct) : wv_lds_bytes<false, 9>(a.N, direct)), s,
+                              aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
+            }
             prof_end(ctx, e0, APD_PROF_WEAK_SWEEP, n);
         }
         if ((st = check_launch(ctx, "weak sweep"))) return st;
@@ -4426,16 +4462,10 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
         const int dwc = dw_chunk(a.N, a.geom != 0, sa_lds_bytes(a));
         Args ad = a;
         ad.evals = (ctx->prof && ctx->evals.p) ? (APD_G unsigned long long *)ctx->evals.p : nullptr;
-        // fp16 problems: DepthToWeak's taps over pre-differenced texels (FastTexD; optional buffer,
-        // 8 B per padded texel position and view, built from the pairs here)
-        const size_t dpn = a.qstride * (size_t)a.N;
-        const bool dp = a.tex_f16 && ctx->dtex && try_ensure(ctx, ctx->dpairs, dpn * sizeof(uint2));
-        if (dp)
-            hipLaunchKernelGGL(k_build_dpairs, dim3((unsigned)std::min<size_t>(blocks_for(dpn, BLOCK), 65535u * 8u)), dim3(BLOCK), 0, s,
-                               (const uint32_t *)ctx->quad.p, (uint2 *)ctx->dpairs.p, a.W, a.H, a.N, a.qstride);
+        // fp16 problems: DepthToWeak's taps over the pre-differenced texels (FastTexD, apd_set_problem)
+        const bool dp = a.dpairs != nullptr;
         hipEvent_t e0 = prof_begin(ctx);
         if (dp) {
-            ad.dpairs = devptr<decltype(ad.dpairs)>(ctx->dpairs.p);
             const size_t lds = dw_lds_bytes(a.N, a.geom != 0, dwc) + sa_lds_bytes(a);
             if (a.sa_any) hipLaunchKernelGGL((k_depth_to_weak_vm<true, true, true>), dim3(nb), dim3(VM_BLOCK), lds, s, ad, dwc, tw);
             else hipLaunchKernelGGL((k_depth_to_weak_vm<true, false, true>), dim3(nb), dim3(VM_BLOCK), lds, s, ad, dwc, tw);
