@@ -1663,12 +1663,11 @@ __device__ __forceinline__ AncRecV<F16> load_anc_rec(const Args &a, int q, int f
 // SA = false: no SA masks in this problem, so every window's tap mask is full (compile-time constant:
 // no per-tap mask selects). BOX: L.box holds the pixel's anchor bounding box, and one
 // window_rcp_ok_box over it (taps included) stands for the per-window checks when it holds.
-template <bool F16, bool SA = true, bool BOX = false, int NWIN, bool DP = false>
+template <bool F16, bool SA = true, bool BOX = false, int NWIN>
 __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWIN> &L, int p, int px, int py, int s, float4 pl,
                                             bool want, bool *seldep = nullptr, uint32_t *nwc = nullptr,
                                             uint32_t *nwa = nullptr) {
-    // DP: the windows' taps over the pre-differenced fp16 texels (FastTexD, a.dpairs)
-    using TT = typename std::conditional<DP && F16, FastTexD<true>, FastTex<F16, true>>::type;
+    using TT = FastTex<F16, true>;  // (FastTexD measured 9 % slower in the Weak sweep: twice the texel footprint)
     const int W = a.W, H = a.H;
     const Hom Hm = homography(a, s, pl);
     float ptx, pty;
@@ -1795,7 +1794,7 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
 #ifndef WV_LDS_OCC
 #define WV_LDS_OCC 3  // workgroups per CU the registers are bounded for
 #endif
-template <bool F16, bool SA, bool DP = false>
+template <bool F16, bool SA>
 __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
                                                                 int iter, const float *__restrict__ cand, int wc) {
     const int N = a.N, W = a.W;
@@ -1889,7 +1888,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
         const bool want = pv1 && ((L.flags[p1] >> h) & 1u);
         const float4 pl = L.hyp[h * VM_P + p1];
-        const float nv = ncc_new_vm<F16, SA, true, 9, DP>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
+        const float nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
         if (want) val = nv;
         costL[t * VM_P + p1] = val;
     }
@@ -2001,7 +2000,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
             if (iter == 0 && a.wcur && !__ballot(want && __builtin_isnan(kept)))
                 nv = kept;
             else
-                nv = ncc_new_vm<F16, SA, true, 9, DP>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
+                nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
             if (want) {
                 val = nv;
                 if (geom) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
@@ -2093,7 +2092,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
             const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[p1];
             LANE_STAT(22, want);
             const float4 fit = fit1;
-            const float nv = ncc_new_vm<F16, SA, true, 9, DP>(a, L, p1, px1, py1, v + 1, fit, want, nullptr, &nwc, &nwa);
+            const float nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, fit, want, nullptr, &nwc, &nwa);
             if (want) {
                 cv = nv;
                 if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, fit), cv);
@@ -2191,7 +2190,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
                     const int px = pxy & 0xFFFF, py = pxy >> 16;
                     const float4 tp = WV_CAND(L)[k * VM_P + p];
                     LANE_STAT(20, want);
-                    const float nv = ncc_new_vm<F16, SA, true, 9, DP>(a, L, p, px, py, v + 1, tp, want, nullptr, &nwc, &nwa);
+                    const float nv = ncc_new_vm<F16, SA, true>(a, L, p, px, py, v + 1, tp, want, nullptr, &nwc, &nwa);
                     if (want) {
                         float cv = nv;
                         if (geom) cv = fmaf(gf, geom_cost(a, px, py, v + 1, tp), cv);
@@ -2233,7 +2232,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
             const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[(1 + k) * VM_P + p1];
             LANE_STAT(20, want);
             const float4 tp = WV_CAND(L)[k * VM_P + p1];
-            const float nv = ncc_new_vm<F16, SA, true, 9, DP>(a, L, p1, px1, py1, v + 1, tp, want, nullptr, &nwc, &nwa);
+            const float nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, tp, want, nullptr, &nwc, &nwa);
             if (want) {
                 cv = nv;
                 if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
@@ -2656,11 +2655,10 @@ __device__ __forceinline__ float gp_combine(float cc, const float (&sc)[8]) {
 // anchor 0 projected out of frame). With an SA label at the pixel the centre window is used only
 // when anchor 0 carries the label (else center_cost stays 0, APD.cu:493-497) and its taps are
 // filtered by it (APD.cu:526-530); an empty window leaves center_cost 0 (APD.cu:543).
-template <bool F16, bool SA, bool DP = false>
+template <bool F16, bool SA>
 __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__restrict__ list, int count,
                                                           const uint8_t *__restrict__ cbw, float *__restrict__ out, int wc) {
-    // DP: the centre windows' taps over the pre-differenced fp16 texels (FastTexD, a.dpairs)
-    using TT = typename std::conditional<DP && F16, FastTexD<true>, FastTex<F16, true>>::type;
+    using TT = FastTex<F16, true>;  // (FastTexD measured 1.4 % slower per iteration here, profiles/r5_ab_dtex_kernels.txt)
     // (fp16 reference taps when the images are: fp32 measured 6 % slower, profiles/r4_ab_cand_g_fp32_ref.txt)
     using RT = typename std::conditional<F16, _Float16, float>::type;
     __shared__ RT cref[36 * VM_P];
@@ -3593,9 +3591,7 @@ struct apd_ctx {
                                    // leaves them to the sweep
     bool gp_on = false;            // the pair table of the prepared problem is built (apd_stage_prepare)
     bool rec_on = false;           // the anchor-window records of the prepared problem are built (k_anchor_rec)
-    bool dtex = true;              // pre-differenced fp16 texels (FastTexD) for the VALU-bound kernels; APD_NO_DTEX=1 disables
-    bool dtex_cand = true;         // ... in k_weak_cand_g (APD_NO_DTEX_CAND=1: the plain pairs there only)
-    bool dtex_sweep = false;       // ... in k_sweep_weak_vm (APD_DTEX_SWEEP=1; A/B)
+    bool dtex = true;              // DepthToWeak over pre-differenced fp16 texels (FastTexD); APD_NO_DTEX=1 disables
     int gp_np = 0;                 // its distinct pairs
     bool lr_handover = true;       // LocalRefine reads DepthToWeak's samples; APD_NO_LR_HANDOVER=1 disables
     bool wcur_on = true;           // RandomInit keeps WEAK current-plane costs for iteration 0; APD_NO_WCUR=1 disables
@@ -3797,8 +3793,7 @@ apd_ctx *apd_create(int32_t device) {
     ctx->lr_handover = getenv("APD_NO_LR_HANDOVER") == nullptr;
     ctx->wcur_on = getenv("APD_NO_WCUR") == nullptr;
     ctx->dtex = getenv("APD_NO_DTEX") == nullptr;
-    ctx->dtex_cand = getenv("APD_NO_DTEX_CAND") == nullptr;
-    ctx->dtex_sweep = getenv("APD_DTEX_SWEEP") != nullptr;
+
     // tile_pix needs the tile width to divide the 64-pixel tile (otherwise two workgroups share pixels)
     if (const char *e = getenv("APD_DW_TILE_W")) {
         const int t = atoi(e);
@@ -3814,7 +3809,6 @@ apd_ctx *apd_create(int32_t device) {
         (const void *)k_sweep_strong_vm<true, true>, (const void *)k_sweep_strong_vm<false, true>,
         (const void *)k_sweep_weak_vm<true, false>, (const void *)k_sweep_weak_vm<false, false>,
         (const void *)k_sweep_weak_vm<true, true>, (const void *)k_sweep_weak_vm<false, true>,
-        (const void *)k_sweep_weak_vm<true, false, true>, (const void *)k_sweep_weak_vm<true, true, true>,
         (const void *)k_depth_to_weak_vm<true, false>, (const void *)k_depth_to_weak_vm<false, false>,
         (const void *)k_depth_to_weak_vm<true, true>, (const void *)k_depth_to_weak_vm<false, true>,
         (const void *)k_depth_to_weak_vm<true, false, true>, (const void *)k_depth_to_weak_vm<true, true, true>,
@@ -4046,8 +4040,8 @@ int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
                                (float4 *)ctx->quad.p, W, H, N, qstride);
         if ((st = check_launch(ctx, "k_build_quads"))) return st;
     }
-    // fp16 problems: the pre-differenced texel records (FastTexD) of DepthToWeak and the anchor
-    // candidates' centre windows, 8 B per padded texel position and view (2 GB at C3); optional
+    // fp16 problems: the pre-differenced texel records (FastTexD) DepthToWeak samples, 8 B per padded
+    // texel position and view (2 GB at C3); optional
     a.dpairs = nullptr;
     if (tex_f16 && ctx->dtex && try_ensure(ctx, ctx->dpairs, qstride * (size_t)N * sizeof(uint2))) {
         const size_t dpn = qstride * (size_t)N;
@@ -4385,15 +4379,8 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
                                (const int2 *)ctx->gp_plist.p, ctx->gp_np, (float *)ctx->gp_pcost.p);
                 prof_end(ctx, e1, APD_PROF_GP_COST, ctx->gp_np);
                 e1 = prof_begin(ctx);
-                if (a.dpairs && ctx->dtex_cand) {
-                    if (a.sa_any) hipLaunchKernelGGL((k_weak_cand_g<true, true, true>), dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), 0, s,
-                                                     ac, (const int *)ctx->wlist.p, nw, (const uint8_t *)ctx->gp_cb.p, (float *)ctx->wcand.p, wc);
-                    else hipLaunchKernelGGL((k_weak_cand_g<true, false, true>), dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), 0, s,
-                                            ac, (const int *)ctx->wlist.p, nw, (const uint8_t *)ctx->gp_cb.p, (float *)ctx->wcand.p, wc);
-                } else {
-                    LAUNCH_TEX_SA(k_weak_cand_g, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), 0, s, ac, (const int *)ctx->wlist.p, nw,
-                                  (const uint8_t *)ctx->gp_cb.p, (float *)ctx->wcand.p, wc);
-                }
+                LAUNCH_TEX_SA(k_weak_cand_g, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), 0, s, ac, (const int *)ctx->wlist.p, nw,
+                              (const uint8_t *)ctx->gp_cb.p, (float *)ctx->wcand.p, wc);
                 prof_end(ctx, e1, APD_PROF_WEAK_CAND_G, nw);
                 e1 = prof_begin(ctx);
                 hipLaunchKernelGGL(k_weak_cand_comb, dim3(2 * blocks_for((size_t)nw, VM_P)), dim3(BLOCK), 0, s, ac,
@@ -4413,17 +4400,9 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             e0 = prof_begin(ctx);
             // k_sweep_weak_vm's small cost table when every pixel's candidates are in `cand`
             const bool direct = cand != nullptr;
-            if (a.dpairs && ctx->dtex_sweep) {
-                const size_t lds = wv_lds_bytes<true, 9>(a.N, direct);
-                if (a.sa_any) hipLaunchKernelGGL((k_sweep_weak_vm<true, true, true>), dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), lds, s,
-                                                 aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
-                else hipLaunchKernelGGL((k_sweep_weak_vm<true, false, true>), dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK), lds, s,
-                                        aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
-            } else {
-                LAUNCH_TEX_SA(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
-                              (ctx->args.tex_f16 ? wv_lds_bytes<true, 9>(a.N, direct) : wv_lds_bytes<false, 9>(a.N, direct)), s,
-                              aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
-            }
+            LAUNCH_TEX_SA(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
+                          (ctx->args.tex_f16 ? wv_lds_bytes<true, 9>(a.N, direct) : wv_lds_bytes<false, 9>(a.N, direct)), s,
+                          aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
             prof_end(ctx, e0, APD_PROF_WEAK_SWEEP, n);
         }
         if ((st = check_launch(ctx, "weak sweep"))) return st;
