@@ -24,7 +24,7 @@ WEAK, STRONG, UNKNOWN = 0, 1, 2
 
 # apd_profile_kernel kinds and apd_profile_counters slots (include/apd_hip.h)
 PROF_STRONG_SWEEP, PROF_RANSAC_FIT, PROF_WEAK_CAND, PROF_WEAK_SWEEP = 0, 1, 2, 3
-PROF_DEPTH_TO_WEAK, PROF_GP_COST, PROF_WEAK_CAND_G, PROF_WEAK_CAND_COMB = 4, 5, 6, 7
+PROF_DEPTH_TO_WEAK, PROF_GP_COST, PROF_WEAK_CAND_G, PROF_WEAK_CAND_COMB, PROF_WEAK_PATH = 4, 5, 6, 7, 8
 # apd_hip.h's counters: [0] NCC-Old (Strong sweep), [1] NCC-New (Weak sweep, algorithmic), [2] geometric
 # terms (Weak sweep), [3] NCC-Old (DepthToWeak), [4] geometric terms (DepthToWeak), [5] pair windows
 # (k_gp_cost), [6] centre windows (k_weak_cand_g), [7] centre / [8] anchor windows (k_sweep_weak_vm)

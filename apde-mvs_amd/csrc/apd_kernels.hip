@@ -3574,6 +3574,12 @@ void set_global_err(const std::string &s) {
 struct apd_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // side streams of the loop body: RANSACToGetFitPlane and k_gp_cost run beside the anchor
+    // candidates' centre windows (none of them reads what another writes); the ctx stream joins them
+    // before the kernels that read their outputs. ev_fork / ev_side: ordering only (no timing).
+    hipStream_t side[2] = {nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_side[2] = {nullptr, nullptr};
+    bool overlap = true;           // APD_NO_OVERLAP=1: the loop body on the ctx stream alone
     std::string err;
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
@@ -3789,6 +3795,18 @@ apd_ctx *apd_create(int32_t device) {
         return nullptr;
     }
     for (auto &e : ctx->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);  // timing only
+    for (auto &ss : ctx->side) {
+        if (hipStreamCreateWithFlags(&ss, hipStreamNonBlocking) != hipSuccess) {
+            set_global_err("hipStreamCreate failed");
+            for (auto &t : ctx->side) if (t) (void)hipStreamDestroy(t);
+            (void)hipStreamDestroy(ctx->stream);
+            delete ctx;
+            return nullptr;
+        }
+    }
+    (void)hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
+    for (auto &e : ctx->ev_side) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    ctx->overlap = getenv("APD_NO_OVERLAP") == nullptr;
     ctx->cand_pairs = getenv("APD_NO_CAND_PAIRS") == nullptr;
     ctx->lr_handover = getenv("APD_NO_LR_HANDOVER") == nullptr;
     ctx->wcur_on = getenv("APD_NO_WCUR") == nullptr;
@@ -3837,6 +3855,9 @@ void apd_destroy(apd_ctx *ctx) {
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
     for (auto &pe : ctx->prof_ev) { (void)hipEventDestroy(pe.e0); (void)hipEventDestroy(pe.e1); }
     for (hipEvent_t e : ctx->prof_pool) (void)hipEventDestroy(e);
+    for (auto &ss : ctx->side) if (ss) { (void)hipStreamSynchronize(ss); (void)hipStreamDestroy(ss); }
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    for (auto &e : ctx->ev_side) if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -4324,18 +4345,18 @@ static hipEvent_t prof_event(apd_ctx *ctx) {
     }
     return e;
 }
-static hipEvent_t prof_begin(apd_ctx *ctx) {
+static hipEvent_t prof_begin(apd_ctx *ctx, hipStream_t st = nullptr) {
     hipEvent_t e0 = nullptr;
     if (ctx->prof) {
         e0 = prof_event(ctx);
-        (void)hipEventRecord(e0, ctx->stream);
+        (void)hipEventRecord(e0, st ? st : ctx->stream);
     }
     return e0;
 }
-static void prof_end(apd_ctx *ctx, hipEvent_t e0, int kind, int64_t px) {
+static void prof_end(apd_ctx *ctx, hipEvent_t e0, int kind, int64_t px, hipStream_t st = nullptr) {
     if (!ctx->prof) return;
     hipEvent_t e1 = prof_event(ctx);
-    (void)hipEventRecord(e1, ctx->stream);
+    (void)hipEventRecord(e1, st ? st : ctx->stream);
     ctx->prof_ev.push_back({e0, e1, kind, px});
 }
 
@@ -4359,9 +4380,21 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
         if ((st = check_launch(ctx, "k_sweep_strong"))) return st;
     }
     if (a.use_apd) {
-        hipEvent_t e0 = prof_begin(ctx);
-        hipLaunchKernelGGL(k_ransac_fit, dim3(blocks_for((size_t)a.HW, BLOCK)), dim3(BLOCK), 0, s, a, iter);
-        prof_end(ctx, e0, APD_PROF_RANSAC_FIT, a.HW);
+        // the Weak path's wall time (RANSAC beside the candidate kernels, then the Weak sweeps)
+        hipEvent_t ewp = prof_begin(ctx);
+        // fork: RANSAC (side stream 0) and k_gp_cost (side stream 1) beside k_weak_cand_g (ctx stream)
+        hipStream_t sr = s, sg = s;
+        if (ctx->overlap) {
+            HIP_OK(ctx, hipEventRecord(ctx->ev_fork, s));
+            HIP_OK(ctx, hipStreamWaitEvent(ctx->side[0], ctx->ev_fork, 0));
+            HIP_OK(ctx, hipStreamWaitEvent(ctx->side[1], ctx->ev_fork, 0));
+            sr = ctx->side[0];
+            sg = ctx->side[1];
+        }
+        hipEvent_t e0 = prof_begin(ctx, sr);
+        hipLaunchKernelGGL(k_ransac_fit, dim3(blocks_for((size_t)a.HW, BLOCK)), dim3(BLOCK), 0, sr, a, iter);
+        prof_end(ctx, e0, APD_PROF_RANSAC_FIT, a.HW, sr);
+        if (ctx->overlap) HIP_OK(ctx, hipEventRecord(ctx->ev_side[0], sr));
         const int nw = ctx->cnt[2] + ctx->cnt[3];
         const int wc = std::max(ctx->weak_count, 1);
         const float *cand = nullptr;
@@ -4373,15 +4406,17 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             Args ac = a;
             ac.evals = evals;
             {
-                hipEvent_t e1 = prof_begin(ctx);
+                hipEvent_t e1 = prof_begin(ctx, sg);
                 if (ctx->gp_np > 0)
-                    LAUNCH_TEX_SA(k_gp_cost, dim3(blocks_for((size_t)ctx->gp_np, BLOCK)), dim3(BLOCK), gp_cost_lds_bytes(a.N), s, ac,
+                    LAUNCH_TEX_SA(k_gp_cost, dim3(blocks_for((size_t)ctx->gp_np, BLOCK)), dim3(BLOCK), gp_cost_lds_bytes(a.N), sg, ac,
                                (const int2 *)ctx->gp_plist.p, ctx->gp_np, (float *)ctx->gp_pcost.p);
-                prof_end(ctx, e1, APD_PROF_GP_COST, ctx->gp_np);
+                prof_end(ctx, e1, APD_PROF_GP_COST, ctx->gp_np, sg);
+                if (ctx->overlap) HIP_OK(ctx, hipEventRecord(ctx->ev_side[1], sg));
                 e1 = prof_begin(ctx);
                 LAUNCH_TEX_SA(k_weak_cand_g, dim3(blocks_for((size_t)nw, VM_P)), dim3(PK_BLOCK), 0, s, ac, (const int *)ctx->wlist.p, nw,
                               (const uint8_t *)ctx->gp_cb.p, (float *)ctx->wcand.p, wc);
                 prof_end(ctx, e1, APD_PROF_WEAK_CAND_G, nw);
+                if (ctx->overlap) HIP_OK(ctx, hipStreamWaitEvent(s, ctx->ev_side[1], 0));  // join k_gp_cost
                 e1 = prof_begin(ctx);
                 hipLaunchKernelGGL(k_weak_cand_comb, dim3(2 * blocks_for((size_t)nw, VM_P)), dim3(BLOCK), 0, s, ac,
                                    (const int *)ctx->wlist.p, nw, (const uint8_t *)ctx->gp_cb.p, (const uint8_t *)ctx->gp_cb.p + wc,
@@ -4390,6 +4425,7 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             }
             cand = (const float *)ctx->wcand.p;
         }
+        if (ctx->overlap) HIP_OK(ctx, hipStreamWaitEvent(s, ctx->ev_side[0], 0));  // join RANSAC (the sweep reads a.fit)
         for (int colour = 0; colour < 2; ++colour) {
             const int n = ctx->cnt[2 + colour];
             if (n <= 0) continue;
@@ -4405,6 +4441,7 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
                           aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
             prof_end(ctx, e0, APD_PROF_WEAK_SWEEP, n);
         }
+        prof_end(ctx, ewp, APD_PROF_WEAK_PATH, ctx->cnt[2] + ctx->cnt[3]);
         if ((st = check_launch(ctx, "weak sweep"))) return st;
     }
     ctx->wcur_fresh = false;

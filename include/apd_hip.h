@@ -212,6 +212,9 @@ int32_t apd_get_timing(apd_ctx *ctx, apd_timing *timing);
 #define APD_PROF_GP_COST 5      /* k_gp_cost alone (pair windows, inside APD_PROF_WEAK_CAND)         */
 #define APD_PROF_WEAK_CAND_G 6  /* k_weak_cand_g alone (centre windows, inside APD_PROF_WEAK_CAND)    */
 #define APD_PROF_WEAK_CAND_COMB 7 /* k_weak_cand_comb alone (focal combination, inside WEAK_CAND)   */
+#define APD_PROF_WEAK_PATH 8    /* wall time from the end of the Strong sweeps to the end of the Weak
+                                   sweeps: RANSAC and k_gp_cost run on side streams beside the
+                                   candidate kernels, so the kernels' own brackets overlap           */
 int32_t apd_profile_reset(apd_ctx *ctx, int32_t enable);
 int32_t apd_profile_kernel(apd_ctx *ctx, int32_t kind, double *ms_total, int64_t *launches,
                            int64_t *pixels);
