@@ -4251,6 +4251,38 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         if ((st = check_launch(ctx, "anchors"))) return st;
     }
     (void)hipEventRecord(ctx->ev[1], s);
+    // RandomInitialization needs the anchors and the input state only: with overlap it runs on side
+    // stream 0 beside the lists and the pair table (which read neither what it writes -- planes,
+    // costs, the next selections, view weights, kept costs -- nor write what it reads)
+    hipStream_t sri = s;
+    if (ctx->overlap) {
+        HIP_OK(ctx, hipEventRecord(ctx->ev_fork, s));
+        HIP_OK(ctx, hipStreamWaitEvent(ctx->side[0], ctx->ev_fork, 0));
+        sri = ctx->side[0];
+    }
+    {
+        const int tw = ctx->dw_tile_w, th = VM_P / tw;
+        const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
+        if (a.use_apd) {
+            if (a.sa_any) {
+                if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, true, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, true>(a.N) + sa_lds_bytes(a)), sri, a, tw);
+                else hipLaunchKernelGGL((k_random_init_vm<false, true, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, true>(a.N) + sa_lds_bytes(a)), sri, a, tw);
+            } else {
+                if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, true, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, true>(a.N)), sri, a, tw);
+                else hipLaunchKernelGGL((k_random_init_vm<false, true, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, true>(a.N)), sri, a, tw);
+            }
+        } else {
+            if (a.sa_any) {
+                if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, false, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, false>(a.N) + sa_lds_bytes(a)), sri, a, tw);
+                else hipLaunchKernelGGL((k_random_init_vm<false, false, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, false>(a.N) + sa_lds_bytes(a)), sri, a, tw);
+            } else {
+                if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, false, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, false>(a.N)), sri, a, tw);
+                else hipLaunchKernelGGL((k_random_init_vm<false, false, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, false>(a.N)), sri, a, tw);
+            }
+        }
+        if ((st = check_launch(ctx, "k_random_init"))) return st;
+        if (ctx->overlap) HIP_OK(ctx, hipEventRecord(ctx->ev_side[0], sri));
+    }
     // pixel lists for the sweeps (after NeigbourUpdate)
     {
         int *tot = (int *)ctx->totals.p;
@@ -4302,29 +4334,8 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         }
     }
     (void)hipEventRecord(ctx->ev[2], s);
-    {
-        const int tw = ctx->dw_tile_w, th = VM_P / tw;
-        const unsigned nb = (unsigned)(((a.W + tw - 1) / tw) * ((a.H + th - 1) / th));
-        if (a.use_apd) {
-            if (a.sa_any) {
-                if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, true, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, true>(a.N) + sa_lds_bytes(a)), s, a, tw);
-                else hipLaunchKernelGGL((k_random_init_vm<false, true, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, true>(a.N) + sa_lds_bytes(a)), s, a, tw);
-            } else {
-                if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, true, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, true>(a.N)), s, a, tw);
-                else hipLaunchKernelGGL((k_random_init_vm<false, true, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, true>(a.N)), s, a, tw);
-            }
-        } else {
-            if (a.sa_any) {
-                if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, false, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, false>(a.N) + sa_lds_bytes(a)), s, a, tw);
-                else hipLaunchKernelGGL((k_random_init_vm<false, false, true>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, false>(a.N) + sa_lds_bytes(a)), s, a, tw);
-            } else {
-                if (a.tex_f16) hipLaunchKernelGGL((k_random_init_vm<true, false, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<true, false>(a.N)), s, a, tw);
-                else hipLaunchKernelGGL((k_random_init_vm<false, false, false>), dim3(nb), dim3(VM_BLOCK), (ri_lds_bytes<false, false>(a.N)), s, a, tw);
-            }
-        }
-    }
+    if (ctx->overlap) HIP_OK(ctx, hipStreamWaitEvent(s, ctx->ev_side[0], 0));  // join RandomInitialization
     HIP_OK(ctx, hipMemcpyAsync(ctx->sel.p, ctx->sel2.p, (size_t)a.HW * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-    if ((st = check_launch(ctx, "k_random_init"))) return st;
     (void)hipEventRecord(ctx->ev[3], s);
     ctx->wcur_fresh = a.wcur != nullptr;
     ctx->prepared = true;
