@@ -4281,6 +4281,7 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
             }
         }
         if ((st = check_launch(ctx, "k_random_init"))) return st;
+        (void)hipEventRecord(ctx->ev[15], sri);  // (apd_timing.init_ms = ev[1] -> ev[15])
         if (ctx->overlap) HIP_OK(ctx, hipEventRecord(ctx->ev_side[0], sri));
     }
     // pixel lists for the sweeps (after NeigbourUpdate)
@@ -4530,9 +4531,12 @@ int32_t apd_run_patchmatch(apd_ctx *ctx) {
     memset(&t, 0, sizeof(t));
     (void)hipEventElapsedTime(&t.total_ms, ctx->ev[0], ctx->ev[13]);
     (void)hipEventElapsedTime(&t.anchors_ms, ctx->ev[0], ctx->ev[1]);
+    // RandomInitialization runs first after the anchors, beside the lists and the pair table when
+    // the ctx overlaps (side stream 0): init_ms is its own duration, lists_ms + pairs_ms the ctx
+    // stream's, and their sum can exceed the bracket; ev[2] -> ev[3] (the join) is not reported
     (void)hipEventElapsedTime(&t.lists_ms, ctx->ev[1], ctx->ev[14]);
     (void)hipEventElapsedTime(&t.pairs_ms, ctx->ev[14], ctx->ev[2]);
-    (void)hipEventElapsedTime(&t.init_ms, ctx->ev[2], ctx->ev[3]);
+    (void)hipEventElapsedTime(&t.init_ms, ctx->ev[1], ctx->ev[15]);
     (void)hipEventElapsedTime(&t.sweep_ms, ctx->ev[3], ctx->ev[12]);
     (void)hipEventElapsedTime(&t.post_ms, ctx->ev[12], ctx->ev[13]);
     const int ni = std::min(iters, 8);

@@ -144,7 +144,8 @@ typedef struct apd_outputs {
 /* Device-time breakdown of the last apd_run_patchmatch (HIP events on the ctx stream), ms. */
 typedef struct apd_timing {
     float total_ms;            /* whole RunPatchMatch bracket (main.cpp:157-159 equivalent) */
-    float init_ms;             /* RandomInitialization                                     */
+    float init_ms;             /* RandomInitialization (beside the lists and the pair table
+                                  on a side stream, so the phases may sum to more than total) */
     float anchors_ms;          /* FindNearestStrongPoint + GenAnchors + NeigbourUpdate      */
     float sweep_ms;            /* all sweep iterations (Strong + RANSAC fit + Weak)         */
     float post_ms;             /* GetDepthandNormal + filter + DepthToWeak + Confidence + LocalRefine */
