@@ -986,6 +986,29 @@ __device__ __forceinline__ float geom_cost_p(const Args &a, int px, int py, int 
     float e = sqrtf(dx * dx + dy * dy);
     return fminf(3.0f, e);
 }
+// geom_cost_p in two halves around its one gather (the source depth), so that a caller scoring
+// several planes can issue all the gathers before consuming any: the same statements.
+struct GeomHead { size_t idx; float sx, sy; };
+__device__ __forceinline__ GeomHead geom_head(const Args &a, int s, const float P[3]) {
+    const APD_C Cam &sc = a.cams[s];
+    GeomHead h;
+    float sd;
+    project_cam(P, sc, h.sx, h.sy, sd);
+    h.idx = (size_t)s * a.HW + trunc_clamp(h.sy, a.H) * a.W + trunc_clamp(h.sx, a.W);
+    return h;
+}
+__device__ __forceinline__ float geom_tail(const Args &a, int px, int py, int s, const GeomHead &h, float src_depth) {
+    if (src_depth == 0.0f) return 3.0f;
+    const APD_C Cam &rc = a.cams[0];
+    const APD_C Cam &sc = a.cams[s];
+    float Q[3];
+    world_point(sc, h.sx, h.sy, src_depth, Q);
+    float bx, by, rd;
+    project_cam(Q, rc, bx, by, rd);
+    float dx = (float)px - bx, dy = (float)py - by;
+    float e = sqrtf(dx * dx + dy * dy);
+    return fminf(3.0f, e);
+}
 __device__ __forceinline__ float geom_cost(const Args &a, int px, int py, int s, float4 pl) {
     float P[3];
     geom_point(a, px, py, pl, P);

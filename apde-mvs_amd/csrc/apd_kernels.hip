@@ -1787,6 +1787,9 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
 #ifndef WV_P5_PACKED
 #define WV_P5_PACKED 1  // P5's (candidate, pixel) items packed per view into dense lanes
 #endif
+#ifndef WV_P2_GEOM_BATCH
+#define WV_P2_GEOM_BATCH 1  // P2a's 8 geometric terms with their gathers batched (0: one at a time)
+#endif
 #ifndef WV_P5_CHUNKS
 #define WV_P5_CHUNKS 3  // P5 batches: whole views until at least this many 64-item chunks
 #endif
@@ -1936,6 +1939,28 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
 #ifdef APD_PHASE_STAMPS
         const long long tg0_ = clock64();
 #endif
+#if WV_P2_GEOM_BATCH
+        // the 8 geometric terms with their source-depth gathers all in flight before the first is
+        // consumed (geom_head / geom_tail: the same statements as geom_cost)
+        if (geom && w > 0) {
+            GeomHead gh[8];
+            float sdep[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float P[3];
+                geom_point(a, px, py, L.hyp[j * VM_P + p], P);
+                gh[j] = geom_head(a, v + 1, P);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sdep[j] = ((hflag >> j) & 1u) ? a.depth[gh[j].idx] : 0.0f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                gval[j] = ((hflag >> j) & 1u) ? fmaf(gf, geom_tail(a, px, py, v + 1, gh[j], sdep[j]), ca[j]) : fmaf(gf, 3.0f, ca[j]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gval[j] = ca[j];
+        }
+#else
 #pragma unroll 1
         for (int j = 0; j < 8; ++j) {
             float cj = ca[0];
@@ -1947,6 +1972,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
 #pragma unroll
             for (int k = 0; k < 8; ++k) if (j == k) gval[k] = vv;
         }
+#endif
 #ifdef APD_PHASE_STAMPS
         if (a.evals && threadIdx.x == 0) atomicAdd(PROF_AT(a.evals, APD_INSTR + 8 + 7), (unsigned long long)(clock64() - tg0_));
 #endif
