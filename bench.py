@@ -599,6 +599,8 @@ def main():
                        "width": W, "height": H, "n_src": N, "texture": args.texture,
                        "weak_frac": round(weak_frac, 4), "global_batch": n_gpus,
                        "parallelism": f"views{n_gpus}"},
+            # the per-pass pair table spread over the pass's 3 iterations; pairs_ms is its bracket on the
+            # ctx stream with RandomInitialization running beside it, an upper bound of its cost
             "mpix_s_iter_amortised": (round(W * H / (elapsed / args.steps + e2e["pairs_ms"] * 1e-3 / 3) / 1e6 * n_gpus, 3)
                                       if e2e else None),
             "multi_gpu": exch,
