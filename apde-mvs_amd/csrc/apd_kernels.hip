@@ -1322,12 +1322,15 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 // image-wide records at four workgroups per CU measured equal over the whole C3 N = 10 scan --
 // profiles/r5_scan_c3_n10_rec_vs_lds.txt -- and +11 % at N = 25, since its record loads scale with the
 // evaluations per pixel while this layout builds each window once per pixel; it was retired in round 5.)
-template <bool F16, int NWIN = 9>
+// SA = false (no SA masks in the problem): every tap of a window is valid, so the tap masks and
+// 1 / wsum are compile-time constants and their arrays shrink to one element.
+template <bool F16, int NWIN = 9, bool SA = true>
 struct WvRefT {
-    uint64_t tmask0[VM_P];       // SA tap masks (all ones without SA)
+    static constexpr int MP = SA ? VM_P : 1;  // per-pixel extent of the SA-only arrays
+    uint64_t tmask0[MP];         // SA tap masks
     // per window, the reference side of ncc_finalize over its valid taps, once per pixel instead of
-    // once per evaluation: 1 / wsum (0: empty window), sr / wsum, var_ref -- the same statements
-    float winv[NWIN * VM_P], wsrp[NWIN * VM_P], wvar[NWIN * VM_P];
+    // once per evaluation: 1 / wsum (0: empty window; SA only), sr / wsum, var_ref -- the same statements
+    float winv[NWIN * MP], wsrp[NWIN * VM_P], wvar[NWIN * VM_P];
     int anc[9 * VM_P];           // packed (x, y) of anchors 0..8, -1 = none
     uint32_t flags[VM_P];        // bits 0-8: hypothesis h present (anchor STRONG); 16-24: window k evaluated
                                  // (anchor present and SA label matches); 25-27: the best anchor
@@ -1336,12 +1339,12 @@ struct WvRefT {
     // [tap][p]: window 0 taps 0..35 (6x6, step 2), anchor k taps 36+9(k-1).. (3x3, step 5); fp16 when
     // the images are (exactly) fp16-representable, see apd_set_problem
     typename std::conditional<F16, _Float16, float>::type rref[(36 + 9 * (NWIN - 1)) * VM_P];
-    uint16_t tmask[(NWIN - 1) * VM_P];
+    uint16_t tmask[(NWIN - 1) * MP];
     uint32_t box[2 * VM_P];      // bounding box of the anchors 0..8 (x0 | y0 << 16, x1 | y1 << 16)
 };
 // the Weak sweep's per-workgroup state: the reference side plus the hypotheses and per-pixel state
-template <bool F16, int NWIN = 9>
-struct WvLdsT : WvRefT<F16, NWIN> {
+template <bool F16, int NWIN = 9, bool SA = true>
+struct WvLdsT : WvRefT<F16, NWIN, SA> {
     float4 hyp[9 * VM_P];        // [h][p]: anchor planes 1..8 (if STRONG) + current; P4 overwrites [0..4]
                                  // with the refinement candidates (WV_CAND) after P2's last read
     float4 pnow[VM_P];
@@ -1349,28 +1352,43 @@ struct WvLdsT : WvRefT<F16, NWIN> {
     uint32_t tsel[VM_P];         // views with weight > 0 (the selection the best anchor hypothesis brings)
     uint16_t rng_n[VM_P];
     int pxy[VM_P];               // packed (x, y) of pixel slot p (P5's packed items)
-    uint32_t asel[8 * VM_P];     // [k-1][p]: selected views of anchor k (P2a's priors; no launch writes them)
 };
 #define WV_CAND(L) ((L).hyp)
-// With the direct 5-slot cost table at N = 10 (fp16 reference taps): 49.5 KiB (three workgroups per
-// CU). (The sweep's own candidate path, a 9-slot table, runs one fewer per CU.)
-static_assert(sizeof(WvLdsT<true, 9>) + 5 * 10 * VM_P * sizeof(float) + 10 * VM_P <= 160 * 1024 / 3,
-              "k_sweep_weak_vm (direct) at N = 10 must fit three workgroups per CU (160 KiB LDS)");
-// `direct` (the pair-table kernels handled every pixel): the sweep reads the anchor candidates'
-// costs from their buffer in P2 and its table holds [5][N][64] (current plane, fit plane,
-// refinement candidates) instead of [9][N][64]: 48 KiB at N = 10, three workgroups per CU instead of two.
+#ifndef WV_P5_CHUNKS
+#define WV_P5_CHUNKS 3  // P5 batches: whole views until at least this many 64-item chunks
+#endif
+// The dynamic part after WvLdsT: the cost table (rows of 64 floats), then [N][64] view weights and
+// [N][64] anchor-selection bytes (bit k-1: anchor k selected view v, P2a's priors). Rows: `direct`
+// (the pair-table kernels handled every pixel, P2 reads the anchor candidates' costs from their
+// buffer) N for the current / fit plane and 5 x min(WV_P5_CHUNKS, N) for one P5 batch (its views
+// with items, at most one per chunk); otherwise [9][N] (P1's anchor candidates and the current plane).
+__host__ __device__ __forceinline__ int wv_cost_rows(int N, bool direct) {
+    const int p5 = 5 * (N < WV_P5_CHUNKS ? N : WV_P5_CHUNKS);
+    const int base = direct ? N : 9 * N;
+    return base > p5 ? base : p5;
+}
 #ifndef APD_WV_LDS_PAD
 #define APD_WV_LDS_PAD 0  // experiments: extra LDS bytes per workgroup (fewer workgroups per CU)
 #endif
-template <bool F16, int NWIN>
+template <bool F16, int NWIN, bool SA>
 static inline size_t wv_lds_bytes(int N, bool direct = false) {
-    return APD_WV_LDS_PAD + sizeof(WvLdsT<F16, NWIN>) + (size_t)(direct ? 5 : 9) * N * VM_P * sizeof(float) + (size_t)N * VM_P;
+    return APD_WV_LDS_PAD + sizeof(WvLdsT<F16, NWIN, SA>) + (size_t)wv_cost_rows(N, direct) * VM_P * sizeof(float) +
+           (size_t)2 * N * VM_P;
 }
+// Occupancy: the headline's instantiation (fp16 taps, no SA masks, direct) at N = 10 fits four
+// workgroups per CU (160 KiB of LDS); with SA masks three.
+static_assert(sizeof(WvLdsT<true, 9, false>) + 15 * VM_P * sizeof(float) + 2 * 10 * VM_P <= 160 * 1024 / 4,
+              "k_sweep_weak_vm<fp16, no SA> (direct) at N = 10 must fit four workgroups per CU");
+static_assert(sizeof(WvLdsT<true, 9, true>) + 15 * VM_P * sizeof(float) + 2 * 10 * VM_P <= 160 * 1024 / 3,
+              "k_sweep_weak_vm<fp16, SA> (direct) at N = 10 must fit three workgroups per CU");
 __device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
     const long idx = (long)y * a.W + x;
     if (idx < 0 || idx >= a.HW) return -1;
     return a.sa[idx];
 }
+#ifndef WV_CENTRE_PIPE
+#define WV_CENTRE_PIPE true  // NCC-New's centre window software-pipelined by columns (ncc_new_window PIPE)
+#endif
 // One NCC-New window of pixel slot p against source view s: taps (ax - 5 + inc*i, ay - 5 + inc*j),
 // i outer, j inner, skipping taps outside the SA mask; the reference's moments come from WvLds.
 // `fast` = window_rcp_ok for this lane (Newton reciprocal + packed taps); otherwise the IEEE
@@ -1501,8 +1519,8 @@ __device__ __forceinline__ void ncc_new_window(const Args &a, RT rb,
 // masks and moments; wave w builds windows w, w + nwaves, ... (tap order = the reference's). Each
 // window's taps (and SA labels) are all loaded before the in-order moment sums, so a window costs one
 // memory round trip instead of one per tap.
-template <bool F16, int N1, int INC, int NWIN>
-__device__ __forceinline__ void wv_build_window(const Args &a, WvRefT<F16, NWIN> &L, int p1, int k, int ax, int ay,
+template <bool F16, int N1, int INC, int NWIN, bool SA>
+__device__ __forceinline__ void wv_build_window(const Args &a, WvRefT<F16, NWIN, SA> &L, int p1, int k, int ax, int ay,
                                                 bool use_sa, int cid) {
     constexpr int NT = N1 * N1;
     const int tap0 = (k == 0) ? 0 : 36 + 9 * (k - 1);
@@ -1516,7 +1534,7 @@ __device__ __forceinline__ void wv_build_window(const Args &a, WvRefT<F16, NWIN>
         r[tk] = tex_ref(a, rx, ry);
         in[tk] = true;
     }
-    if (a.sa_any) {
+    if (SA && a.sa_any) {
 #pragma unroll
         for (int tk = 0; tk < NT; ++tk) {
             const int i = tk / N1, j = tk - N1 * (tk / N1);
@@ -1542,14 +1560,16 @@ __device__ __forceinline__ void wv_build_window(const Args &a, WvRefT<F16, NWIN>
     }
     // (ncc_finalize's reference-side statements: inv = 1 / wsum, sr *= inv, srr *= inv, var_ref)
     const float inv = 1.0f / ws, srp = sr * inv, srrp = srr * inv;
-    L.winv[k * VM_P + p1] = ws != 0.0f ? inv : 0.0f;
     L.wsrp[k * VM_P + p1] = srp;
     L.wvar[k * VM_P + p1] = fmaf(-srp, srp, srrp);
-    if (k == 0) L.tmask0[p1] = mask;
-    else L.tmask[(k - 1) * VM_P + p1] = (uint16_t)mask;
+    if constexpr (SA) {
+        L.winv[k * VM_P + p1] = ws != 0.0f ? inv : 0.0f;
+        if (k == 0) L.tmask0[p1] = mask;
+        else L.tmask[(k - 1) * VM_P + p1] = (uint16_t)mask;
+    }
 }
-template <bool F16, int NWIN>
-__device__ __forceinline__ void wv_build_windows(const Args &a, WvRefT<F16, NWIN> &L, int p, const APD_G short2 *anc, int cid,
+template <bool F16, int NWIN, bool SA>
+__device__ __forceinline__ void wv_build_windows(const Args &a, WvRefT<F16, NWIN, SA> &L, int p, const APD_G short2 *anc, int cid,
                                                  int wave, int nwaves) {
     const bool use_sa = cid != 0;
     for (int k = wave; k < NWIN; k += nwaves) {
@@ -1663,8 +1683,9 @@ __device__ __forceinline__ AncRecV<F16> load_anc_rec(const Args &a, int q, int f
 // SA = false: no SA masks in this problem, so every window's tap mask is full (compile-time constant:
 // no per-tap mask selects). BOX: L.box holds the pixel's anchor bounding box, and one
 // window_rcp_ok_box over it (taps included) stands for the per-window checks when it holds.
-template <bool F16, bool SA = true, bool BOX = false, int NWIN>
-__device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWIN> &L, int p, int px, int py, int s, float4 pl,
+// PIPE: the centre window's columns software-pipelined (ncc_new_window).
+template <bool F16, bool SA = true, bool BOX = false, int NWIN, bool PIPE = WV_CENTRE_PIPE>
+__device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWIN, SA> &L, int p, int px, int py, int s, float4 pl,
                                             bool want, bool *seldep = nullptr, uint32_t *nwc = nullptr,
                                             uint32_t *nwa = nullptr) {
     using TT = FastTex<F16, true>;  // (FastTexD measured 9 % slower in the Weak sweep: twice the texel footprint)
@@ -1739,12 +1760,19 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
         float ss = 0.0f, sss = 0.0f, srs = 0.0f;
         float inv, srp, var;
         if (k == 0) {
-            ncc_new_window<F16, 6, 2>(a, &L.rref[p], VM_P, SA ? L.tmask0[p] : ~0ull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
-            inv = L.winv[p]; srp = L.wsrp[p]; var = L.wvar[p];
+            uint64_t m0 = ~0ull;
+            if constexpr (SA) m0 = L.tmask0[p];
+            ncc_new_window<F16, 6, 2, PIPE>(a, &L.rref[p], VM_P, m0, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            inv = 1.0f / 36.0f;  // (wv_build_window's 1 / wsum over the 36 taps)
+            if constexpr (SA) inv = L.winv[p];
+            srp = L.wsrp[p]; var = L.wvar[p];
         } else {
-            ncc_new_window<F16, 3, 5>(a, &L.rref[(36 + 9 * (k - 1)) * VM_P + p], VM_P,
-                                      SA ? (uint64_t)L.tmask[(k - 1) * VM_P + p] : 0x1FFull, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
-            inv = L.winv[k * VM_P + p]; srp = L.wsrp[k * VM_P + p]; var = L.wvar[k * VM_P + p];
+            uint64_t mk = 0x1FFull;
+            if constexpr (SA) mk = L.tmask[(k - 1) * VM_P + p];
+            ncc_new_window<F16, 3, 5>(a, &L.rref[(36 + 9 * (k - 1)) * VM_P + p], VM_P, mk, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            inv = 1.0f / 9.0f;
+            if constexpr (SA) inv = L.winv[k * VM_P + p];
+            srp = L.wsrp[k * VM_P + p]; var = L.wvar[k * VM_P + p];
         }
         if (!live) continue;
         if (nwc) { if (k == 0) ++*nwc; else ++*nwa; }  // (profiling: windows evaluated)
@@ -1779,37 +1807,40 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
     return (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
 }
 
-// Occupancy: three workgroups per CU (LDS-bound at 49.5 KiB, ~161 VGPRs). Four would need both the
-// LDS below 40 KiB and the registers within 128 (124 B per lane of spills today).
+// Occupancy: the fp16 / no-SA instantiation (the headline's) at four workgroups per CU -- 39 KiB of
+// LDS at N = 10 and 128 VGPRs, with the centre window unpipelined (the pipelined window needs ~30
+// more registers and is worth < 1 % at three per CU, profiles/r5_ab_centre_pipe.txt); the others at
+// three. WV_LDS_OCC overrides both (experiments).
 #ifndef WV_WAVES
 #define WV_WAVES 4  // waves per Weak-sweep workgroup (64 pixels)
-#endif
-#ifndef WV_P5_PACKED
-#define WV_P5_PACKED 1  // P5's (candidate, pixel) items packed per view into dense lanes
 #endif
 #ifndef WV_P2_GEOM_BATCH
 #define WV_P2_GEOM_BATCH 1  // P2a's 8 geometric terms with their gathers batched (0: one at a time)
 #endif
-#ifndef WV_P5_CHUNKS
-#define WV_P5_CHUNKS 3  // P5 batches: whole views until at least this many 64-item chunks
-#endif
 #define WV_BLOCK (WV_WAVES * WAVE)
-#ifndef WV_LDS_OCC
-#define WV_LDS_OCC 3  // workgroups per CU the registers are bounded for
+template <bool F16, bool SA> struct WvOcc {
+#ifdef WV_LDS_OCC
+    static constexpr int occ = WV_LDS_OCC;
+#else
+    static constexpr int occ = (F16 && !SA) ? 4 : 3;  // workgroups per CU the registers are bounded for
 #endif
+    static constexpr bool pipe = occ < 4 && WV_CENTRE_PIPE;
+};
 template <bool F16, bool SA>
-__global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
+__global__ __launch_bounds__(WV_BLOCK, (WvOcc<F16, SA>::occ)) void k_sweep_weak_vm(Args a, const int *__restrict__ list, int count,
                                                                 int iter, const float *__restrict__ cand, int wc) {
     const int N = a.N, W = a.W;
+    constexpr bool PIPE = WvOcc<F16, SA>::pipe;
     PHASE_BEGIN;
     // direct: the pair-table kernels evaluated every pixel's anchor candidates, so P2 reads their
-    // costs from `cand` and the table is [N][64] (current plane), later [5][N][64] (wv_lds_bytes);
-    // without them (cand == nullptr: APD_NO_CAND_PAIRS=1 or a pair table that does not fit) P1
-    // evaluates the candidates here
+    // costs from `cand`; without them (cand == nullptr: APD_NO_CAND_PAIRS=1 or a pair table that does
+    // not fit) P1 evaluates the candidates here (the cost table's rows: wv_cost_rows)
     const bool direct = cand != nullptr;
-    WvLdsT<F16, 9> &L = *reinterpret_cast<WvLdsT<F16, 9> *>(apd_dyn_lds);
-    float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64] (direct: [N][64]), later [5][N][64]
-    uint8_t *wts = reinterpret_cast<uint8_t *>(costL + (direct ? 5 : 9) * N * VM_P);  // [N][64] view weights
+    WvLdsT<F16, 9, SA> &L = *reinterpret_cast<WvLdsT<F16, 9, SA> *>(apd_dyn_lds);
+    float *costL = reinterpret_cast<float *>(&L + 1);
+    uint8_t *wts = reinterpret_cast<uint8_t *>(costL + wv_cost_rows(N, direct) * VM_P);  // [N][64] view weights
+    uint8_t *asl = wts + N * VM_P;  // [N][64] anchor-selection bytes (bit k-1: anchor k selected view v)
+    const int VB = min(WV_P5_CHUNKS, N);  // views with items per P5 batch at most
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int first = blk * VM_P;
     const int np = min(VM_P, count - first);
@@ -1846,8 +1877,12 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
                 st[k] = a.weak[qk[k]];
                 sl[k] = a.sel[qk[k]];
             }
+            for (int v = 0; v < N; ++v) {
+                uint32_t b = 0;
 #pragma unroll
-            for (int k = 1; k < 9; ++k) L.asel[(k - 1) * VM_P + p1] = sl[k];
+                for (int k = 1; k < 9; ++k) b |= ((sl[k] >> v) & 1u) << (k - 1);
+                asl[v * VM_P + p1] = (uint8_t)b;
+            }
             float4 hp[9];
 #pragma unroll
             for (int k = 1; k < 9; ++k) hp[k] = a.plane[st[k] == APD_STRONG ? qk[k] : c1];
@@ -1891,7 +1926,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;
         const bool want = pv1 && ((L.flags[p1] >> h) & 1u);
         const float4 pl = L.hyp[h * VM_P + p1];
-        const float nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
+        const float nv = ncc_new_vm<F16, SA, true, 9, PIPE>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
         if (want) val = nv;
         costL[t * VM_P + p1] = val;
     }
@@ -1917,10 +1952,11 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
         const int py = c / W, px = c - py * W;
         const uint32_t hflag = L.flags[p] & 0x1FFu;
         float prior = 0.0f;
+        const uint32_t asv = asl[v * VM_P + p];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int pk = L.anc[(i + 1) * VM_P + p];  // anchor i+1's pixel, if any
-            if (pk >= 0) prior += ((L.asel[i * VM_P + p] >> v) & 1u) ? 0.9f : 0.1f;
+            if (pk >= 0) prior += ((asv >> i) & 1u) ? 0.9f : 0.1f;
         }
         float ca[8];
         if (direct) {  // the candidates' costs from the pair-table kernels; absent ones as P1 sets them
@@ -2026,7 +2062,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
             if (iter == 0 && a.wcur && !__ballot(want && __builtin_isnan(kept)))
                 nv = kept;
             else
-                nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
+                nv = ncc_new_vm<F16, SA, true, 9, PIPE>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
             if (want) {
                 val = nv;
                 if (geom) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
@@ -2118,7 +2154,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
             const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[p1];
             LANE_STAT(22, want);
             const float4 fit = fit1;
-            const float nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, fit, want, nullptr, &nwc, &nwa);
+            const float nv = ncc_new_vm<F16, SA, true, 9, PIPE>(a, L, p1, px1, py1, v + 1, fit, want, nullptr, &nwc, &nwa);
             if (want) {
                 cv = nv;
                 if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, fit), cv);
@@ -2164,14 +2200,16 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
     __syncthreads();
     PHASE_STAMP(4);
 
-#if WV_P5_PACKED
     // ---- P5: candidate evaluations (views with weight > 0), early exit against the cost after the fit
     // plane (slots 1..5). Per view the (candidate, pixel) items that are still wanted are packed into
     // dense lanes (a (candidate, view) task keeps only ~half of its 64 lanes: the view's weight is 0 or
     // the candidate is already rejected), in (candidate, pixel) order; a wave takes 64 items of ONE view
     // (the waves still sample one source image). Batches of whole views (at least WV_P5_CHUNKS chunks,
     // dealt round-robin over the waves) end with the fold, so a rejection found in a batch stops the
-    // candidate's later views. Item masks are ballots of LDS state every wave computes alike.
+    // candidate's later views. The cost table holds [5][VB][64]: a batch's views that have items
+    // (`ne`), at most one per chunk, in view order; a slot folds only views whose weight is > 0 for its
+    // pixel, where it -- live until the fold -- had an item. Item masks are ballots of LDS state every
+    // wave computes alike.
     {
         auto view_masks = [&](int v, uint64_t (&m)[5]) {
             const bool base = refine && wts[v * VM_P + p1] > 0;
@@ -2179,14 +2217,16 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
             for (int k = 0; k < 5; ++k) m[k] = __ballot(base && !dead[(1 + k) * VM_P + p1]);
         };
         for (int v0 = 0; v0 < N;) {
-            int v1 = v0, nch = 0;
-            while (v1 < N && nch < WV_P5_CHUNKS) {
+            int v1 = v0, nch = 0, nne = 0;
+            uint64_t ne = 0;  // bit v - v0: view v has items
+            while (v1 < N && nne < VB && nch < WV_P5_CHUNKS) {
                 uint64_t m[5];
                 view_masks(v1, m);
                 int t = 0;
 #pragma unroll
                 for (int k = 0; k < 5; ++k) t += __builtin_popcountll(m[k]);
                 nch += (t + WAVE - 1) / WAVE;
+                if (t > 0) { ne |= 1ull << (v1 - v0); ++nne; }
                 ++v1;
             }
             int g = 0;  // chunk index within the batch
@@ -2216,13 +2256,13 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
                     const int px = pxy & 0xFFFF, py = pxy >> 16;
                     const float4 tp = WV_CAND(L)[k * VM_P + p];
                     LANE_STAT(20, want);
-                    const float nv = ncc_new_vm<F16, SA, true>(a, L, p, px, py, v + 1, tp, want, nullptr, &nwc, &nwa);
+                    const float nv = ncc_new_vm<F16, SA, true, 9, PIPE>(a, L, p, px, py, v + 1, tp, want, nullptr, &nwc, &nwa);
                     if (want) {
                         float cv = nv;
                         if (geom) cv = fmaf(gf, geom_cost(a, px, py, v + 1, tp), cv);
                         ++issued_nn;
                         issued_g += geom;
-                        costL[(k * N + v) * VM_P + p] = cv;
+                        costL[(k * VB + __builtin_popcountll(ne & ((1ull << (v - v0)) - 1ull))) * VM_P + p] = cv;
                     }
                 }
             }
@@ -2235,7 +2275,7 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
                 float P = part[sl];
                 for (; v < v1; ++v) {
                     const int wk = wts[v * VM_P + p];
-                    if (wk > 0) P = fmaf((float)wk, costL[(k * N + v) * VM_P + p], P);
+                    if (wk > 0) P = fmaf((float)wk, costL[(k * VB + __builtin_popcountll(ne & ((1ull << (v - v0)) - 1ull))) * VM_P + p], P);
                 }
                 nxt[sl] = (uint8_t)v;
                 part[sl] = P;
@@ -2245,31 +2285,6 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
             v0 = v1;
         }
     }
-#else
-    // ---- P5: candidate tasks (views with weight > 0), view-major, early exit against the cost after
-    // the fit plane (slots 1..5)
-    for (int u0 = 0; u0 < 5 * N; u0 += WV_WAVES) {
-        if (u0 > 0)
-            for (int k = 0; k < 5; ++k) fold(1 + k, 5, k, k * N, u0);
-        const int u = u0 + wave;
-        if (u < 5 * N) {
-            const int v = u / 5, k = u - 5 * v, t = k * N + v;
-            float cv = 0.0f;
-            const bool want = refine && wts[v * VM_P + p1] > 0 && !dead[(1 + k) * VM_P + p1];
-            LANE_STAT(20, want);
-            const float4 tp = WV_CAND(L)[k * VM_P + p1];
-            const float nv = ncc_new_vm<F16, SA, true>(a, L, p1, px1, py1, v + 1, tp, want, nullptr, &nwc, &nwa);
-            if (want) {
-                cv = nv;
-                if (geom) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
-                ++issued_nn;
-                issued_g += geom;
-            }
-            costL[t * VM_P + p1] = cv;
-        }
-        __syncthreads();
-    }
-#endif
     PHASE_STAMP(5);
 
     if (a.evals && wave == 0) {
@@ -2314,12 +2329,8 @@ __global__ __launch_bounds__(WV_BLOCK, WV_LDS_OCC) void k_sweep_weak_vm(Args a, 
                 for (int k = 0; k < 5; ++k) {
                     if (dead[(1 + k) * VM_P + p1]) continue;  // its partial cost already reached cost_now
                     const float4 t = WV_CAND(L)[k * VM_P + p1];
-                    float tc = 0.0f;
-                    for (int kk = 0; kk < N; ++kk) {
-                        const int wk = wts[kk * VM_P + p1];
-                        if (wk > 0) tc = fmaf((float)wk, costL[(k * N + kk) * VM_P + p1], tc);
-                    }
-                    tc /= wn;
+                    // (P5's folds ran this slot's chain fmaf(w_v, c_v, .) over all N views in order)
+                    const float tc = part[(1 + k) * VM_P + p1] / wn;
                     const float db = depth_from_plane(cam0, t, px1, py1);
                     if (db >= a.dmin && db <= a.dmax && tc < cost_now) { pnow = t; cost_now = tc; }
                 }
@@ -4475,7 +4486,9 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
             // k_sweep_weak_vm's small cost table when every pixel's candidates are in `cand`
             const bool direct = cand != nullptr;
             LAUNCH_TEX_SA(k_sweep_weak_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(WV_BLOCK),
-                          (ctx->args.tex_f16 ? wv_lds_bytes<true, 9>(a.N, direct) : wv_lds_bytes<false, 9>(a.N, direct)), s,
+                          (ctx->args.tex_f16 ? (ctx->args.sa_any ? wv_lds_bytes<true, 9, true>(a.N, direct) : wv_lds_bytes<true, 9, false>(a.N, direct))
+                                             : (ctx->args.sa_any ? wv_lds_bytes<false, 9, true>(a.N, direct) : wv_lds_bytes<false, 9, false>(a.N, direct))),
+                          s,
                           aw, (const int *)list_ptr(ctx, 2 + colour), n, iter, cand, wc);
             prof_end(ctx, e0, APD_PROF_WEAK_SWEEP, n);
         }
