@@ -1322,15 +1322,15 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 // image-wide records at four workgroups per CU measured equal over the whole C3 N = 10 scan --
 // profiles/r5_scan_c3_n10_rec_vs_lds.txt -- and +11 % at N = 25, since its record loads scale with the
 // evaluations per pixel while this layout builds each window once per pixel; it was retired in round 5.)
-// SA = false (no SA masks in the problem): every tap of a window is valid, so the tap masks and
-// 1 / wsum are compile-time constants and their arrays shrink to one element.
+// SA = false (no SA masks in the problem): every tap of a window is valid, so the tap masks are
+// compile-time constants and their arrays shrink to one element.
 template <bool F16, int NWIN = 9, bool SA = true>
 struct WvRefT {
     static constexpr int MP = SA ? VM_P : 1;  // per-pixel extent of the SA-only arrays
     uint64_t tmask0[MP];         // SA tap masks
     // per window, the reference side of ncc_finalize over its valid taps, once per pixel instead of
-    // once per evaluation: 1 / wsum (0: empty window; SA only), sr / wsum, var_ref -- the same statements
-    float winv[NWIN * MP], wsrp[NWIN * VM_P], wvar[NWIN * VM_P];
+    // once per evaluation: sr / wsum, var_ref -- the same statements (1 / wsum: inv_lut)
+    float wsrp[NWIN * VM_P], wvar[NWIN * VM_P];
     int anc[9 * VM_P];           // packed (x, y) of anchors 0..8, -1 = none
     uint32_t flags[VM_P];        // bits 0-8: hypothesis h present (anchor STRONG); 16-24: window k evaluated
                                  // (anchor present and SA label matches); 25-27: the best anchor
@@ -1341,7 +1341,18 @@ struct WvRefT {
     typename std::conditional<F16, _Float16, float>::type rref[(36 + 9 * (NWIN - 1)) * VM_P];
     uint16_t tmask[(NWIN - 1) * MP];
     uint32_t box[2 * VM_P];      // bounding box of the anchors 0..8 (x0 | y0 << 16, x1 | y1 << 16)
+    // 1 / wsum by a window's valid-tap count (wsum is that count: each valid tap adds 1.0f), 0 for an
+    // empty window: wv_build_window's IEEE quotients, per workgroup (wv_init_lut) instead of per
+    // (pixel, window). Without SA masks wsum is 36 or 9 and the quotient a constant.
+    float inv_lut[SA ? 40 : 1];
 };
+template <bool F16, int NWIN, bool SA>
+__device__ __forceinline__ void wv_init_lut(WvRefT<F16, NWIN, SA> &L) {
+    if constexpr (SA) {
+        const int t = threadIdx.x;
+        if (t < 40) L.inv_lut[t] = t ? 1.0f / (float)t : 0.0f;
+    }
+}
 // the Weak sweep's per-workgroup state: the reference side plus the hypotheses and per-pixel state
 template <bool F16, int NWIN = 9, bool SA = true>
 struct WvLdsT : WvRefT<F16, NWIN, SA> {
@@ -1375,12 +1386,11 @@ static inline size_t wv_lds_bytes(int N, bool direct = false) {
     return APD_WV_LDS_PAD + sizeof(WvLdsT<F16, NWIN, SA>) + (size_t)wv_cost_rows(N, direct) * VM_P * sizeof(float) +
            (size_t)2 * N * VM_P;
 }
-// Occupancy: the headline's instantiation (fp16 taps, no SA masks, direct) at N = 10 fits four
-// workgroups per CU (160 KiB of LDS); with SA masks three.
+// Occupancy: the fp16 instantiations (direct) at N = 10 fit four workgroups per CU (160 KiB of LDS).
 static_assert(sizeof(WvLdsT<true, 9, false>) + 15 * VM_P * sizeof(float) + 2 * 10 * VM_P <= 160 * 1024 / 4,
               "k_sweep_weak_vm<fp16, no SA> (direct) at N = 10 must fit four workgroups per CU");
-static_assert(sizeof(WvLdsT<true, 9, true>) + 15 * VM_P * sizeof(float) + 2 * 10 * VM_P <= 160 * 1024 / 3,
-              "k_sweep_weak_vm<fp16, SA> (direct) at N = 10 must fit three workgroups per CU");
+static_assert(sizeof(WvLdsT<true, 9, true>) + 15 * VM_P * sizeof(float) + 2 * 10 * VM_P <= 160 * 1024 / 4,
+              "k_sweep_weak_vm<fp16, SA> (direct) at N = 10 must fit four workgroups per CU");
 __device__ __forceinline__ int sa_at_dev(const Args &a, int x, int y) {
     const long idx = (long)y * a.W + x;
     if (idx < 0 || idx >= a.HW) return -1;
@@ -1563,7 +1573,6 @@ __device__ __forceinline__ void wv_build_window(const Args &a, WvRefT<F16, NWIN,
     L.wsrp[k * VM_P + p1] = srp;
     L.wvar[k * VM_P + p1] = fmaf(-srp, srp, srrp);
     if constexpr (SA) {
-        L.winv[k * VM_P + p1] = ws != 0.0f ? inv : 0.0f;
         if (k == 0) L.tmask0[p1] = mask;
         else L.tmask[(k - 1) * VM_P + p1] = (uint16_t)mask;
     }
@@ -1764,14 +1773,14 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
             if constexpr (SA) m0 = L.tmask0[p];
             ncc_new_window<F16, 6, 2, PIPE>(a, &L.rref[p], VM_P, m0, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
             inv = 1.0f / 36.0f;  // (wv_build_window's 1 / wsum over the 36 taps)
-            if constexpr (SA) inv = L.winv[p];
+            if constexpr (SA) inv = L.inv_lut[__builtin_popcountll(m0)];
             srp = L.wsrp[p]; var = L.wvar[p];
         } else {
             uint64_t mk = 0x1FFull;
             if constexpr (SA) mk = L.tmask[(k - 1) * VM_P + p];
             ncc_new_window<F16, 3, 5>(a, &L.rref[(36 + 9 * (k - 1)) * VM_P + p], VM_P, mk, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
             inv = 1.0f / 9.0f;
-            if constexpr (SA) inv = L.winv[k * VM_P + p];
+            if constexpr (SA) inv = L.inv_lut[__builtin_popcount((uint32_t)mk)];
             srp = L.wsrp[k * VM_P + p]; var = L.wvar[k * VM_P + p];
         }
         if (!live) continue;
@@ -1807,10 +1816,10 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
     return (float)(0.25 * (double)center_cost + 0.75 * (double)acc);
 }
 
-// Occupancy: the fp16 / no-SA instantiation (the headline's) at four workgroups per CU -- 39 KiB of
-// LDS at N = 10 and 128 VGPRs, with the centre window unpipelined (the pipelined window needs ~30
-// more registers and is worth < 1 % at three per CU, profiles/r5_ab_centre_pipe.txt); the others at
-// three. WV_LDS_OCC overrides both (experiments).
+// Occupancy: the fp16 instantiations at four workgroups per CU -- at N = 10 38.6 KiB of LDS without
+// SA masks, 39.3 KiB with them -- and 128 VGPRs, with the centre window unpipelined (the pipelined
+// window needs ~30 more registers and is worth < 1 % at three per CU, profiles/r5_ab_centre_pipe.txt);
+// the fp32-texel ones at three. WV_LDS_OCC overrides both (experiments).
 #ifndef WV_WAVES
 #define WV_WAVES 4  // waves per Weak-sweep workgroup (64 pixels)
 #endif
@@ -1822,7 +1831,7 @@ template <bool F16, bool SA> struct WvOcc {
 #ifdef WV_LDS_OCC
     static constexpr int occ = WV_LDS_OCC;
 #else
-    static constexpr int occ = (F16 && !SA) ? 4 : 3;  // workgroups per CU the registers are bounded for
+    static constexpr int occ = F16 ? 4 : 3;  // workgroups per CU the registers are bounded for
 #endif
     static constexpr bool pipe = occ < 4 && WV_CENTRE_PIPE;
 };
@@ -1837,6 +1846,7 @@ __global__ __launch_bounds__(WV_BLOCK, (WvOcc<F16, SA>::occ)) void k_sweep_weak_
     // not fit) P1 evaluates the candidates here (the cost table's rows: wv_cost_rows)
     const bool direct = cand != nullptr;
     WvLdsT<F16, 9, SA> &L = *reinterpret_cast<WvLdsT<F16, 9, SA> *>(apd_dyn_lds);
+    wv_init_lut(L);  // (read after P0's barrier)
     float *costL = reinterpret_cast<float *>(&L + 1);
     uint8_t *wts = reinterpret_cast<uint8_t *>(costL + wv_cost_rows(N, direct) * VM_P);  // [N][64] view weights
     uint8_t *asl = wts + N * VM_P;  // [N][64] anchor-selection bytes (bit k-1: anchor k selected view v)
@@ -3234,6 +3244,7 @@ template <bool F16, bool APD, bool SA>
 __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_random_init_vm(Args a, int tw) {
     const int N = a.N;
     WvRefT<F16> *W = APD ? &reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds)->w : nullptr;
+    if constexpr (APD) wv_init_lut(*W);  // (read after the reference side's barrier)
     RiLds &L = APD ? reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds)->r : *reinterpret_cast<RiLds *>(apd_dyn_lds);
     float *cvL = APD ? reinterpret_cast<float *>(reinterpret_cast<RiApdLds<F16> *>(apd_dyn_lds) + 1)
                      : reinterpret_cast<float *>(&L + 1);  // [N][64]
