@@ -1824,7 +1824,7 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
 #define WV_WAVES 4  // waves per Weak-sweep workgroup (64 pixels)
 #endif
 #ifndef WV_P2_GEOM_BATCH
-#define WV_P2_GEOM_BATCH 1  // P2a's 8 geometric terms with their gathers batched (0: one at a time)
+X
 #endif
 #define WV_BLOCK (WV_WAVES * WAVE)
 template <bool F16, bool SA> struct WvOcc {
@@ -2065,14 +2065,15 @@ __global__ __launch_bounds__(WV_BLOCK, (WvOcc<F16, SA>::occ)) void k_sweep_weak_
         LANE_STAT(24, want);
         if (__ballot(want)) {
             const float4 pl = L.hyp[8 * VM_P + p1];
-            float nv;
             // iteration 0: the current plane is RandomInitialization's, whose NCC-New it kept (a.wcur)
-            // unless the value read a selected view; the task runs only if a lane lacks it
-            const float kept = (iter == 0 && a.wcur && want) ? a.wcur[(size_t)v * a.HW + c1] : 0.0f;
-            if (iter == 0 && a.wcur && !__ballot(want && __builtin_isnan(kept)))
-                nv = kept;
-            else
-                nv = ncc_new_vm<F16, SA, true, 9, PIPE>(a, L, p1, px1, py1, v + 1, pl, want, nullptr, &nwc, &nwa);
+            // unless the value read a selected view (NaN); only the lanes lacking it evaluate
+            const float kept = (iter == 0 && a.wcur && want) ? a.wcur[(size_t)v * a.HW + c1] : __int_as_float(0x7fc00000);
+            const bool eval = want && __builtin_isnan(kept);
+            float nv = kept;
+            if (__ballot(eval)) {
+                const float e = ncc_new_vm<F16, SA, true, 9, PIPE>(a, L, p1, px1, py1, v + 1, pl, eval, nullptr, &nwc, &nwa);
+                if (eval) nv = e;
+            }
             if (want) {
                 val = nv;
                 if (geom) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
