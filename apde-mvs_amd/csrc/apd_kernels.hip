@@ -1824,7 +1824,9 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
 #define WV_WAVES 4  // waves per Weak-sweep workgroup (64 pixels)
 #endif
 #ifndef WV_P2_GEOM_BATCH
-X
+// P2a's 8 geometric terms with their gathers batched (1) or one at a time (0): batched was -0.7 % at
+// three workgroups per CU, one at a time is -0.3 % at four (profiles/r5_ab_sa_occ4.txt, r5_ab_kept_lanes.txt)
+#define WV_P2_GEOM_BATCH 0
 #endif
 #define WV_BLOCK (WV_WAVES * WAVE)
 template <bool F16, bool SA> struct WvOcc {
