@@ -880,7 +880,12 @@ struct VmLds {  // static part; the cost table [9][N][64] and the weights [N][64
     float st[4 * VM_P];          // depth_now, cost_now, cost_init, weight_norm
     float vsu[VS_DRAWS * VM_P];  // [k][p]: the view selection's 15 uniform() draws of the pixel's stream
     uint32_t tsel[VM_P];         // views with a sampled weight > 0
+    float rmean[VM_P], rvar[VM_P];  // reference-window moments (RefWin) of pixel slot p (P3's packed items)
+    int pxy[VM_P];               // packed (x, y) of pixel slot p
 };
+#ifndef SS_P3_CHUNKS
+#define SS_P3_CHUNKS 3  // Strong sweep P3 batches: whole views until at least this many 64-item chunks
+#endif
 #define VM_CAND(L) ((L).hyp)
 // per-pixel SaWin table appended to the view-major kernels' dynamic LDS when the problem has SA masks
 static inline size_t sa_lds_bytes(const Args &a) { return a.sa_any ? VM_P * sizeof(SaWin) + 16 : 0; }
@@ -1035,7 +1040,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
                 L.nval[d * VM_P + p] = q[r] >= 0;
                 if (q[r] >= 0) L.hyp[d * VM_P + p] = hp[r];
             }
-            if (wave == 0) L.hyp[8 * VM_P + p] = hp[2];
+            if (wave == 0) { L.hyp[8 * VM_P + p] = hp[2]; L.pxy[p] = px | (py << 16); }
 #pragma unroll
             for (int kk = 0; kk < 36 / VM_WAVES; ++kk) L.refw[(wave + VM_WAVES * kk) * VM_P + p] = rv[kk];
             if (SA && wave == VM_WAVES - 1) saw[p] = sa_window(a, px, py);
@@ -1055,6 +1060,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     if (pv1) { c1 = list[first + p1]; py1 = c1 / W; px1 = c1 - py1 * W; }
     RefWin rw = refwin_from_lds<VM_P>(&L.refw[p1]);
     if (SA) rw.sa = &saw[p1];
+    if (wave == 0 && pv1) { L.rmean[p1] = rw.mean; L.rvar[p1] = rw.var; }  // (read after P1's barrier)
     // tasks whose window needs the out-of-line path are collected in `defer` (bit k = k-th task of
     // this wave) and evaluated after the loop, so the hot loop holds no call.
     uint64_t defer[2] = {0, 0};  // up to 128 tasks per wave (9 * 31 / VM_WAVES)
@@ -1193,13 +1199,15 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     }
     __syncthreads();
 
-    // ---- P3: lane = pixel, wave = (candidate, view) tasks, view-major batches of VM_WAVES (one task per
-    // wave), with the exact early exit of k_sweep_weak_vm: a candidate is accepted only if
-    // fl(S / wn) < cost_now, cost_now never exceeds its value after P2b (L.st[1]), and every view-order
-    // prefix P of the fmaf chain S (weights > 0, costs >= 0) has fl(P / wn) <= fl(S / wn); so once
-    // fl(P / wn) >= L.st[1] the candidate's remaining views are not evaluated and P4 skips it. Before
-    // each batch wave 0 folds the views the earlier batches completed into P (lane = pixel); a task
-    // deferred to the out-of-line path holds -1 until it is evaluated, which stops its prefix there.
+    // ---- P3: refinement evaluations (views with weight > 0) with the exact early exit of
+    // k_sweep_weak_vm: a candidate is accepted only if fl(S / wn) < cost_now, cost_now never exceeds its
+    // value after P2b (L.st[1]), and every view-order prefix P of the fmaf chain S (weights > 0, costs
+    // >= 0) has fl(P / wn) <= fl(S / wn); so once fl(P / wn) >= L.st[1] the candidate's remaining views
+    // are not evaluated and P4 skips it. As in the Weak sweep's P5, per view the (candidate, pixel) items
+    // still wanted are packed into dense lanes (ballots of LDS state every wave computes alike; a wave
+    // takes 64 items of ONE view), batches of whole views (>= SS_P3_CHUNKS chunks, dealt round-robin)
+    // end with the fold over the batch's views. Items whose window needs the out-of-line path are
+    // evaluated after the batch's item loop (the hot loop holds no call).
     // part / nxt / dead overlay hyp[5..7] (P2b was their last reader).
     float *part = reinterpret_cast<float *>(&L.hyp[5 * VM_P]);   // [5][64]
     uint8_t *nxt = reinterpret_cast<uint8_t *>(part + 5 * VM_P); // [5][64] next view to fold
@@ -1207,64 +1215,117 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     static_assert(5 * VM_P * (sizeof(float) + 2) <= 3 * VM_P * sizeof(float4), "early-exit state overlays hyp[5..7]");
     for (int i = tid; i < 5 * VM_P; i += VM_BLOCK) { part[i] = 0.0f; nxt[i] = 0; dead[i] = 0; }
     __syncthreads();
-    defer[0] = defer[1] = 0;
-    for (int u0 = 0, kt = 0; u0 < 5 * N; u0 += VM_WAVES, ++kt) {
-        if (u0 > 0 && wave == 0) {
-            const float thr = L.st[1 * VM_P + p1], wn = L.st[3 * VM_P + p1];
-#pragma unroll 1
-            for (int k = 0; k < 5; ++k) {
-                const int it = k * VM_P + p1;
-                if (dead[it]) continue;
-                int v = nxt[it];
-                float P = part[it];
-                const int v0 = v;
-                for (; v < N && v * 5 + k < u0; ++v) {
-                    const int wk = wts[v * VM_P + p1];
-                    if (wk > 0) {
-                        const float c = costL[(k * N + v) * VM_P + p1];
-                        if (c < 0.0f) break;  // deferred: not evaluated yet
-                        P = fmaf((float)wk, c, P);
+    {
+        auto view_masks = [&](int v, uint64_t (&m)[5]) {
+            const bool base = pv1 && wts[v * VM_P + p1] > 0;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) m[k] = __ballot(base && !dead[k * VM_P + p1]);
+        };
+        // item `it` of view v's packing (masks m, prefix offsets off) -> candidate k, pixel slot p
+        auto decode = [&](const uint64_t (&m)[5], const int (&off)[6], int it, int &k, int &p) {
+            k = 0;
+#pragma unroll
+            for (int q = 1; q < 5; ++q) k += it >= off[q];
+            uint64_t mk = m[0];
+            int pk = 0;
+#pragma unroll
+            for (int q = 1; q < 5; ++q) if (k == q) { mk = m[q]; pk = off[q]; }
+            p = nth_set_bit(mk, it - pk);
+        };
+        for (int v0 = 0; v0 < N;) {
+            int v1 = v0, nch = 0;
+            while (v1 < N && nch < SS_P3_CHUNKS) {
+                uint64_t m[5];
+                view_masks(v1, m);
+                int t = 0;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) t += __builtin_popcountll(m[k]);
+                nch += (t + WAVE - 1) / WAVE;
+                ++v1;
+            }
+            uint64_t wdef = 0, ldef = 0;  // chunks of this batch with a deferred item: in the wave / this lane's
+            int g = 0;                    // chunk index within the batch
+            for (int v = v0; v < v1; ++v) {
+                uint64_t m[5];
+                view_masks(v, m);
+                int off[6];
+                off[0] = 0;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) off[k + 1] = off[k] + __builtin_popcountll(m[k]);
+                const int nv_items = off[5];
+                for (int j = 0; j * WAVE < nv_items; ++j, ++g) {
+                    if (g % VM_WAVES != wave) continue;
+                    const int it = j * WAVE + lane;
+                    const bool want = it < nv_items;
+                    int k = 0, p = p1;
+                    if (want) decode(m, off, it, k, p);
+                    const int xy = L.pxy[p];
+                    const int px = xy & 0xFFFF, py = xy >> 16;
+                    bool slow = false;
+                    if (want) {
+                        const RefWin rwq{&L.refw[p], L.rmean[p], L.rvar[p], SA ? &saw[p] : nullptr};
+                        const float4 tp = VM_CAND(L)[k * VM_P + p];
+                        ++issued;
+                        float cv = ncc_old_fast<F16, VM_P>(a, px, py, v + 1, tp, rwq, slow);
+                        if (!slow) {
+                            if (geom_imp) cv = fmaf(gf, geom_cost(a, px, py, v + 1, tp), cv);
+                            costL[(k * N + v) * VM_P + p] = cv;
+                        }
+                    }
+                    if (__ballot(slow)) {
+                        wdef |= 1ull << g;
+                        if (slow) ldef |= 1ull << g;
                     }
                 }
-                if (v == v0) continue;
-                nxt[it] = (uint8_t)v;
-                part[it] = P;
-                if (P / wn >= thr) dead[it] = 1;
             }
-        }
-        const int u = u0 + wave;
-        if (u < 5 * N) {
-            const int v = u / 5, k = u - 5 * v, t = k * N + v;
-            float cv = 0.0f;
-            // a view with sampled weight 0 contributes fmaf(0, cv, tc) == tc for every finite cv (costs are
-            // clamped to [0, 2]), so its refinement NCCs are skipped without changing any result
-            if (pv1 && wts[v * VM_P + p1] > 0 && !dead[k * VM_P + p1]) {
-                const float4 tp = VM_CAND(L)[k * VM_P + p1];
-                bool slow;
-                ++issued;
-                cv = ncc_old_fast<F16, VM_P>(a, px1, py1, v + 1, tp, rw, slow);
-                if (slow) {
-                    defer[kt >> 6] |= 1ull << (kt & 63);
-                    cv = -1.0f;
-                } else if (geom_imp) {
-                    cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
+            // this wave's deferred items: find each chunk's view and offset again (wave-uniform walk)
+            while (wdef) {
+                const int gd = __builtin_ctzll(wdef);
+                wdef &= wdef - 1;
+                int gg = 0;
+                for (int v = v0; v < v1; ++v) {
+                    uint64_t m[5];
+                    view_masks(v, m);
+                    int off[6];
+                    off[0] = 0;
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) off[k + 1] = off[k] + __builtin_popcountll(m[k]);
+                    const int nc = (off[5] + WAVE - 1) / WAVE;
+                    if (gd < gg + nc) {
+                        if ((ldef >> gd) & 1ull) {
+                            int k, p;
+                            decode(m, off, (gd - gg) * WAVE + lane, k, p);
+                            const int xy = L.pxy[p];
+                            const int px = xy & 0xFFFF, py = xy >> 16;
+                            const float4 tp = VM_CAND(L)[k * VM_P + p];
+                            float cv = ncc_old_slow<F16>(a.self, px, py, v + 1, tp, &L.refw[p], VM_P, L.rmean[p], L.rvar[p]);
+                            if (geom_imp) cv = fmaf(gf, geom_cost(a, px, py, v + 1, tp), cv);
+                            costL[(k * N + v) * VM_P + p] = cv;
+                        }
+                        break;
+                    }
+                    gg += nc;
                 }
             }
-            costL[t * VM_P + p1] = cv;
+            __syncthreads();
+            // fold views [nxt, v1) of the pixels' 5 slots (all threads: slot i / 64)
+            for (int i = tid; i < 5 * VM_P; i += VM_BLOCK) {
+                const int k = i / VM_P, p = i - k * VM_P;
+                if (dead[i] || p >= np) continue;
+                int v = nxt[i];
+                float P = part[i];
+                for (; v < v1; ++v) {
+                    const int wk = wts[v * VM_P + p];
+                    if (wk > 0) P = fmaf((float)wk, costL[(k * N + v) * VM_P + p], P);
+                }
+                nxt[i] = (uint8_t)v;
+                part[i] = P;
+                if (P / L.st[3 * VM_P + p] >= L.st[1 * VM_P + p]) dead[i] = 1;
+            }
+            __syncthreads();
+            v0 = v1;
         }
-        __syncthreads();
     }
-    for (int w2 = 0; w2 < 2; ++w2)
-    while (defer[w2]) {
-        const int kt = __builtin_ctzll(defer[w2]) + 64 * w2;
-        defer[w2] &= defer[w2] - 1;
-        const int u = wave + kt * VM_WAVES, v = u / 5, k = u - 5 * v, t = k * N + v;
-        const float4 tp = VM_CAND(L)[k * VM_P + p1];
-        float cv = ncc_old_slow<F16>(a.self, px1, py1, v + 1, tp, rw.r, VM_P, rw.mean, rw.var);
-        if (geom_imp) cv = fmaf(gf, geom_cost(a, px1, py1, v + 1, tp), cv);
-        costL[t * VM_P + p1] = cv;
-    }
-    __syncthreads();
 
     if (a.evals) {  // profiling: one atomic per wave
         uint32_t sum = issued;
@@ -1285,9 +1346,9 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
             for (int k = 0; k < 5; ++k) {
                 if (dead[k * VM_P + p]) continue;  // its partial cost already reached cost_now
                 const float4 t = VM_CAND(L)[k * VM_P + p];
-                float tc = 0.0f;
-                for (int kk = 0; kk < N; ++kk) tc = fmaf((float)wts[kk * VM_P + p], costL[(k * N + kk) * VM_P + p], tc);
-                tc /= wn;
+                // (P3's folds ran this slot's chain fmaf(w_v, c_v, .) over all N views in order; a weight-0
+                // view adds fmaf(0, c_v, tc) == tc)
+                const float tc = part[k * VM_P + p] / wn;
                 const float db = depth_from_plane(cam0, t, px1, py1);
                 if (db >= a.dmin && db <= a.dmax && tc < cost_now) { pnow = t; cost_now = tc; }
             }

@@ -3,7 +3,7 @@ library builds, interleaved in one process. Priors come from FIRST_INIT runs of 
 views (first library), as in tools/time_apd_pass.py. Prints the HIP-event breakdown per build and
 whether every build's outputs are bit-identical to the first's.
 Usage: python tools/ab_apd.py libA.so[:ENV=VAL,...] libB.so [...]   (AB_W / AB_H / AB_N / AB_ROUNDS / AB_SA;
-AB_FIRST=1 times a FIRST_INIT problem instead)"""
+AB_FIRST=1 times a FIRST_INIT problem instead; AB_TEXTURE=rich the texture-rich scene)"""
 import os, sys, statistics
 import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -12,7 +12,7 @@ import apd_abi as A, synth, cases
 
 W, H, N = int(os.environ.get("AB_W", 3024)), int(os.environ.get("AB_H", 2016)), int(os.environ.get("AB_N", 8))
 ROUNDS = int(os.environ.get("AB_ROUNDS", 3))
-sc = synth.make_scene(W, H, N)
+sc = synth.make_scene(W, H, N, texture=os.environ.get("AB_TEXTURE", "smooth"))  # AB_TEXTURE=rich: the texture-rich variant
 
 
 def make_engine(spec):
