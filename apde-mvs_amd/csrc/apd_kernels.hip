@@ -2445,8 +2445,15 @@ __global__ __launch_bounds__(WV_BLOCK, (WvOcc<F16, SA>::occ)) void k_sweep_weak_
 //     pixel, wave = candidate) and the focal combination reading the pair costs, and writes the same
 //     [view][candidate][WEAK index] costs the sweep reads (direct mode).
 // ---------------------------------------------------------------------------------------------
+#ifndef GP_CHUNK
 #define GP_CHUNK 256   // references per batch of k_gp_dedup (one workgroup per window anchor)
-#define GP_HS 8192     // LDS hash slots (a table closes at GP_HS / 2 keys; + <= 8 * GP_CHUNK per batch: load <= 0.75)
+#endif
+#ifndef GP_HS
+#define GP_HS 8192     // LDS hash slots
+#endif
+// a table closes once it holds GP_CLOSE keys after a batch; a batch adds <= 8 * GP_CHUNK: load <= 0.75
+#define GP_CLOSE (GP_HS * 3 / 4 - 8 * GP_CHUNK)
+static_assert(GP_CLOSE > 0 && GP_HS >= 256 && 256 % GP_CHUNK == 0, "k_gp_dedup table sizing");
 #define GP_NONE 0xFFFFFFFFu
 
 // profiling: a wave's sum of the lanes' counts, one atomic per wave
@@ -2611,7 +2618,7 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
         // every thread has read nfresh before any wave's next-batch inserts can add to it (else
         // `close` and `base` could differ between waves)
         __syncthreads();
-        const bool close = nd >= GP_HS / 2 || b0 + GP_CHUNK >= n;
+        const bool close = nd >= GP_CLOSE || b0 + GP_CHUNK >= n;
         if (!close) continue;  // (uniform)
         if (PASS == 1) {
             // plist[base + id] = (window anchor, candidate anchor)
