@@ -499,7 +499,11 @@ struct FastMod {
         return (uint32_t)__umul64hi(low, (uint64_t)d);
     }
 };
-__global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
+// stage (SPLIT, [34][wc] words per WEAK index wi): [wi] the stream position << 6 | the number of
+// points (0: no RANSAC), [wc + wi] the pixel, [(2 + i) * wc + wi] point i (short2, dvalid order):
+// k_gen_anchors_fit runs the RANSAC
+template <bool SPLIT>
+__global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restrict__ stage, int wc) {
     const int c = blockIdx.x * BLOCK + threadIdx.x;
     if (c >= a.HW) return;
     if (a.weak[c] != APD_WEAK) return;
@@ -597,73 +601,204 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a) {
             }
         }
     }
-    if (nsp <= 3) { a.reliable[c] = 0; return; }
-    short2 vp[32];
-    float v3[32][3];
-    int vc = 0;
-    float X[3];
-    get3d(cam, (float)px, (float)py, a.plane[c].w, X);
-    const float cw0 = X[0], cw1 = X[1], cw2 = X[2];
-    for (int i = 0; i < 32; ++i) {
-        vp[i] = make_short2(-1, -1);
-        if ((dvalid >> i) & 1u) {
-            vp[vc] = sp[i];
-            get3d(cam, (float)sp[i].x, (float)sp[i].y, a.plane[sp[i].x + sp[i].y * W].w, X);
-            v3[vc][0] = X[0]; v3[vc][1] = X[1]; v3[vc][2] = X[2];
-            vc++;
-        }
+    if (nsp <= 3) {
+        a.reliable[c] = 0;
+        if constexpr (SPLIT) stage[a.amap[c]] = 0u;
+        return;
     }
-    float4 best = make_float4(0, 0, 0, 0);
-    int ua = -1, ub = -1, uc = -1;
-    bool has = false;
-    float min_cost = APD_FLT_MAX;
-    int max_count = 3;
+    if constexpr (SPLIT) {
+        const size_t wi = (size_t)a.amap[c];
+        int vc = 0;
+        for (int i = 0; i < 32; ++i)
+            if ((dvalid >> i) & 1u) {
+                stage[(size_t)(2 + vc) * wc + wi] = (uint32_t)(uint16_t)sp[i].x | ((uint32_t)(uint16_t)sp[i].y << 16);
+                vc++;
+            }
+        stage[wi] = (g.n << 6) | (uint32_t)vc;
+        stage[(size_t)wc + wi] = (uint32_t)c;
+        return;
+    } else {
+        short2 vp[32];
+        float v3[32][3];
+        int vc = 0;
+        float X[3];
+        get3d(cam, (float)px, (float)py, a.plane[c].w, X);
+        const float cw0 = X[0], cw1 = X[1], cw2 = X[2];
+        for (int i = 0; i < 32; ++i) {
+            vp[i] = make_short2(-1, -1);
+            if ((dvalid >> i) & 1u) {
+                vp[vc] = sp[i];
+                get3d(cam, (float)sp[i].x, (float)sp[i].y, a.plane[sp[i].x + sp[i].y * W].w, X);
+                v3[vc][0] = X[0]; v3[vc][1] = X[1]; v3[vc][2] = X[2];
+                vc++;
+            }
+        }
+        float4 best = make_float4(0, 0, 0, 0);
+        int ua = -1, ub = -1, uc = -1;
+        bool has = false;
+        float min_cost = APD_FLT_MAX;
+        int max_count = 3;
+        const FastMod fm((uint32_t)vc);
+        for (int it = 0; it < 50; ++it) {
+            int ia = (int)fm.mod(g.u32());
+            int ib = (int)fm.mod(g.u32());
+            int ic = (int)fm.mod(g.u32());
+            if (ia == ib || ib == ic || ia == ic) continue;
+            if (!point_in_triangle(vp[ia].x, vp[ia].y, vp[ib].x, vp[ib].y, vp[ic].x, vp[ic].y, px, py)) continue;
+            const float *A = v3[ia], *B = v3[ib], *C = v3[ic];
+            float ACx = A[0] - C[0], ACy = A[1] - C[1], ACz = A[2] - C[2];
+            float BCx = B[0] - C[0], BCy = B[1] - C[1], BCz = B[2] - C[2];
+            float4 cr = make_float4(ACy * BCz - BCy * ACz, -(ACx * BCz - BCx * ACz), ACx * BCy - BCx * ACy, 0.0f);
+            if ((cr.x == 0 && cr.y == 0 && cr.z == 0) || isnan(cr.x) || isnan(cr.y) || isnan(cr.z)) continue;
+            normalize3(cr);
+            cr.w = -(cr.x * A[0] + cr.y * A[1] + cr.z * A[2]);
+            int tcnt = 0;
+            for (int k = 0; k < vc; ++k) {
+                float d = fabsf(cr.x * v3[k][0] + cr.y * v3[k][1] + cr.z * v3[k][2] + cr.w);
+                if (anc_inlier(a, d, depth_diff)) tcnt++;
+            }
+            if (tcnt < 6) continue;
+            if (tcnt > max_count) {
+                max_count = tcnt;
+                min_cost = fabsf(cr.x * cw0 + cr.y * cw1 + cr.z * cw2 + cr.w);
+                best = cr; has = true; ua = ia; ub = ib; uc = ic;
+            } else if (tcnt == max_count) {
+                float cd = fabsf(cr.x * cw0 + cr.y * cw1 + cr.z * cw2 + cr.w);
+                if (cd < min_cost) { min_cost = cd; best = cr; ua = ia; ub = ib; uc = ic; }
+            }
+        }
+        if (!has) { a.reliable[c] = 0; return; }
+        float wgt[32];
+        for (int i = 0; i < vc; ++i) {
+            float d = fabsf(best.x * v3[i][0] + best.y * v3[i][1] + best.z * v3[i][2] + best.w);
+            if (!anc_inlier(a, d, depth_diff)) { vp[i] = make_short2(-1, -1); wgt[i] = APD_FLT_MAX; continue; }
+            if (i == ua || i == ub || i == uc) d -= 1;
+            wgt[i] = d;
+        }
+        for (int i = 1; i < vc; ++i) {  // sort_small_weighted, APD.cu:25-38
+            short2 tp = vp[i];
+            float tw = wgt[i];
+            int j;
+            for (j = i; j >= 1 && tw < wgt[j - 1]; j--) { vp[j] = vp[j - 1]; wgt[j] = wgt[j - 1]; }
+            vp[j] = tp; wgt[j] = tw;
+        }
+        for (int i = 1; i < 9; ++i) anc[i] = vp[i - 1];
+        a.reliable[c] = 1;
+    }
+}
+
+// GenAnchors' RANSAC and anchor ordering (APD.cu:1994-2081), a wave per WEAK pixel with a pending
+// RANSAC (the search's stage): lane i holds point i; lane `it` < 50 runs RANSAC iteration it (its 3
+// draws are stream positions n + 3 it .. n + 3 it + 2, so a Philox block per lane stands for the
+// sequential stream), counting inliers over the points broadcast lane by lane. The sequential
+// selection -- a larger inlier count wins, an equal count a strictly smaller centre distance, so the
+// earliest of equal candidates stays -- is replayed over the lanes in iteration order, and
+// sort_small_weighted (stable insertion sort) is a rank: #{j : w_j < w_i} + #{j < i : w_j == w_i}.
+// The same statements per iteration as k_gen_anchors<false> (the path taken when the stage does not
+// fit): that kernel's per-lane point arrays went to scratch and to HBM (74 % waiting, L2 hit 24 %,
+// profiles/r5_pmc_k_gen_anchors_c3.json), and an LDS version at one pixel per lane was as slow.
+__device__ __forceinline__ uint32_t rng_draw(const Rng &g, uint32_t d) {
+    const uint4 b = g.block(d >> 2);
+    const uint32_t j = d & 3u;
+    return j == 0 ? b.x : (j == 1 ? b.y : (j == 2 ? b.z : b.w));
+}
+#define GA_FIT_WAVES 4
+__global__ __launch_bounds__(GA_FIT_WAVES * WAVE) void k_gen_anchors_fit(Args a, const uint32_t *__restrict__ stage, int wc) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wi = __builtin_amdgcn_readfirstlane(blockIdx.x * GA_FIT_WAVES + (int)(threadIdx.x >> 6));
+    if (wi >= wc) return;
+    const uint32_t hdr = __builtin_amdgcn_readfirstlane(stage[wi]);
+    const int vc = (int)(hdr & 63u);
+    if (vc == 0) return;
+    const int c = __builtin_amdgcn_readfirstlane((int)stage[(size_t)wc + wi]);
+    const int W = a.W;
+    const int py = c / W, px = c - py * W;
+    const float depth_diff = a.dmax - a.dmin;
+    const APD_C Cam &cam = a.cams[0];
+    // lane i: point i (X, Y, Z, packed position)
+    float X[3] = {0.0f, 0.0f, 0.0f};
+    uint32_t q = 0xFFFFFFFFu;
+    if (lane < vc) {
+        q = stage[(size_t)(2 + lane) * wc + wi];
+        const int qx = (int)(int16_t)(q & 0xFFFFu), qy = (int)(int16_t)(q >> 16);
+        get3d(cam, (float)qx, (float)qy, a.plane[qx + qy * W].w, X);
+    }
+    const float X0 = X[0], X1 = X[1], X2 = X[2];
+    float Cw[3];
+    get3d(cam, (float)px, (float)py, a.plane[c].w, Cw);
+    // lane it: RANSAC iteration it
+    const Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_ANCHORS);
     const FastMod fm((uint32_t)vc);
-    for (int it = 0; it < 50; ++it) {
-        int ia = (int)fm.mod(g.u32());
-        int ib = (int)fm.mod(g.u32());
-        int ic = (int)fm.mod(g.u32());
-        if (ia == ib || ib == ic || ia == ic) continue;
-        if (!point_in_triangle(vp[ia].x, vp[ia].y, vp[ib].x, vp[ib].y, vp[ic].x, vp[ic].y, px, py)) continue;
-        const float *A = v3[ia], *B = v3[ib], *C = v3[ic];
-        float ACx = A[0] - C[0], ACy = A[1] - C[1], ACz = A[2] - C[2];
-        float BCx = B[0] - C[0], BCy = B[1] - C[1], BCz = B[2] - C[2];
-        float4 cr = make_float4(ACy * BCz - BCy * ACz, -(ACx * BCz - BCx * ACz), ACx * BCy - BCx * ACy, 0.0f);
-        if ((cr.x == 0 && cr.y == 0 && cr.z == 0) || isnan(cr.x) || isnan(cr.y) || isnan(cr.z)) continue;
+    const uint32_t d0 = (hdr >> 6) + 3u * (uint32_t)lane;
+    const int ia = (int)fm.mod(rng_draw(g, d0));
+    const int ib = (int)fm.mod(rng_draw(g, d0 + 1u));
+    const int ic = (int)fm.mod(rng_draw(g, d0 + 2u));
+    bool ok = lane < 50 && !(ia == ib || ib == ic || ia == ic);
+    const float Ax = __shfl(X0, ia), Ay = __shfl(X1, ia), Az = __shfl(X2, ia);
+    const float Bx = __shfl(X0, ib), By = __shfl(X1, ib), Bz = __shfl(X2, ib);
+    const float Cx = __shfl(X0, ic), Cy = __shfl(X1, ic), Cz = __shfl(X2, ic);
+    const uint32_t qa = (uint32_t)__shfl((int)q, ia), qb = (uint32_t)__shfl((int)q, ib), qc = (uint32_t)__shfl((int)q, ic);
+    ok = ok && point_in_triangle((int16_t)(qa & 0xFFFFu), (int16_t)(qa >> 16), (int16_t)(qb & 0xFFFFu), (int16_t)(qb >> 16),
+                                 (int16_t)(qc & 0xFFFFu), (int16_t)(qc >> 16), px, py);
+    float ACx = Ax - Cx, ACy = Ay - Cy, ACz = Az - Cz;
+    float BCx = Bx - Cx, BCy = By - Cy, BCz = Bz - Cz;
+    float4 cr = make_float4(ACy * BCz - BCy * ACz, -(ACx * BCz - BCx * ACz), ACx * BCy - BCx * ACy, 0.0f);
+    ok = ok && !((cr.x == 0 && cr.y == 0 && cr.z == 0) || isnan(cr.x) || isnan(cr.y) || isnan(cr.z));
+    if (ok) {
         normalize3(cr);
-        cr.w = -(cr.x * A[0] + cr.y * A[1] + cr.z * A[2]);
-        int tcnt = 0;
-        for (int k = 0; k < vc; ++k) {
-            float d = fabsf(cr.x * v3[k][0] + cr.y * v3[k][1] + cr.z * v3[k][2] + cr.w);
-            if (anc_inlier(a, d, depth_diff)) tcnt++;
+        cr.w = -(cr.x * Ax + cr.y * Ay + cr.z * Az);
+    }
+    int tcnt = 0;
+    for (int k = 0; k < vc; ++k) {  // (k uniform: the point's coordinates by readlane)
+        const float P0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(X0), k));
+        const float P1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(X1), k));
+        const float P2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(X2), k));
+        float d = fabsf(cr.x * P0 + cr.y * P1 + cr.z * P2 + cr.w);
+        if (anc_inlier(a, d, depth_diff)) tcnt++;
+    }
+    ok = ok && tcnt >= 6;
+    const float cd = fabsf(cr.x * Cw[0] + cr.y * Cw[1] + cr.z * Cw[2] + cr.w);
+    // the sequential selection, replayed in iteration order (uniform)
+    const uint64_t okm = __ballot(ok);
+    int best_it = -1, max_count = 3;
+    float min_cost = APD_FLT_MAX;
+    for (uint64_t m = okm; m; m &= m - 1) {
+        const int it = __builtin_ctzll(m);
+        const int tc = __builtin_amdgcn_readlane(tcnt, it);
+        const float ci = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cd), it));
+        if (tc > max_count) { max_count = tc; min_cost = ci; best_it = it; }
+        else if (tc == max_count && ci < min_cost) { min_cost = ci; best_it = it; }
+    }
+    if (best_it < 0) {
+        if (lane == 0) a.reliable[c] = 0;
+        return;
+    }
+    float4 best;
+    best.x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cr.x), best_it));
+    best.y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cr.y), best_it));
+    best.z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cr.z), best_it));
+    best.w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cr.w), best_it));
+    const int ua = __builtin_amdgcn_readlane(ia, best_it), ub = __builtin_amdgcn_readlane(ib, best_it),
+              uc = __builtin_amdgcn_readlane(ic, best_it);
+    // weights, then the stable rank of each point (sort_small_weighted, APD.cu:25-38)
+    float wgt = APD_FLT_MAX;
+    uint32_t vq = 0xFFFFFFFFu;
+    if (lane < vc) {
+        float d = fabsf(best.x * X0 + best.y * X1 + best.z * X2 + best.w);
+        if (anc_inlier(a, d, depth_diff)) {
+            if (lane == ua || lane == ub || lane == uc) d -= 1;
+            wgt = d;
+            vq = q;
         }
-        if (tcnt < 6) continue;
-        if (tcnt > max_count) {
-            max_count = tcnt;
-            min_cost = fabsf(cr.x * cw0 + cr.y * cw1 + cr.z * cw2 + cr.w);
-            best = cr; has = true; ua = ia; ub = ib; uc = ic;
-        } else if (tcnt == max_count) {
-            float cd = fabsf(cr.x * cw0 + cr.y * cw1 + cr.z * cw2 + cr.w);
-            if (cd < min_cost) { min_cost = cd; best = cr; ua = ia; ub = ib; uc = ic; }
-        }
     }
-    if (!has) { a.reliable[c] = 0; return; }
-    float wgt[32];
-    for (int i = 0; i < vc; ++i) {
-        float d = fabsf(best.x * v3[i][0] + best.y * v3[i][1] + best.z * v3[i][2] + best.w);
-        if (!anc_inlier(a, d, depth_diff)) { vp[i] = make_short2(-1, -1); wgt[i] = APD_FLT_MAX; continue; }
-        if (i == ua || i == ub || i == uc) d -= 1;
-        wgt[i] = d;
+    int rank = 0;
+    for (int j = 0; j < vc; ++j) {
+        const float wj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wgt), j));
+        rank += (wj < wgt || (wj == wgt && j < lane)) ? 1 : 0;
     }
-    for (int i = 1; i < vc; ++i) {  // sort_small_weighted, APD.cu:25-38
-        short2 tp = vp[i];
-        float tw = wgt[i];
-        int j;
-        for (j = i; j >= 1 && tw < wgt[j - 1]; j--) { vp[j] = vp[j - 1]; wgt[j] = wgt[j - 1]; }
-        vp[j] = tp; wgt[j] = tw;
-    }
-    for (int i = 1; i < 9; ++i) anc[i] = vp[i - 1];
-    a.reliable[c] = 1;
+    APD_G short2 *anc = a.anchors + (size_t)wi * 9;
+    if (lane < vc && rank < 8) anc[1 + rank] = make_short2((short)(vq & 0xFFFFu), (short)(vq >> 16));
+    if (lane == 0) a.reliable[c] = 1;
 }
 
 // NeigbourUpdate (APD.cu:2084-2100)
@@ -3702,7 +3837,7 @@ struct apd_ctx {
     std::string err;
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
-        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, lrs, wcur, arec,
+        fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, lrs, wcur, arec, ga_stage,
         wlist, gp_cb, gp_cnt, gp_cur, gp_refs, gp_ccnt, gp_cbase, gp_plist, gp_pidx, gp_pcost, gp_tmp, dpairs;
     int n_near = 0;
     int host_stat[4] = {0, 0, 0, 0};  // apd_set_problem's read-back (see there)
@@ -3715,6 +3850,7 @@ struct apd_ctx {
     bool cand_pairs = true;        // Weak sweep candidates through the image-wide pair table; APD_NO_CAND_PAIRS=1
                                    // leaves them to the sweep
     bool gp_on = false;            // the pair table of the prepared problem is built (apd_stage_prepare)
+    bool ga_split = true;          // GenAnchors' RANSAC in k_gen_anchors_fit; APD_NO_GA_SPLIT=1: in k_gen_anchors
     bool rec_on = false;           // the anchor-window records of the prepared problem are built (k_anchor_rec)
     bool dtex = true;              // DepthToWeak over pre-differenced fp16 texels (FastTexD); APD_NO_DTEX=1 disables
     int gp_np = 0;                 // its distinct pairs
@@ -3927,6 +4063,7 @@ apd_ctx *apd_create(int32_t device) {
     for (auto &e : ctx->ev_side) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     ctx->overlap = getenv("APD_NO_OVERLAP") == nullptr;
     ctx->cand_pairs = getenv("APD_NO_CAND_PAIRS") == nullptr;
+    ctx->ga_split = getenv("APD_NO_GA_SPLIT") == nullptr;
     ctx->lr_handover = getenv("APD_NO_LR_HANDOVER") == nullptr;
     ctx->wcur_on = getenv("APD_NO_WCUR") == nullptr;
     ctx->dtex = getenv("APD_NO_DTEX") == nullptr;
@@ -3966,7 +4103,7 @@ void apd_destroy(apd_ctx *ctx) {
     DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
-                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand, &ctx->arec,
+                      &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand, &ctx->arec, &ctx->ga_stage,
                       &ctx->lrs, &ctx->wcur, &ctx->wlist, &ctx->gp_cb, &ctx->gp_cnt, &ctx->gp_cur, &ctx->gp_refs, &ctx->gp_ccnt,
                       &ctx->gp_cbase, &ctx->gp_plist, &ctx->gp_pidx, &ctx->gp_pcost, &ctx->gp_tmp, &ctx->dpairs};
     for (DevBuf *b : bufs)
@@ -4364,7 +4501,17 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         {
             Args ag = a;  // (profiling counters: instrumented builds of k_gen_anchors only)
             ag.evals = (ctx->prof && ctx->evals.p) ? (APD_G unsigned long long *)ctx->evals.p : nullptr;
-            hipLaunchKernelGGL(k_gen_anchors, dim3(gpx), dim3(BLOCK), 0, s, ag);
+            // the RANSAC in its own kernel when the stage fits (34 words per WEAK pixel); else in k_gen_anchors
+            const size_t wc = (size_t)std::max(ctx->weak_count, 1);
+            uint32_t *stage = (ctx->ga_split && ctx->weak_count > 0 && try_ensure(ctx, ctx->ga_stage, 34 * wc * sizeof(uint32_t)))
+                                  ? (uint32_t *)ctx->ga_stage.p : nullptr;
+            if (stage) {
+                hipLaunchKernelGGL(k_gen_anchors<true>, dim3(gpx), dim3(BLOCK), 0, s, ag, stage, (int)wc);
+                hipLaunchKernelGGL(k_gen_anchors_fit, dim3(blocks_for(wc, GA_FIT_WAVES)), dim3(GA_FIT_WAVES * WAVE), 0, s, a,
+                                   (const uint32_t *)stage, (int)wc);
+            } else {
+                hipLaunchKernelGGL(k_gen_anchors<false>, dim3(gpx), dim3(BLOCK), 0, s, ag, stage, (int)wc);
+            }
         }
         hipLaunchKernelGGL(k_neighbour_update, dim3(gpx), dim3(BLOCK), 0, s, a);
         if ((st = check_launch(ctx, "anchors"))) return st;
