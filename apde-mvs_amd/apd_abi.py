@@ -76,7 +76,8 @@ class ApdOutputs(C.Structure):
 class ApdTiming(C.Structure):
     _fields_ = [("total_ms", C.c_float), ("init_ms", C.c_float), ("anchors_ms", C.c_float),
                 ("sweep_ms", C.c_float), ("post_ms", C.c_float), ("iter_ms", C.c_float * 8),
-                ("iterations", C.c_int32), ("lists_ms", C.c_float), ("pairs_ms", C.c_float)]
+                ("iterations", C.c_int32), ("lists_ms", C.c_float), ("pairs_ms", C.c_float),
+                ("join_ms", C.c_float), ("prepare_ms", C.c_float)]
 
 
 def default_params(num_images: int, depth_min: float, depth_max: float, **kw) -> ApdParams:
@@ -222,7 +223,7 @@ class Outputs:
 
 EXPORTS = ["apd_abi_version", "apd_device_count", "apd_create", "apd_destroy", "apd_last_error",
            "apd_set_problem", "apd_run_patchmatch", "apd_stage_prepare", "apd_stage_iteration",
-           "apd_stage_finish", "apd_synchronize", "apd_get_results", "apd_get_timing", "apd_profile_reset",
+           "apd_stage_finish", "apd_synchronize", "apd_get_results", "apd_get_timing", "apd_get_prepare_timing", "apd_profile_reset",
            "apd_profile_query", "apd_profile_kernel", "apd_profile_counters", "apd_profile_evaluations", "apd_epilogue", "apd_device_alloc", "apd_device_free",
            "apd_device_copy", "apd_device_mem_info", "apd_device_resize_nearest", "apd_result_device", "apd_fusion_create", "apd_fusion_destroy",
            "apd_fusion_last_error", "apd_fusion_set_views", "apd_fusion_weak_filter", "apd_fusion_consistency",
@@ -270,6 +271,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.apd_get_results.argtypes = [C.c_void_p, C.POINTER(ApdOutputs)]
     lib.apd_get_timing.restype = C.c_int32
     lib.apd_get_timing.argtypes = [C.c_void_p, C.POINTER(ApdTiming)]
+    lib.apd_get_prepare_timing.restype = C.c_int32
+    lib.apd_get_prepare_timing.argtypes = [C.c_void_p, C.POINTER(ApdTiming)]
     lib.apd_profile_reset.restype = C.c_int32
     lib.apd_profile_reset.argtypes = [C.c_void_p, C.c_int32]
     lib.apd_profile_evaluations.restype = C.c_int32
@@ -459,6 +462,12 @@ class Engine:
     def timing(self) -> ApdTiming:
         t = ApdTiming()
         self._check(self.lib.apd_get_timing(self.ctx, C.byref(t)), "apd_get_timing")
+        return t
+
+    def prepare_timing(self) -> ApdTiming:
+        """The prepare-phase fields of the last apd_stage_prepare (waits for the ctx stream)."""
+        t = ApdTiming()
+        self._check(self.lib.apd_get_prepare_timing(self.ctx, C.byref(t)), "apd_get_prepare_timing")
         return t
 
     def profile_reset(self, enable: bool = True):

@@ -3844,6 +3844,7 @@ struct apd_ctx {
     int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
     Args args{};
     bool loaded = false, prepared = false;
+    bool prep_timed = false;       // the prepare events (ev[0..3], ev[14], ev[15]) of the last apd_stage_prepare
     int dw_tile_w = 8;             // DepthToWeak pixel tile width (64 / tile height); APD_DW_TILE_W
     int tile_w = 16;               // sweep list tile width (tile = tile_w x 256/tile_w positions); APD_TILE_W
                                    // (16 x 16: -1 % per C3 iteration against 8 x 32, profiles/r4_ab_tile_shape.txt)
@@ -4016,6 +4017,15 @@ static bool inlier_limit(float D, float t, float *limit) {
     return true;
 }
 
+// Wait for everything the ctx launched, on its stream and on both side streams. A stage that returns
+// early between a fork (RandomInitialization, RANSAC, k_gp_cost on side streams) and its join leaves
+// that work running; every entry point that reuses or frees ctx buffers drains first.
+static void drain(apd_ctx *ctx) {
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto &ss : ctx->side)
+        if (ss) (void)hipStreamSynchronize(ss);
+}
+
 static inline unsigned blocks_for(size_t n, int per_block) { return (unsigned)((n + per_block - 1) / per_block); }
 
 extern "C" {
@@ -4099,7 +4109,7 @@ apd_ctx *apd_create(int32_t device) {
 void apd_destroy(apd_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
+    drain(ctx);
     DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
                       &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
@@ -4131,7 +4141,8 @@ static bool try_ensure(apd_ctx *ctx, DevBuf &b, size_t bytes) {
 int32_t apd_set_problem(apd_ctx *ctx, const apd_problem *pb) {
     if (!ctx || !pb) return APD_EINVAL;
     (void)hipSetDevice(ctx->device);
-    ctx->loaded = ctx->prepared = false;
+    drain(ctx);  // (a previous stage that failed between a fork and its join: its side work reads these buffers)
+    ctx->loaded = ctx->prepared = ctx->prep_timed = false;
     const int W = pb->width, H = pb->height, NI = pb->num_images;
     if (NI > APD_MAX_IMAGES) { ctx->err = "num_images > 32"; return APD_ETOOMANYVIEWS; }
     if (W < 1 || H < 1 || NI < 2 || !pb->images || !pb->cameras) { ctx->err = "bad problem dimensions"; return APD_EINVAL; }
@@ -4604,6 +4615,7 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
     if (ctx->overlap) HIP_OK(ctx, hipStreamWaitEvent(s, ctx->ev_side[0], 0));  // join RandomInitialization
     HIP_OK(ctx, hipMemcpyAsync(ctx->sel.p, ctx->sel2.p, (size_t)a.HW * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     (void)hipEventRecord(ctx->ev[3], s);
+    ctx->prep_timed = true;
     ctx->wcur_fresh = a.wcur != nullptr;
     ctx->prepared = true;
     return APD_OK;
@@ -4780,6 +4792,30 @@ int32_t apd_stage_finish(apd_ctx *ctx) {
     return APD_OK;
 }
 
+// the prepare phase's fields of apd_timing from its events (the ctx stream has passed ev[3]).
+// RandomInitialization runs first after the anchors, beside the lists and the pair table when the
+// ctx overlaps (side stream 0): init_ms is its own duration, lists_ms + pairs_ms the ctx stream's,
+// join_ms the ctx stream's wait for it, and anchors + lists + pairs + join == prepare.
+static void prepare_timing(apd_ctx *ctx, apd_timing &t) {
+    memset(&t, 0, sizeof(t));
+    if (!ctx->prep_timed) return;
+    (void)hipEventElapsedTime(&t.anchors_ms, ctx->ev[0], ctx->ev[1]);
+    (void)hipEventElapsedTime(&t.lists_ms, ctx->ev[1], ctx->ev[14]);
+    (void)hipEventElapsedTime(&t.pairs_ms, ctx->ev[14], ctx->ev[2]);
+    (void)hipEventElapsedTime(&t.join_ms, ctx->ev[2], ctx->ev[3]);
+    (void)hipEventElapsedTime(&t.prepare_ms, ctx->ev[0], ctx->ev[3]);
+    (void)hipEventElapsedTime(&t.init_ms, ctx->ev[1], ctx->ev[15]);
+}
+
+int32_t apd_get_prepare_timing(apd_ctx *ctx, apd_timing *timing) {
+    if (!ctx || !timing) return APD_EINVAL;
+    if (!ctx->prepared) return APD_ESTATE;
+    (void)hipSetDevice(ctx->device);
+    HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+    prepare_timing(ctx, *timing);
+    return APD_OK;
+}
+
 int32_t apd_run_patchmatch(apd_ctx *ctx) {
     if (!ctx || !ctx->loaded) return APD_ESTATE;
     (void)hipSetDevice(ctx->device);
@@ -4796,15 +4832,8 @@ int32_t apd_run_patchmatch(apd_ctx *ctx) {
     (void)hipEventRecord(ctx->ev[13], s);
     HIP_OK(ctx, hipStreamSynchronize(s));
     apd_timing &t = ctx->timing;
-    memset(&t, 0, sizeof(t));
+    prepare_timing(ctx, t);
     (void)hipEventElapsedTime(&t.total_ms, ctx->ev[0], ctx->ev[13]);
-    (void)hipEventElapsedTime(&t.anchors_ms, ctx->ev[0], ctx->ev[1]);
-    // RandomInitialization runs first after the anchors, beside the lists and the pair table when
-    // the ctx overlaps (side stream 0): init_ms is its own duration, lists_ms + pairs_ms the ctx
-    // stream's, and their sum can exceed the bracket; ev[2] -> ev[3] (the join) is not reported
-    (void)hipEventElapsedTime(&t.lists_ms, ctx->ev[1], ctx->ev[14]);
-    (void)hipEventElapsedTime(&t.pairs_ms, ctx->ev[14], ctx->ev[2]);
-    (void)hipEventElapsedTime(&t.init_ms, ctx->ev[1], ctx->ev[15]);
     (void)hipEventElapsedTime(&t.sweep_ms, ctx->ev[3], ctx->ev[12]);
     (void)hipEventElapsedTime(&t.post_ms, ctx->ev[12], ctx->ev[13]);
     const int ni = std::min(iters, 8);
@@ -4952,7 +4981,7 @@ int32_t apd_device_free(apd_ctx *ctx, void *ptr) {
     if (!ctx) return APD_EINVAL;
     (void)hipSetDevice(ctx->device);
     if (ptr) {
-        HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+        drain(ctx);
         HIP_OK(ctx, hipFree(ptr));
     }
     return APD_OK;

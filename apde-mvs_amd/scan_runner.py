@@ -156,24 +156,25 @@ class Exchange:
         return int(self.store.add(key, 1)) - 1
 
     def all_gather_state(self, mine: Dict[int, "object"], meta: Dict[int, float], h: int, w: int):
-        """Every rank's new view states ([6, h, w] float32: depth, normal xyz, weak, confidence) to every
-        rank, on the device with RCCL when the ranks run on GPUs (no host round trip), plus the views'
-        measured times for the next pass's queue order."""
+        """Every rank's new view states to every rank, on the device with RCCL when the ranks run on GPUs
+        (no host round trip), plus the views' measured times for the next pass's queue order. On the
+        wire a state is WIRE_BYTES_PER_PX = 18 B/px (wire_pack: depth + normal xyz as f32, pixel state
+        + confidence as u8) instead of the [6, h, w] f32 it is held as (24 B/px)."""
         torch, dist = self.torch, self.dist
         ids = sorted(mine)
         lists = [None] * self.world
         dist.all_gather_object(lists, [(v, meta[v]) for v in ids])
         kmax = max(1, max(len(l) for l in lists))
         dev = self.device or "cpu"
-        buf = torch.zeros((kmax, 6, h, w), dtype=torch.float32, device=dev)
+        buf = torch.zeros((kmax, wire_bytes(h, w)), dtype=torch.uint8, device=dev)
         for k, v in enumerate(ids):
-            buf[k] = mine[v]
+            buf[k] = wire_pack(mine[v])
         outs = [torch.empty_like(buf) for _ in range(self.world)]
         dist.all_gather(outs, buf)
         states, times = {}, {}
         for r in range(self.world):
             for k, (v, t) in enumerate(lists[r]):
-                states[v] = outs[r][k]
+                states[v] = wire_unpack(outs[r][k], h, w)
                 times[v] = t
         return states, times
 
@@ -184,6 +185,36 @@ class Exchange:
 def _pack(depth, normal, weak, conf):
     import torch
     return torch.cat([depth[None], normal.permute(2, 0, 1), weak[None].float(), conf[None].float()], 0)
+
+
+WIRE_BYTES_PER_PX = 4 * 4 + 2  # depth + normal xyz (f32), pixel state + confidence (u8)
+
+
+def wire_bytes(h: int, w: int) -> int:
+    """Bytes of one packed state, padded to 16 so that every state of a [k, wire_bytes] buffer starts
+    4-byte aligned (its f32 planes are viewed in place)."""
+    return (WIRE_BYTES_PER_PX * h * w + 15) // 16 * 16
+
+
+def wire_pack(state):
+    """A [6, h, w] f32 view state as the exchange's flat u8 buffer: the four f32 planes' bytes, then
+    the pixel state and confidence planes as u8 (they hold small integers: exact both ways)."""
+    import torch
+    h, w = state.shape[-2], state.shape[-1]
+    out = torch.zeros(wire_bytes(h, w), dtype=torch.uint8, device=state.device)
+    n = 16 * h * w
+    out[:n] = state[:4].contiguous().view(torch.uint8).reshape(-1)
+    out[n:n + 2 * h * w] = state[4:6].to(torch.uint8).reshape(-1)
+    return out
+
+
+def wire_unpack(buf, h: int, w: int):
+    """Inverse of wire_pack: the [6, h, w] f32 view state, bit-identical to the packed one."""
+    import torch
+    n = 4 * h * w
+    f = buf[:4 * n].view(torch.float32).reshape(4, h, w)
+    u = buf[4 * n:4 * n + 2 * h * w].reshape(2, h, w).float()
+    return torch.cat([f, u], 0)
 
 
 def run_scan(folder: str, run_fn: Callable, rank: int = 0, world: int = 1, exchange: Optional[Exchange] = None,

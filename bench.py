@@ -78,9 +78,27 @@ def workload_name(W, H, N, apd):
     return known.get((W, H, N, apd), "custom")
 
 
+KERNEL_SOURCES = ("apde-mvs_amd/csrc/apd_kernels.hip", "apde-mvs_amd/csrc/apd_device.h")
+
+
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) of the kernel sources libapd_hip.so is built from: a PMC summary
+    carries the hash of the sources it was collected with (tools/pmc_c3.sh), and only a summary whose
+    hash matches the tree's is taken as this build's traffic."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(REPO, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def latest_pmc(kernel: str, W: int, n_src: int):
-    """The newest (by round/session file name) PMC summary under profiles/ for this kernel and shape.
-    Other PMC files (counter studies of other shapes or blocks) are skipped, not taken as the latest."""
+    """The PMC summary under profiles/ for this kernel and shape collected from THIS build's kernel
+    sources (its source_hash equals source_hash()), or None: a summary of another build (a superseded
+    variant, an older round) is never reported as the current traffic. Among matching files the
+    newest by name wins. Counter studies of other shapes are skipped."""
+    want = source_hash()
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
         try:
             pmc = json.load(open(f))
@@ -88,7 +106,7 @@ def latest_pmc(kernel: str, W: int, n_src: int):
             continue
         if (isinstance(pmc, dict) and str(pmc.get("kernel", "")).startswith(kernel)
                 and pmc.get("width") == W and pmc.get("n_src") == n_src
-                and pmc.get("hbm_bytes_per_launch") is not None):
+                and pmc.get("hbm_bytes_per_launch") is not None and pmc.get("source_hash") == want):
             pmc["_file"] = os.path.relpath(f, REPO)
             return pmc
     return None
@@ -146,12 +164,18 @@ def final_round_problem(sc, priors, ref, N, sa=False):
     return arr
 
 
-def timed_fresh_iterations(eng, arr, steps, warmup, barrier, exchange=None):
+def timed_fresh_iterations(eng, arr, steps, warmup, barrier, exchange=None, exchange_every=1):
     """Warm-up, then `steps` loop-body iterations taken in blocks of one fresh run's iterations
     0..max_iterations-1; each block re-uploads and re-initialises the problem untimed, and is timed
-    between a barrier + device synchronisation on both sides. `exchange` (N > 1): the pass's
-    all-gather of the view states, run at the end of every block inside the timed region.
-    Returns (summed seconds, per-step ms)."""
+    between a barrier + device synchronisation on both sides. `exchange(k)` (N > 1): the pass's
+    all-gather of the k view states a rank produced since the last one, run inside the timed region
+    after every `exchange_every` blocks (a scan pass: ceil(views / ranks) problems per rank, then one
+    all-gather, scan_runner.py) and after the last block.
+    The per-pass pair table (built in apd_stage_prepare: it replaces candidate work the reference
+    does inside every CheckerboardPropagationWeak, APD.cu:1442-1615) is charged to the iterations:
+    each block adds its own build's device time (apd_get_prepare_timing().pairs_ms, HIP events)
+    times n / max_iterations for the n iterations it times.
+    Returns (summed seconds incl. the charged pair tables, per-step ms, charged pair-table ms)."""
     iters = max(1, arr.params.max_iterations)
     done = 0
     while done < warmup:
@@ -163,11 +187,12 @@ def timed_fresh_iterations(eng, arr, steps, warmup, barrier, exchange=None):
         done += n
     eng.synchronize()
     eng.profile_reset(True)
-    elapsed, step_ms, done = 0.0, [], 0
+    elapsed, step_ms, done, pairs_ms, pending = 0.0, [], 0, 0.0, 0
     while done < steps:
         eng.set_problem(arr)
         eng.prepare()
         eng.synchronize()
+        pairs_ms += eng.prepare_timing().pairs_ms * min(iters, steps - done) / iters
         barrier()
         t_block = time.perf_counter()
         t_prev = t_block
@@ -178,13 +203,15 @@ def timed_fresh_iterations(eng, arr, steps, warmup, barrier, exchange=None):
             t = time.perf_counter()
             step_ms.append((t - t_prev) * 1e3)
             t_prev = t
-        if exchange is not None:
-            exchange()
+        pending += 1
+        if exchange is not None and (pending == exchange_every or done + n >= steps):
+            exchange(pending)
+            pending = 0
             t_prev = time.perf_counter()
         elapsed += t_prev - t_block
         barrier()
         done += n
-    return elapsed, step_ms
+    return elapsed + pairs_ms * 1e-3, step_ms, pairs_ms
 
 
 def kernel_stats(eng, kind):
@@ -342,11 +369,13 @@ def apd_pass_once(eng, sc, ref, N, label, sa=False):
     ids = [ref] + [j for j, _ in sc.pairs[ref]][:N]
     priors = first_init_priors(eng, sc, ids, N)
     arr = final_round_problem(sc, priors, ref, N, sa=sa)
-    el, step_ms = timed_fresh_iterations(eng, arr, arr.params.max_iterations, 1, lambda: None)
+    el, step_ms, pairs = timed_fresh_iterations(eng, arr, arr.params.max_iterations, 1, lambda: None)
     roof = weak_roofline(eng, len(step_ms), W, N)
     eng.profile_reset(False)
     e2e = end_to_end(eng, arr, sc, ref, W, H, N)
     r = {"workload": label, "mpix_s_iter": round(W * H * len(step_ms) / el / 1e6, 3),
+         "mpix_s_iter_loop": round(W * H * len(step_ms) / (el - pairs * 1e-3) / 1e6, 3),
+         "pairs_ms_charged": round(pairs, 3),
          "iter_ms": [round(x, 2) for x in step_ms], "weak_frac": round(float((arr.weak_info == 0).mean()), 4),
          "roofline_frac": roof["frac"], "roofline_achieved": roof["achieved"],
          "launch_avg_ms": roof["launch_avg_ms"], "end_to_end": e2e}
@@ -361,7 +390,7 @@ def c2_first_init(eng, steps, warmup):
     W, H, N = 3024, 2016, 8
     sc = make_scene(W, H, N, 1, "smooth")
     arr = A.scene_problem(sc, 0, [j for j, _ in sc.pairs[0]][:N], seed=0x5EED)
-    el, step_ms = timed_fresh_iterations(eng, arr, steps, warmup, lambda: None)
+    el, step_ms, _ = timed_fresh_iterations(eng, arr, steps, warmup, lambda: None)
     roof = strong_roofline(eng, W, N)
     eng.profile_reset(False)
     e2e = end_to_end(eng, arr, sc, 0, W, H, N)
@@ -418,30 +447,35 @@ def self_launch_cmd(argv, gpus, env):
             "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
 
 
-def state_exchange(tdist, torch, state, world):
-    """The scan runner's per-pass step (scan_runner.Exchange.all_gather_state): every
-    rank's new view state [6, H, W] fp32 to every rank, device to device (RCCL over xGMI; gloo in the
-    one-GPU rehearsal). Returns (exchange, timed): exchange() runs one all-gather and waits for it;
-    timed(reps) is the median ms of `reps` all-gathers, each after a barrier (the collective alone,
-    without the ranks' load imbalance)."""
-    outs = [torch.empty_like(state) for _ in range(world)]
+def state_exchange(tdist, torch, state, world, kmax=1):
+    """The scan runner's per-pass step (scan_runner.Exchange.all_gather_state): the k view
+    states each rank produced to every rank, in the exchange's wire format (scan_runner.wire_pack:
+    18 B/px, depth + normal f32, pixel state + confidence u8), device to device (RCCL over xGMI; gloo
+    in the one-GPU rehearsal). Buffers for up to kmax states per rank are allocated here, outside the
+    timed region. Returns (exchange, timed, wire_bytes): exchange(k) runs one all-gather of k states
+    per rank and waits for it; timed(reps, k) is the median ms of `reps` all-gathers, each after a
+    barrier (the collective alone, without the ranks' load imbalance)."""
+    import scan_runner
+    wire = scan_runner.wire_pack(state)
+    buf = wire.unsqueeze(0).repeat(kmax, 1).contiguous()
+    outs = [torch.empty_like(buf) for _ in range(world)]
 
-    def exchange():
-        tdist.all_gather(outs, state)
-        if state.is_cuda:
+    def exchange(k=1):
+        tdist.all_gather([o[:k] for o in outs], buf[:k])
+        if buf.is_cuda:
             torch.cuda.synchronize()
 
-    def timed(reps):
+    def timed(reps, k=1):
         ms = []
         for _ in range(reps):
             tdist.barrier()
-            if state.is_cuda:
+            if buf.is_cuda:
                 torch.cuda.synchronize()
             t0 = time.perf_counter()
-            exchange()
+            exchange(k)
             ms.append((time.perf_counter() - t0) * 1e3)
         return statistics.median(ms)
-    return exchange, timed
+    return exchange, timed, int(wire.numel())
 
 
 def main():
@@ -459,6 +493,9 @@ def main():
     ap.add_argument("--c2", type=int, default=1, help="also measure configs[1] (C2 FIRST_INIT) (0/1)")
     ap.add_argument("--rich", type=int, default=1, help="also measure the texture-rich scene variant (0/1)")
     ap.add_argument("--sa", type=int, default=1, help="also measure the headline pass with SA labels (C5's pass) (0/1)")
+    ap.add_argument("--scan-views", type=int, default=26,
+                    help="views of the modelled scan (ETH3D office: 26): at N > 1 every rank runs "
+                         "ceil(views / N) problems per pass, then the pass's all-gather")
     args = ap.parse_args()
     t_start_all = time.time()
     cmd = self_launch_cmd(sys.argv[1:], args.gpus, os.environ)
@@ -514,6 +551,7 @@ def main():
     weak_frac = float((arr.weak_info == A.WEAK).mean())
 
     exchange = exchange_timed = None
+    per_rank = max(1, -(-args.scan_views // world))
     if dist:
         # this rank's view state as the scan runner packs it (depth, normal xyz, state, confidence),
         # from a finished run of its problem, on its device
@@ -524,36 +562,46 @@ def main():
         o = eng.results_device(W, H, f"cuda:{device}")
         state = scan_runner._pack(o.planes[..., 3], o.planes[..., :3], o.weak_info, o.confidence).contiguous()
         del o
-        exchange, exchange_timed = state_exchange(tdist, torch, state, world)
-        exchange()  # (first use: communicator setup out of the timed region)
-    elapsed, step_ms = timed_fresh_iterations(eng, arr, args.steps, args.warmup, barrier, exchange)
+        exchange, exchange_timed, wire_bytes = state_exchange(tdist, torch, state, world, per_rank)
+        exchange(per_rank)  # (first use: communicator setup out of the timed region)
+    elapsed, step_ms, pairs_ms = timed_fresh_iterations(eng, arr, args.steps, args.warmup, barrier, exchange, per_rank)
     roof = weak_roofline(eng, args.steps, W, N)
     roof_strong_apd = strong_roofline(eng, W, N)
     eng.profile_reset(False)
     exch = None
     if dist:
         torch, tdist, backend = dist
-        ex_ms = exchange_timed(5)
+        ex_ms = exchange_timed(5, per_rank)
         dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-        mine = torch.tensor([elapsed, statistics.median(step_ms), ex_ms], dtype=torch.float64, device=dev)
+        mine = torch.tensor([elapsed, statistics.median(step_ms), ex_ms, pairs_ms], dtype=torch.float64, device=dev)
         every = [torch.zeros_like(mine) for _ in range(world)]
         tdist.all_gather(every, mine)
         every = [e.cpu().tolist() for e in every]
         elapsed = max(e[0] for e in every)
+        loop_elapsed = max(e[0] - e[3] * 1e-3 for e in every)
         blocks = -(-args.steps // max(1, arr.params.max_iterations))
         exch = {"exchange_ms": round(max(e[2] for e in every), 3),
-                "exchange_bytes_per_rank": int(state.numel() * state.element_size()),
-                "exchanges_in_timed_region": blocks,
+                "exchange_bytes_per_rank": wire_bytes,
+                "exchange_bytes_per_px": scan_runner.WIRE_BYTES_PER_PX,
+                "problems_per_rank_per_exchange": per_rank,
+                "exchange_ms_basis": f"all-gather of {per_rank} states per rank",
+                "exchanges_in_timed_region": -(-blocks // per_rank),
                 "exchange_backend": backend,
                 "rank_ms_per_step": [round(e[0] / args.steps * 1e3, 3) for e in every],
                 "rank_iter_ms_median": [round(e[1], 3) for e in every],
-                "note": "one all-gather of the [6, H, W] fp32 view states per block of fresh iterations (one "
-                        "pass's loop body) inside the timed region, as scan_runner.py ends every pass; "
-                        "exchange_ms = median of 5 barrier-separated all-gathers, max over ranks"}
+                "note": "a scan pass on N ranks: every rank runs ceil(scan_views / N) problems (blocks of "
+                        "fresh iterations), then one all-gather of their states (18 B/px wire format) inside "
+                        "the timed region, as scan_runner.py ends every pass; exchange_ms = median of 5 "
+                        "barrier-separated all-gathers of that many states, max over ranks"}
         del state
 
     n_gpus = world if dist else 1
+    if not dist:
+        loop_elapsed = elapsed - pairs_ms * 1e-3
+    # the headline charges each pass's pair table to its iterations (timed_fresh_iterations);
+    # the bare loop body is reported beside it
     value = n_gpus * W * H * args.steps / elapsed / 1e6
+    value_loop = n_gpus * W * H * args.steps / loop_elapsed / 1e6
 
     line = None
     if rank == 0:
@@ -599,10 +647,13 @@ def main():
                        "width": W, "height": H, "n_src": N, "texture": args.texture,
                        "weak_frac": round(weak_frac, 4), "global_batch": n_gpus,
                        "parallelism": f"views{n_gpus}"},
-            # the per-pass pair table spread over the pass's 3 iterations; pairs_ms is its bracket on the
-            # ctx stream with RandomInitialization running beside it, an upper bound of its cost
-            "mpix_s_iter_amortised": (round(W * H / (elapsed / args.steps + e2e["pairs_ms"] * 1e-3 / 3) / 1e6 * n_gpus, 3)
-                                      if e2e else None),
+            # `value` includes each pass's pair-table build (its HIP-event bracket on the ctx stream,
+            # with RandomInitialization running beside it on a side stream: an upper bound of its
+            # cost) spread over the pass's iterations; the loop body alone:
+            "mpix_s_iter_loop": round(value_loop, 3),
+            "pairs_ms_per_pass": round(pairs_ms / args.steps * max(1, arr_iters()), 3),
+            "value_basis": "W*H*steps*n_gpus / (timed loop-body iterations + each pass's pair-table build "
+                           "charged per iteration, max over ranks)",
             "multi_gpu": exch,
             "iter_ms_median": round(statistics.median(step_ms), 3),
             "iter_ms": [round(x, 2) for x in step_ms],
@@ -630,6 +681,10 @@ def main():
 
 def arr_rt():
     return min(2 ** FINAL_ROUND, 4)
+
+
+def arr_iters():
+    return 3  # main.h:80 max_iterations (the final round's REFINE_ITER pass)
 
 
 if __name__ == "__main__":

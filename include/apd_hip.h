@@ -41,7 +41,8 @@
 extern "C" {
 #endif
 
-#define APD_ABI_VERSION 2  /* 2: apd_timing.lists_ms / pairs_ms, 9 profiling counters, kinds 4-7 */
+#define APD_ABI_VERSION 3  /* 2: apd_timing.lists_ms / pairs_ms, 9 profiling counters, kinds 4-7;
+                                  3: apd_timing.join_ms / prepare_ms, apd_get_prepare_timing */
 #define APD_MAX_IMAGES 32          /* main.h:40  MAX_IMAGES            */
 #define APD_ANCHOR_NUM 9           /* main.h:41  ANCHOR_NUM            */
 #define APD_MAX_SEARCH_RADIUS 4096 /* main.h:42  MAX_SEARCH_RADIUS     */
@@ -152,8 +153,15 @@ typedef struct apd_timing {
     float iter_ms[8];          /* per-iteration sweep time (first 8 iterations)             */
     int32_t iterations;
     float lists_ms;            /* the sweeps' pixel lists (after NeigbourUpdate)            */
-    float pairs_ms;            /* the Weak candidates' image-wide pair table (APD passes)   */
-    /* total_ms == anchors_ms + lists_ms + pairs_ms + init_ms + sweep_ms + post_ms           */
+    float pairs_ms;            /* the Weak candidates' image-wide pair table (APD passes) and
+                                  the anchor-window records it reads                         */
+    float join_ms;             /* the wait for RandomInitialization after the pair table    */
+    float prepare_ms;          /* apd_stage_prepare's bracket: anchors .. join               */
+    /* Serial ctx (APD_NO_OVERLAP=1): total_ms == anchors_ms + lists_ms + pairs_ms + init_ms
+       + sweep_ms + post_ms. Overlapped (default): RandomInitialization runs on a side stream from
+       the end of the anchors, so prepare_ms == anchors_ms + lists_ms + pairs_ms + join_ms and
+       total_ms == prepare_ms + sweep_ms + post_ms; init_ms is then RandomInitialization's own
+       span, overlapping lists_ms + pairs_ms. */
 } apd_timing;
 
 typedef struct apd_ctx apd_ctx;
@@ -198,6 +206,11 @@ int32_t apd_get_results(apd_ctx *ctx, const apd_outputs *out);
 
 /* Device timing of the last apd_run_patchmatch. */
 int32_t apd_get_timing(apd_ctx *ctx, apd_timing *timing);
+
+/* The prepare-phase fields (anchors_ms, lists_ms, pairs_ms, init_ms, join_ms, prepare_ms) of the
+   last apd_stage_prepare, whether or not apd_run_patchmatch ran it; the other fields are zero.
+   Waits for the ctx stream. bench.py charges pairs_ms to the iterations of a staged pass. */
+int32_t apd_get_prepare_timing(apd_ctx *ctx, apd_timing *timing);
 
 /* Profiling of the loop-body kernels (APD.cu:2699-2708), used by bench.py for roofline.achieved.
    apd_profile_reset(ctx, 1) clears and enables it: every later launch of the kinds below is

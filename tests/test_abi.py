@@ -37,7 +37,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_abi_version(lib):
-    assert lib.apd_abi_version() == 2
+    assert lib.apd_abi_version() == 3
 
 
 def test_no_device_is_an_error_not_a_crash(lib):

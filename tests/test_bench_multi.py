@@ -50,10 +50,12 @@ def test_state_exchange_gloo_cpu():
         port = s_.getsockname()[1]
     tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     try:
-        st = torch.arange(6 * 4 * 5, dtype=torch.float32).reshape(6, 4, 5)
-        ex, timed = bench.state_exchange(tdist, torch, st, 1)
-        ex()
-        assert timed(2) >= 0.0
+        st = torch.arange(6 * 4 * 8, dtype=torch.float32).reshape(6, 4, 8)
+        ex, timed, nbytes = bench.state_exchange(tdist, torch, st, 1, kmax=3)
+        assert nbytes == 18 * 4 * 8  # (a multiple of 16 already: no row padding)
+        ex(3)
+        ex(1)
+        assert timed(2, 2) >= 0.0
     finally:
         tdist.destroy_process_group()
 
@@ -75,4 +77,6 @@ def test_bench_two_ranks_self_launch():
     assert line["n_gpus"] == 2 and line["value"] > 0
     mg = line["multi_gpu"]
     assert mg["exchange_ms"] > 0 and len(mg["rank_ms_per_step"]) == 2
-    assert mg["exchange_bytes_per_rank"] == 6 * 378 * 252 * 4
+    # the 18 B/px wire format (scan_runner.wire_pack), ceil(26 views / 2 ranks) problems per exchange
+    assert mg["exchange_bytes_per_rank"] == 18 * 378 * 252 and mg["exchange_bytes_per_px"] == 18
+    assert mg["problems_per_rank_per_exchange"] == 13 and mg["exchanges_in_timed_region"] == 1

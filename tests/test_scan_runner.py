@@ -127,3 +127,25 @@ def test_nearest_index_equals_host_resize():
         ref = host.resize_nearest(idx, dw, dh)
         yo, xo = SR.nearest_index(sw, sh, dw, dh)
         assert np.array_equal(idx[yo][:, xo], ref)
+
+
+def test_wire_format_round_trip():
+    """The exchange's 18 B/px wire format (scan_runner.wire_pack): bit-identical round trip of a
+    [6, h, w] state whose planes 4-5 hold u8 values, at odd sizes and as the k-th row of a [k, bytes]
+    gather buffer (16-byte row padding keeps the f32 view aligned)."""
+    import sys
+    import torch
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "apde-mvs_amd"))
+    import scan_runner as SR
+    g = torch.Generator().manual_seed(5)
+    for h, w in [(5, 7), (1, 1), (33, 17), (64, 48)]:
+        st = torch.randn(6, h, w, generator=g)
+        st[0, 0, 0] = float("nan")
+        st[1, -1, -1] = -0.0
+        st[4] = torch.randint(0, 3, (h, w), generator=g).float()
+        st[5] = torch.randint(0, 256, (h, w), generator=g).float()
+        assert SR.wire_bytes(h, w) % 16 == 0 and SR.wire_bytes(h, w) >= 18 * h * w
+        buf = torch.stack([SR.wire_pack(st * 0), SR.wire_pack(st), SR.wire_pack(st)])
+        for k in (1, 2):
+            back = SR.wire_unpack(buf[k], h, w)
+            assert torch.equal(back.view(torch.int32), st.view(torch.int32))

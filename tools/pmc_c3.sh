@@ -8,6 +8,9 @@ OUT=${1:-gpurun_out/pmc_c3}
 RE=${2:-"k_sweep_weak_vm|k_weak_cand_g|k_gp_cost"}
 EXTRA="${*:3}"
 mkdir -p "$OUT"
+# the kernel sources' hash at collection time (bench.py source_hash): tools/pmc_json.py stores it in the
+# summary, and bench.py reports the summary's traffic only while the tree still has these sources
+python3 -c "import bench; print(bench.source_hash())" > "$OUT/source_hash"
 export TMPDIR=/tmp
 CMD="python3 bench.py --steps 3 --warmup 0 --no-cpu-baseline --end-to-end 0 --c2 0 --rich 0 --sa 0 $EXTRA"
 i=0

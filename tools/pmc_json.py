@@ -15,6 +15,8 @@ ap.add_argument("--height", type=int, default=2016)
 ap.add_argument("--n-src", type=int, default=8)
 ap.add_argument("--stats")
 ap.add_argument("--last", type=int, default=0, help="only the last N dispatches of the kernel (e.g. the APD pass after its FIRST_INIT priors)")
+ap.add_argument("--source-hash", help="kernel-source hash of the profiled build (default: <src>/source_hash, "
+                                      "written by tools/pmc_c3.sh at collection time)")
 ap.add_argument("--source", default="rocprofv3 --pmc, one pass per counter group (tools/pmc_profile.sh), "
                                     "bench.py --steps 2 --warmup 1")
 a = ap.parse_args()
@@ -60,6 +62,10 @@ if a.stats:
     for r in csv.DictReader(open(a.stats)):
         if a.kernel in r["Name"]:
             out["rocprof_avg_launch_ns"] = float(r["AverageNs"])
+sh = a.source_hash
+if sh is None and os.path.exists(os.path.join(a.src, "source_hash")):
+    sh = open(os.path.join(a.src, "source_hash")).read().strip()
+out["source_hash"] = sh  # bench.py latest_pmc reports this summary only while it equals bench.source_hash()
 out["source"] = a.source
 json.dump(out, open(a.dst, "w"), indent=1)
 print(json.dumps(out, indent=1))
