@@ -17,8 +17,8 @@ import synth
 
 
 @functools.lru_cache(maxsize=None)
-def scene(w=160, h=120, n_src=4, seed=20251114, weak=True, texture="smooth"):
-    return synth.make_scene(w, h, n_src, seed=seed, weak_patches=weak, texture=texture)
+def scene(w=160, h=120, n_src=4, seed=20251114, weak=True, texture="smooth", texture_scale=1.0):
+    return synth.make_scene(w, h, n_src, seed=seed, weak_patches=weak, texture=texture, texture_scale=texture_scale)
 
 
 def base_problem(sc, ref=0, n_src=None, **params):
@@ -113,6 +113,10 @@ CASES = {
     "refine_iter_sa_n10_apd_geom_rt4": (144, 88, 10, "apd_geom_sa_rt4"),
     # config C1 (BASELINE configs[0]): 640x480, 1 ref + 4 src views, 2 iterations, FIRST_INIT
     "c1_first_n4_iter2": (640, 480, 4, "first_c1"),
+    # the headline's exact parameter set (bench.py final_round_problem, main.cpp:336-352 with i = 3,
+    # j = 0, ETH3D): REFINE_ITER, APD + focal + geom (geom_factor 0.2, main.cpp:297) + impetus, N = 10,
+    # rotate_time 4, ransac_threshold 0.00625, weak_peak_radius 4, no SA
+    "refine_iter_eth3d_final_n10": (240, 160, 10, "apd_geom_final"),
 }
 
 
@@ -124,10 +128,26 @@ def c5_final_pass(sc, priors, n, ref=0):
                           rotate_time=4, ransac_threshold=0.01 - 3 * 0.00125, weak_peak_radius=4)
 
 
-def make_case(name, oracle_run):
+def headline_pass(sc, priors, n, ref=0):
+    """bench.py's headline pass: main.cpp's last round (i = 3), first geometric pass (j = 0) of an ETH3D
+    scan without SA masks (main.cpp:336-352): rotate_time min(2^3, 4), ransac_threshold 0.01 - 3 *
+    0.00125, weak_peak_radius max(4 - 2 j, 2), impetus on, geom_factor 0.2 (main.cpp:297)."""
+    return refine_problem(sc, priors, ref, n, state=A.REFINE_ITER, geom=True, apd=True, rotate_time=4,
+                          ransac_threshold=0.01 - 3 * 0.00125, weak_peak_radius=4, use_impetus=1, geom_factor=0.2)
+
+
+def case_scene(name):
     w, h, n, kind = CASES[name]
     rich = kind.endswith("_rich")
-    sc = scene(w, h, max(n, 4), texture="rich" if rich else "smooth")
+    # the headline-parameter case renders C3's texture per pixel (synth texture_scale = 6048 / w), so
+    # that most of its pixels are WEAK as at C3 (bench.py cpu_baseline samples the same way)
+    ts = 6048.0 / w if kind == "apd_geom_final" else 1.0
+    return scene(w, h, max(n, 4), texture="rich" if rich else "smooth", texture_scale=ts)
+
+
+def make_case(name, oracle_run):
+    w, h, n, kind = CASES[name]
+    sc = case_scene(name)
     if kind in ("first", "first_rich"):
         return base_problem(sc, 0, n)
     if kind == "first_c1":
@@ -150,6 +170,8 @@ def make_case(name, oracle_run):
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, sa="zero_band")
     if kind == "apd_geom_sa_rt4":
         return c5_final_pass(sc, priors, n)
+    if kind == "apd_geom_final":
+        return headline_pass(sc, priors, n)
     if kind == "apd_geom_rt4":
         return refine_problem(sc, priors, 0, n, state=A.REFINE_ITER, geom=True, apd=True, rotate_time=4)
     if kind in ("apd_geom", "apd_geom_rich"):

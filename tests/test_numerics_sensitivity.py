@@ -39,7 +39,25 @@ def test_fastmath_variant_builds_and_differs():
 def test_summary_shape():
     rec = {"pass": {"depth_within_1e-3_rel_frac": 0.8, "depth_bit_identical_frac": 0.2, "validity_mask_identical": True,
                     "validity_mask_agree_frac": 1.0, "pixel_state_identical": False, "pixel_state_agree_frac": 0.99,
-                    "selected_views_agree_frac": 0.95}}
+                    "selected_views_agree_frac": 0.95, "depth_in_range_identical": True}}
     s = NS.summary([rec, rec])
     assert s["pass"]["cases"] == 2 and s["pass"]["validity_mask_identical_cases"] == 2
     assert np.isclose(s["pass"]["depth_within_1e-3_rel_frac_median"], 0.8)
+
+
+def test_validity_mask_is_baselines_definition():
+    """validity_mask_* is BASELINE.md §2's mask, depth > 0 and pixel state != UNKNOWN after the epilogue:
+    a pixel whose state alone differs (UNKNOWN in one build, depth in range in both) breaks it, while
+    depth_in_range_* (depth > 0 alone) does not see it."""
+    import copy
+    R = NS.Runner(4)
+    arr = cases.make_case("first_n4", R.run_c)
+    c = R.run_c(arr)
+    f = copy.deepcopy(c)
+    d, _, w = cases.epilogue(c, arr.params.depth_min, arr.params.depth_max)
+    idx = np.argwhere((d > 0) & (w != 2))[:5]
+    for y, x in idx:
+        f.weak_info[y, x] = 2  # UNKNOWN
+    m = NS.metrics(c, f, arr)
+    assert m["depth_in_range_identical"] and not m["validity_mask_identical"]
+    assert m["validity_mask_differing_pixels"] == len(idx) == 5
