@@ -2686,19 +2686,23 @@ __global__ __launch_bounds__(BLOCK) void k_gp_tasks(const int *__restrict__ off,
 // One workgroup per window anchor q (tasks[]): its references, in batches of GP_CHUNK, insert their
 // candidate anchors into an LDS hash (keys qh + 1), sized from the reference count; a table that
 // reaches GP_HS / 2 keys after a batch is closed (a new run of pairs for q starts, so an anchor with
-// more than ~4 k distinct candidates repeats a few pairs). Pass 0 counts the distinct pairs per
-// anchor (acnt); pass 1, from the scanned bases, writes each closed table's pairs (plist, slot order)
-// and then every (pixel, candidate, window) slot of the table's references (pidx).
+// more than ~4 k distinct candidates repeats a few pairs). Each closed table writes its pairs (plist,
+// slot order) and then every (pixel, candidate, window) slot of the table's references (pidx).
+// PASS 2 (the default, one pass): a closed table reserves its range of plist with one atomic on a
+// global counter (acnt[0]); ranges past `pcap` entries are not written, and the host, seeing the
+// counter above pcap, builds the table again with the two passes. PASS 0 counts the distinct pairs
+// per anchor (acnt) and PASS 1 writes them from the scanned bases (abase): the fallback, and the
+// path APD_GP_TWO_PASS=1 forces. Pair ids are labels either way: the costs never depend on them.
 template <int PASS>
 __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__restrict__ tasks, const int *__restrict__ off,
                                                        const uint32_t *__restrict__ refs, const uint8_t *__restrict__ cbw,
                                                        int *__restrict__ acnt,
                                                        const int *__restrict__ abase, int2 *__restrict__ plist,
-                                                       uint32_t *__restrict__ pidx) {
+                                                       uint32_t *__restrict__ pidx, int pcap) {
     __shared__ uint32_t hs[GP_HS];
     __shared__ uint16_t sid[GP_HS];
     __shared__ int scan_w[GP_CHUNK / WAVE + 1];
-    __shared__ int nfresh;
+    __shared__ int nfresh, sbase;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid >> 6;
     const int q = tasks[blockIdx.x];
     const int r0 = off[q], n = off[q + 1] - r0;
@@ -2726,7 +2730,7 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
     for (int i = tid; i < cap; i += GP_CHUNK) hs[i] = 0u;
     if (tid == 0) nfresh = 0;
     __syncthreads();
-    int base = PASS ? abase[blockIdx.x] : 0, total = 0;
+    int base = PASS == 1 ? abase[blockIdx.x] : 0, total = 0;
     int run0 = 0;  // first reference of the open table
     for (int b0 = 0; b0 < n; b0 += GP_CHUNK) {
         const int r = b0 + tid;
@@ -2755,7 +2759,12 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
         __syncthreads();
         const bool close = nd >= GP_CLOSE || b0 + GP_CHUNK >= n;
         if (!close) continue;  // (uniform)
-        if (PASS == 1) {
+        if (PASS == 2) {
+            if (tid == 0) sbase = atomicAdd(acnt, nd);
+            __syncthreads();
+            base = sbase;
+        }
+        if (PASS >= 1) {
             // plist[base + id] = (window anchor, candidate anchor)
             const int per = cap / GP_CHUNK;  // slots per thread (cap >= GP_CHUNK)
             const int s0 = tid * per, s1 = s0 + per;
@@ -2777,7 +2786,8 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
                 const uint32_t key = hs[sl];
                 if (!key) continue;
                 // (window anchor x | SA-filtered << 15 | y << 16, candidate anchor position)
-                plist[base + next] = make_int2(qx | ((key & GP_FILT) ? 0x8000 : 0) | (qy << 16), (int)((key & ~GP_FILT) - 1u));
+                if (PASS == 1 || base + next < pcap)
+                    plist[base + next] = make_int2(qx | ((key & GP_FILT) ? 0x8000 : 0) | (qy << 16), (int)((key & ~GP_FILT) - 1u));
                 sid[sl] = (uint16_t)next;
                 ++next;
             }
@@ -2801,7 +2811,7 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
             }
             __syncthreads();
         }
-        base += nd;
+        if (PASS != 2) base += nd;
         total += nd;
         run0 = b0 + GP_CHUNK;
         for (int i = tid; i < cap; i += GP_CHUNK) hs[i] = 0u;
@@ -3855,6 +3865,8 @@ struct apd_ctx {
     bool rec_on = false;           // the anchor-window records of the prepared problem are built (k_anchor_rec)
     bool dtex = true;              // DepthToWeak over pre-differenced fp16 texels (FastTexD); APD_NO_DTEX=1 disables
     int gp_np = 0;                 // its distinct pairs
+    bool gp_one_pass = true;       // k_gp_dedup in one pass (atomic plist ranges); APD_GP_TWO_PASS=1: count + write
+    int gp_cap_factor = 2;         // one-pass plist capacity in pairs per reference (8 after an overflow)
     bool lr_handover = true;       // LocalRefine reads DepthToWeak's samples; APD_NO_LR_HANDOVER=1 disables
     bool wcur_on = true;           // RandomInit keeps WEAK current-plane costs for iteration 0; APD_NO_WCUR=1 disables
     bool wcur_fresh = false;       // they belong to the current planes (set by prepare, cleared by iteration)
@@ -4077,6 +4089,8 @@ apd_ctx *apd_create(int32_t device) {
     ctx->lr_handover = getenv("APD_NO_LR_HANDOVER") == nullptr;
     ctx->wcur_on = getenv("APD_NO_WCUR") == nullptr;
     ctx->dtex = getenv("APD_NO_DTEX") == nullptr;
+    ctx->gp_one_pass = getenv("APD_GP_TWO_PASS") == nullptr;
+    if (const char *e = getenv("APD_GP_CAP_FACTOR")) ctx->gp_cap_factor = std::max(0, std::min(8, atoi(e)));  // test hook
 
     // tile_pix needs the tile width to divide the 64-pixel tile (otherwise two workgroups share pixels)
     if (const char *e = getenv("APD_DW_TILE_W")) {
@@ -4461,23 +4475,41 @@ static int build_global_pairs(apd_ctx *ctx, int nw) {
     HIP_OK(ctx, hipMemcpyAsync(&ntask, tpos + HW, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_OK(ctx, hipStreamSynchronize(s));
     int *acnt = (int *)ctx->gp_cbase.p, *abase = acnt + (HW + 1);
-    HIP_OK(ctx, hipMemsetAsync(acnt + ntask, 0, sizeof(int), s));
-    if (ntask > 0)
-        hipLaunchKernelGGL((k_gp_dedup<0>), dim3(ntask), dim3(GP_CHUNK), 0, s, a, (const int *)tasks, (const int *)cur,
-                           (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, acnt, (const int *)nullptr,
-                           (int2 *)nullptr, (uint32_t *)nullptr);
-    if ((st = exclusive_scan_int(ctx, acnt, abase, (size_t)ntask + 1))) return st == APD_ENOMEM ? APD_OK : st;
     int npairs = 0;
-    HIP_OK(ctx, hipMemcpyAsync(&npairs, abase + ntask, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_OK(ctx, hipStreamSynchronize(s));
-    if (npairs > 0 && (!try_ensure(ctx, ctx->gp_plist, (size_t)npairs * sizeof(int2)) ||
-                       !try_ensure(ctx, ctx->gp_pcost, (size_t)npairs * ((a.N + 3) & ~3) * sizeof(float))))
-        return APD_OK;
-    if (npairs > 0)
-        hipLaunchKernelGGL((k_gp_dedup<1>), dim3(ntask), dim3(GP_CHUNK), 0, s, a, (const int *)tasks, (const int *)cur,
-                           (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, (int *)nullptr, (const int *)abase,
-                           (int2 *)ctx->gp_plist.p,
-                           (uint32_t *)ctx->gp_pidx.p);
+    bool one_pass = false;
+    if (ctx->gp_one_pass && ntask > 0) {
+        // one pass: the closed tables reserve their plist ranges with an atomic. Capacity: gp_cap_factor
+        // pairs per reference (a reference has <= 8 candidates; at C3 116 M distinct pairs for 183 M
+        // references); a table past it is detected and the two passes below run instead
+        const size_t pcap = std::min<size_t>((size_t)nrefs * ctx->gp_cap_factor, (size_t)INT32_MAX);
+        if (try_ensure(ctx, ctx->gp_plist, pcap * sizeof(int2))) {
+            HIP_OK(ctx, hipMemsetAsync(acnt, 0, sizeof(int), s));
+            hipLaunchKernelGGL((k_gp_dedup<2>), dim3(ntask), dim3(GP_CHUNK), 0, s, a, (const int *)tasks, (const int *)cur,
+                               (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, acnt, (const int *)nullptr,
+                               (int2 *)ctx->gp_plist.p, (uint32_t *)ctx->gp_pidx.p, (int)pcap);
+            HIP_OK(ctx, hipMemcpyAsync(&npairs, acnt, sizeof(int), hipMemcpyDeviceToHost, s));
+            HIP_OK(ctx, hipStreamSynchronize(s));
+            if ((st = check_launch(ctx, "pair table"))) return st;
+            one_pass = npairs >= 0 && (size_t)npairs <= pcap;
+            if (!one_pass) ctx->gp_cap_factor = 8;  // (the exact bound from now on)
+        }
+    }
+    if (!one_pass) {
+        HIP_OK(ctx, hipMemsetAsync(acnt + ntask, 0, sizeof(int), s));
+        if (ntask > 0)
+            hipLaunchKernelGGL((k_gp_dedup<0>), dim3(ntask), dim3(GP_CHUNK), 0, s, a, (const int *)tasks, (const int *)cur,
+                               (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, acnt, (const int *)nullptr,
+                               (int2 *)nullptr, (uint32_t *)nullptr, 0);
+        if ((st = exclusive_scan_int(ctx, acnt, abase, (size_t)ntask + 1))) return st == APD_ENOMEM ? APD_OK : st;
+        HIP_OK(ctx, hipMemcpyAsync(&npairs, abase + ntask, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIP_OK(ctx, hipStreamSynchronize(s));
+        if (npairs > 0 && !try_ensure(ctx, ctx->gp_plist, (size_t)npairs * sizeof(int2))) return APD_OK;
+        if (npairs > 0)
+            hipLaunchKernelGGL((k_gp_dedup<1>), dim3(ntask), dim3(GP_CHUNK), 0, s, a, (const int *)tasks, (const int *)cur,
+                               (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, (int *)nullptr, (const int *)abase,
+                               (int2 *)ctx->gp_plist.p, (uint32_t *)ctx->gp_pidx.p, 0);
+    }
+    if (npairs > 0 && !try_ensure(ctx, ctx->gp_pcost, (size_t)npairs * ((a.N + 3) & ~3) * sizeof(float))) return APD_OK;
     if ((st = check_launch(ctx, "pair table"))) return st;
     ctx->gp_np = npairs;
     ctx->gp_on = true;
