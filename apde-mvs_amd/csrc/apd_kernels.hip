@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <atomic>
 #include <vector>
 
 #include "../../include/apd_hip.h"
@@ -4430,6 +4431,17 @@ static int *list_ptr(apd_ctx *ctx, int which) {
 
 
 // exclusive prefix sum of n ints (rocPRIM) on the ctx stream
+// test hook (tests/test_gpu_cli.py): APD_TEST_LIB_ENOMEM_AT=k makes the k-th APD apd_stage_prepare of the
+// process fail as if its candidate-cost buffer did not fit -- after RandomInitialization was started on
+// a side stream, the early return the callers' release-and-retry must survive (drain())
+static bool test_enomem_hook(apd_ctx *ctx) {
+    static std::atomic<int> n{0};
+    const char *e = getenv("APD_TEST_LIB_ENOMEM_AT");
+    if (!e || ++n != atoi(e)) return false;
+    ctx->err = "hipMalloc failed (APD_TEST_LIB_ENOMEM_AT)";
+    return true;
+}
+
 static int exclusive_scan_int(apd_ctx *ctx, const int *in, int *out, size_t n) {
     size_t tb = 0;
     HIP_OK(ctx, rocprim::exclusive_scan(nullptr, tb, in, out, 0, n, rocprim::plus<int>(), ctx->stream));
@@ -4611,6 +4623,7 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
             // colours (tile order): between the two Weak launches no anchor plane or selection
             // changes. Costs are kept by WEAK index.
             const size_t wc = (size_t)std::max(ctx->weak_count, 1);
+            if (test_enomem_hook(ctx)) return APD_ENOMEM;  // (RandomInitialization is in flight on side stream 0)
             if ((st = ensure(ctx, ctx->wcand, (size_t)a.N * 8 * wc * sizeof(float)))) return st;
             if ((st = ensure(ctx, ctx->wlist, (size_t)(ctx->cnt[2] + ctx->cnt[3]) * sizeof(int)))) return st;
             if ((st = build_tile_list(ctx, 1, 2, (int *)ctx->wlist.p, tot + 5))) return st;
@@ -5024,6 +5037,26 @@ int32_t apd_device_copy(apd_ctx *ctx, void *dst, const void *src, size_t bytes) 
     (void)hipSetDevice(ctx->device);
     HIP_OK(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, ctx->stream));
     HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+    return APD_OK;
+}
+
+int32_t apd_device_copy_peer(apd_ctx *dst_ctx, void *dst, apd_ctx *src_ctx, const void *src, size_t bytes) {
+    if (!dst_ctx || !src_ctx || (!dst && bytes) || (!src && bytes)) return APD_EINVAL;
+    if (!bytes) return APD_OK;
+    (void)hipSetDevice(dst_ctx->device);
+    if (dst_ctx->device == src_ctx->device) {
+        HIP_OK(dst_ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, dst_ctx->stream));
+    } else {
+        // direct over xGMI when the devices can map each other (enabled once per device pair; an
+        // already-enabled pair reports hipErrorPeerAccessAlreadyEnabled), else staged by the runtime
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, dst_ctx->device, src_ctx->device) == hipSuccess && can) {
+            const hipError_t e = hipDeviceEnablePeerAccess(src_ctx->device, 0);
+            if (e != hipSuccess) (void)hipGetLastError();
+        }
+        HIP_OK(dst_ctx, hipMemcpyPeerAsync(dst, dst_ctx->device, src, src_ctx->device, bytes, dst_ctx->stream));
+    }
+    HIP_OK(dst_ctx, hipStreamSynchronize(dst_ctx->stream));
     return APD_OK;
 }
 

@@ -247,7 +247,7 @@ struct Pending {  // Jacobi ordering: outputs committed at the end of the pass
     Mat mat;
 };
 
-// Device-resident view state (one context): the round's images and every view's last depth and
+// Device-resident view state (one per context): the round's images and every view's last depth and
 // (normal, depth) planes stay in HBM between problems. The reference re-reads and re-uploads all of
 // them per problem (APD.cpp:508-684): at 6048x4032 with 10 sources that is 2.5 GB of uploads per
 // problem. The files are still written (fusion and later runs read them) and the maps here hold the
@@ -351,6 +351,29 @@ struct DevStore {
             for (auto &kv : *pair.first)
                 std::swap((*pair.second)[kv.first], kv.second);  // the old buffer serves the next pass
     }
+    // Jacobi over several contexts: view `id`'s new maps, produced by another context, into this
+    // store's pending maps, device to device (apd_device_copy_peer: xGMI between GPUs, a device copy
+    // between two contexts of one GPU). False (the view forgotten here) when there is no room.
+    struct Source {  // a snapshot of another store's pending maps of one view (taken before the pulls)
+        int id;
+        DevStore *from;   // nullptr: no store holds the view's new maps
+        const void *d, *pl;
+        int w, h;
+    };
+    bool pull(const Source &v) {
+        float *d = nullptr, *pl = nullptr;
+        if (!output(v.id, true, v.w, v.h, &d, &pl)) return false;
+        if (apd_device_copy_peer(ctx, d, v.from->ctx, v.d, (size_t)v.w * v.h * sizeof(float)) != APD_OK ||
+            apd_device_copy_peer(ctx, pl, v.from->ctx, v.pl, (size_t)v.w * v.h * 4 * sizeof(float)) != APD_OK) {
+            forget(v.id);
+            return false;
+        }
+        return true;
+    }
+    bool pending_of(int id) const {
+        auto a = pend_depth.find(id), b = pend_planes.find(id);
+        return a != pend_depth.end() && a->second.p && b != pend_planes.end() && b->second.p;
+    }
     ~DevStore() {
         if (!ctx) return;
         drop_images();
@@ -369,7 +392,18 @@ struct Driver {
     bool jacobi = false;
     MatStore *store = nullptr;
     ImageCache images;
-    std::unique_ptr<DevStore> dev;  // single context only (the maps live on its device)
+    // one device store per context (each holds every view's maps on its own device; a Jacobi pass's
+    // new maps are exchanged between them at the commit), or none (APD_DEVICE_STATE=0)
+    std::vector<apd_ctx *> ctxs;
+    std::vector<std::unique_ptr<DevStore>> devs;
+    std::unique_ptr<DevStore> &store_for(apd_ctx *ctx) {
+        static std::unique_ptr<DevStore> none;
+        for (size_t k = 0; k < ctxs.size(); ++k)
+            if (ctxs[k] == ctx && k < devs.size()) return devs[k];
+        none.reset();
+        return none;
+    }
+    std::vector<int> pass_views;  // the views of the current pass (the commit exchanges their maps)
     std::mutex pend_mu;
     std::vector<Pending> pending;
 
@@ -404,13 +438,50 @@ struct Driver {
     void commit() {
         for (auto &p : pending) store->write(p.path, p.mat, flush);
         pending.clear();
-        if (dev) dev->commit();
+        exchange_maps();
+        for (auto &d : devs)
+            if (d) d->commit();
         std::lock_guard<std::mutex> g(fit_mu);
         fitted.clear();
     }
+    // Jacobi over several contexts (after the pass's workers joined): every store gets every view's new
+    // maps. A view that no store holds (its context's store ran out of room or was released) is
+    // forgotten everywhere: the previous pass's map would be stale, and the files hold the new one.
+    // Each destination store pulls on its own thread (its own device and stream).
+    void exchange_maps() {
+        std::vector<DevStore *> live;
+        for (auto &d : devs)
+            if (d) live.push_back(d.get());
+        if (live.size() < 2 && live.size() == devs.size()) return;  // one context: nothing to exchange
+        // the sources, read here before any store changes its maps (each pulling thread then writes
+        // only its own store's maps)
+        std::vector<DevStore::Source> src;
+        for (int id : pass_views) {
+            DevStore::Source v{id, nullptr, nullptr, nullptr, 0, 0};
+            for (DevStore *d : live)
+                if (d->pending_of(id)) {
+                    const DevStore::Map &md = d->pend_depth.at(id), &mp = d->pend_planes.at(id);
+                    v = DevStore::Source{id, d, md.p, mp.p, md.w, md.h};
+                    break;
+                }
+            src.push_back(v);
+        }
+        std::vector<std::thread> th;
+        for (DevStore *to : live)
+            th.emplace_back([&src, to]() {
+                for (const auto &v : src) {
+                    if (v.from == to) continue;
+                    if (!v.from) { to->forget(v.id); continue; }
+                    if (!to->pull(v))
+                        SAY("device state full: view " << v.id << " falls back to the host store on one context");
+                }
+            });
+        for (auto &t : th) t.join();
+    }
     void new_round() {  // each round uses one scale
         images.drop_scaled();
-        if (dev) dev->drop_images();
+        for (auto &d : devs)
+            if (d) d->drop_images();
     }
 
     // APD::InuputInitialization + CudaSpaceInitialization + RunPatchMatch + ProcessProblem
@@ -440,6 +511,7 @@ struct Driver {
 
 bool Driver::process(apd_ctx *ctx, Job &job) {
     const Problem &pb = job.pb;
+    std::unique_ptr<DevStore> &dev = store_for(ctx);  // (this context's store; only its worker uses it)
     const std::string result_folder = dense + "/APD/" + format_index(pb.ref_image_id);
     SAY("Processing image: " << format_index(pb.ref_image_id) << "...");
     const auto start = std::chrono::steady_clock::now();
@@ -692,6 +764,14 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
     }
     const auto t_run = std::chrono::steady_clock::now();
     st = apd_get_results(ctx, &out);
+    if (st == APD_ENOMEM && dev) {
+        // the anchors export's staging buffer did not fit next to the store: release the store (as
+        // above) and read the results again -- the ctx still holds them
+        SAY("device memory exhausted (" << apd_last_error(ctx) << "): device-resident state released, "
+                                         "the run continues from the host store");
+        dev.reset();
+        st = apd_get_results(ctx, &out);
+    }
     const auto t_get = std::chrono::steady_clock::now();
     if (st != APD_OK) { SAY("apd_get_results failed: " << apd_last_error(ctx)); return false; }
     if (dev) {  // this view's next priors, kept in HBM (Jacobi: visible after the pass, as the files)
@@ -893,7 +973,7 @@ int main(int argc, char **argv) {
     drv.seed = std::strtoull(vm["seed"].c_str(), nullptr, 10);
     drv.jacobi = ordering == "jacobi";
     drv.store = &store;
-    std::vector<apd_ctx *> ctxs;
+    std::vector<apd_ctx *> &ctxs = drv.ctxs;
     for (int d : gpus) {
         apd_ctx *c = apd_create(d);
         if (!c) {
@@ -902,19 +982,27 @@ int main(int argc, char **argv) {
         }
         ctxs.push_back(c);
     }
-    if (ctxs.size() == 1 && !(getenv("APD_DEVICE_STATE") && std::string(getenv("APD_DEVICE_STATE")) == "0")) {
-        drv.dev = std::make_unique<DevStore>();
-        drv.dev->ctx = ctxs[0];
-        // default cap: the device's free memory less room for the library's per-problem buffers
-        // (≈ 40 GB at C3 with the pair table and the DepthToWeak hand-over; a quarter of the free
-        // memory, at least 16 GiB); a problem that still runs out releases the store (process())
-        size_t fb = 0, tb = 0;
-        if (apd_device_mem_info(ctxs[0], &fb, &tb) == APD_OK) {
-            const size_t room = std::max<size_t>((size_t)16 << 30, fb / 4);
-            drv.dev->cap = fb > room ? fb - room : 0;
+    if (!(getenv("APD_DEVICE_STATE") && std::string(getenv("APD_DEVICE_STATE")) == "0")) {
+        // one store per context. Default cap: the device's free memory less room for the library's
+        // per-problem buffers (≈ 40 GB at C3 with the pair table and the DepthToWeak hand-over; a quarter
+        // of the free memory, at least 16 GiB), shared by the contexts on that device; a problem that
+        // still runs out releases its context's store (process())
+        std::map<int, int> per_dev;
+        for (int d : gpus) per_dev[d]++;
+        for (size_t k = 0; k < ctxs.size(); ++k) {
+            auto d = std::make_unique<DevStore>();
+            d->ctx = ctxs[k];
+            size_t fb = 0, tb = 0;
+            if (apd_device_mem_info(ctxs[k], &fb, &tb) == APD_OK) {
+                const int share = per_dev[gpus[k]];
+                const size_t room = std::max<size_t>((size_t)16 << 30, fb / 4) * share;
+                d->cap = fb > room ? (fb - room) / share : 0;
+            }
+            if (const char *e = getenv("APD_DEVICE_STATE_CAP_MB")) d->cap = (size_t)std::max(0L, atol(e)) << 20;
+            drv.devs.push_back(std::move(d));
         }
-        if (const char *e = getenv("APD_DEVICE_STATE_CAP_MB")) drv.dev->cap = (size_t)std::max(0L, atol(e)) << 20;
     }
+    for (auto &p : problems) drv.pass_views.push_back(p.ref_image_id);
     std::vector<Job> jobs(problems.size());
     for (size_t i = 0; i < problems.size(); ++i) jobs[i].pb = problems[i];
     bool ok = true;
@@ -1006,8 +1094,14 @@ int main(int argc, char **argv) {
         }
         std::cout << "=============================================================" << std::endl;
     }
-    if (drv.dev) printf("Device-resident state: %.1f MB of image uploads\n", drv.dev->uploaded / 1048576.0);
-    drv.dev.reset();  // its buffers belong to ctxs[0]
+    {
+        long up = 0;
+        bool any = false;
+        for (auto &d : drv.devs)
+            if (d) { up += d->uploaded; any = true; }
+        if (any) printf("Device-resident state: %.1f MB of image uploads\n", up / 1048576.0);
+    }
+    drv.devs.clear();  // their buffers belong to the contexts
     for (apd_ctx *c : ctxs) apd_destroy(c);
     if (!ok) return EXIT_FAILURE;
     const auto end = std::chrono::steady_clock::now();

@@ -267,6 +267,11 @@ int32_t apd_device_free(apd_ctx *ctx, void *ptr);
 int32_t apd_device_copy(apd_ctx *ctx, void *dst, const void *src, size_t bytes);
 /* Free and total bytes of the ctx's device (hipMemGetInfo): the `apd` binary sizes its
    device-resident store from it, leaving room for the library's per-problem buffers. */
+/* Copy `bytes` from device memory of src_ctx's device to device memory of dst_ctx's device (the same
+   device, or a peer over xGMI with peer access enabled on first use); waits for the copy. The `apd`
+   binary moves a Jacobi pass's new view maps between its contexts' device stores with it. */
+int32_t apd_device_copy_peer(apd_ctx *dst_ctx, void *dst, apd_ctx *src_ctx, const void *src, size_t bytes);
+
 int32_t apd_device_mem_info(apd_ctx *ctx, size_t *free_bytes, size_t *total_bytes);
 /* cv::resize INTER_NEAREST (the priors' resize, APD.cpp:605-672) from a device buffer of sw x sh
    elements of elem_bytes to one of dw x dh, with the host library's index arithmetic. */

@@ -68,7 +68,10 @@ def check_outputs(folder, expected):
     ("sequential", "0", "1"),   # one context: images and depth/plane priors resident in HBM
     ("sequential", "0", "0"),   # APD_DEVICE_STATE=0: every input uploaded from the host per problem
     ("jacobi", "0", "1"),       # resident state with this pass's maps held back until the pass ends
-    ("jacobi", "0,0", "1"),     # two contexts: host-side state (the device store is single-context)
+    ("jacobi", "0,0", "1"),     # two contexts, a device store each; the pass's new maps exchanged at the commit
+    ("jacobi", "0,0", "0"),     # two contexts, host-side state
+    ("jacobi", "0,0", "oomlib"),  # a library buffer fails after RandomInitialization started on a side stream:
+                                  # that context's store is released, the other keeps its own; same outputs
     ("sequential", "0", "cap"),  # device store capped (APD_DEVICE_STATE_CAP_MB): views that do not fit
     ("jacobi", "0", "cap"),      # ... fall back to the host store, same outputs
     ("sequential", "0", "oom"),  # a problem finds HBM exhausted (APD_TEST_ENOMEM_AT): the store is released
@@ -78,20 +81,22 @@ def test_cli_matches_schedule(scan, engine, ordering, gpus, device_state, tmp_pa
     import shutil
     folder = str(tmp_path / "run")
     shutil.copytree(scan, folder)
-    env = dict(os.environ, APD_DEVICE_STATE="1" if device_state in ("cap", "oom") else device_state)
+    env = dict(os.environ, APD_DEVICE_STATE="1" if device_state in ("cap", "oom", "oomlib") else device_state)
     if device_state == "cap":  # room for the round's images and a few views' maps, not for all of them
         env["APD_DEVICE_STATE_CAP_MB"] = "40"
     if device_state == "oom":  # the 13th problem (second round, maps and images resident) runs out
         env["APD_TEST_ENOMEM_AT"] = "13"
+    if device_state == "oomlib":  # the second APD problem (round 1) fails inside apd_stage_prepare
+        env["APD_TEST_LIB_ENOMEM_AT"] = "2"
     r = subprocess.run([APD_BIN, "--dense_folder", folder, "--dataset", "ETH3D", "--no_fuse", "true",
                         "--memory_cache", "false", "--gpus", gpus, "--ordering", ordering],
                        capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "Round nums: 2" in r.stdout
-    resident = device_state in ("1", "cap") and "," not in gpus
+    resident = device_state in ("1", "cap", "oomlib")
     if device_state == "cap":
         assert "falls back to the host store" in r.stdout
-    if device_state == "oom":
+    if device_state in ("oom", "oomlib"):
         assert "device-resident state released" in r.stdout
     assert ("Device-resident state:" in r.stdout) == resident
     assert r.stdout.count("RunPatchMatch time:") == 5 * 8

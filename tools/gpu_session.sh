@@ -1,6 +1,7 @@
 #!/bin/bash
 # One GPU-box session of chained steps (run from the repo root): bash tools/gpu_session.sh OUT STEP...
 # Steps: parity | tests:<file,file,...> | gputests | smoke | ab:<AB env>:<libA>,<libB>,... | bench[:args] | pmc:<kernel-regex>:<last>:<bench args> | prof[:args]
+#        | script:<path>[,args] (bash <path> <step out dir> args)
 # Each GPU step has its own time limit; the script stops at the first failure.
 set -e
 OUT=$1; shift
@@ -24,6 +25,7 @@ for step in "$@"; do
     prof) cd /tmp
           timeout -k 10 700 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/s$n.prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --c2 0 --rich 0 --sa 0 --steps 6 --warmup 1 $rest > "$GRAFT_REPO_ROOT/$OUT/s$n.prof_bench.json" 2> "$GRAFT_REPO_ROOT/$OUT/s$n.prof_bench.err"
           cd "$GRAFT_REPO_ROOT" ;;
+    script) timeout -k 10 1100 bash ${rest%%,*} "$OUT/s$n.script" ${rest#*,} > "$OUT/s$n.script.log" 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
