@@ -4073,8 +4073,27 @@ apd_ctx *apd_create(int32_t device) {
         return nullptr;
     }
     for (auto &e : ctx->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);  // timing only
+    // side stream 0 (RandomInitialization beside the lists and the pair table; RANSAC beside the
+    // candidate kernels) at the lowest priority: its work fills what the ctx stream's kernels leave
+    // free instead of sharing the CUs with them evenly (APD_SIDE_PRIORITY=0: every stream at the default)
+    // (priorities: a lower value is a higher priority; when the default is already the least, the ctx
+    // stream and side stream 1 are raised instead)
+    int prio_least = 0, prio_greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+    const bool low_side = !(getenv("APD_SIDE_PRIORITY") && atoi(getenv("APD_SIDE_PRIORITY")) == 0);
+    if (low_side && prio_least <= 0 && prio_greatest < 0) {
+        hipStream_t hi = nullptr;
+        if (hipStreamCreateWithPriority(&hi, hipStreamNonBlocking, prio_greatest) == hipSuccess) {
+            (void)hipStreamDestroy(ctx->stream);
+            ctx->stream = hi;
+        }
+    }
+    if (getenv("APD_DEBUG_PRIO")) fprintf(stderr, "apd: stream priorities least %d greatest %d\n", prio_least, prio_greatest);
     for (auto &ss : ctx->side) {
-        if (hipStreamCreateWithFlags(&ss, hipStreamNonBlocking) != hipSuccess) {
+        int prio = 0;
+        if (low_side && prio_least > 0 && &ss == &ctx->side[0]) prio = prio_least;
+        if (low_side && prio_least <= 0 && prio_greatest < 0 && &ss == &ctx->side[1]) prio = prio_greatest;
+        if (hipStreamCreateWithPriority(&ss, hipStreamNonBlocking, prio) != hipSuccess) {
             set_global_err("hipStreamCreate failed");
             for (auto &t : ctx->side) if (t) (void)hipStreamDestroy(t);
             (void)hipStreamDestroy(ctx->stream);

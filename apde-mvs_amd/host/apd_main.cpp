@@ -23,6 +23,7 @@
 #include <iomanip>
 #include <iostream>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <sstream>
@@ -264,6 +265,8 @@ struct DevStore {
     std::map<std::string, Map> images;          // this round's images, by path
     std::map<int, Map> depth, planes;           // committed maps, by view id
     std::map<int, Map> pend_depth, pend_planes;  // Jacobi: this pass's outputs until commit()
+    std::set<int> fresh;                         // views whose pending maps this pass wrote (commit() clears;
+                                                 // after a commit the pending slots hold recycled buffers)
     Map scratch;                                 // resized priors of one problem
     long uploaded = 0;                           // bytes copied from the host (images)
     // bytes held; an allocation that fails (or would pass APD_DEVICE_STATE_CAP_MB, a test hook) makes
@@ -324,6 +327,7 @@ struct DevStore {
     // view `id` leaves the device state (HBM exhausted): every later problem reads its priors from
     // the store, which always holds the same values (the files are written either way)
     void forget(int id) {
+        fresh.erase(id);
         for (auto *ms : {&depth, &planes, &pend_depth, &pend_planes}) {
             auto it = ms->find(id);
             if (it != ms->end()) {
@@ -342,6 +346,7 @@ struct DevStore {
         }
         md.w = mp.w = w;
         md.h = mp.h = h;
+        if (pending) fresh.insert(id);
         *d = static_cast<float *>(md.p);
         *pl = static_cast<float *>(mp.p);
         return true;
@@ -349,7 +354,8 @@ struct DevStore {
     void commit() {
         for (auto pair : {std::make_pair(&pend_depth, &depth), std::make_pair(&pend_planes, &planes)})
             for (auto &kv : *pair.first)
-                std::swap((*pair.second)[kv.first], kv.second);  // the old buffer serves the next pass
+                if (fresh.count(kv.first)) std::swap((*pair.second)[kv.first], kv.second);  // the old buffer serves the next pass
+        fresh.clear();
     }
     // Jacobi over several contexts: view `id`'s new maps, produced by another context, into this
     // store's pending maps, device to device (apd_device_copy_peer: xGMI between GPUs, a device copy
@@ -370,10 +376,7 @@ struct DevStore {
         }
         return true;
     }
-    bool pending_of(int id) const {
-        auto a = pend_depth.find(id), b = pend_planes.find(id);
-        return a != pend_depth.end() && a->second.p && b != pend_planes.end() && b->second.p;
-    }
+    bool pending_of(int id) const { return fresh.count(id) != 0; }
     ~DevStore() {
         if (!ctx) return;
         drop_images();
