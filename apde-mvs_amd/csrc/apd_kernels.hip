@@ -517,10 +517,21 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
     Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_ANCHORS);
     for (int i = 0; i < 9; ++i) anc[i] = make_short2(-1, -1);
     anc[0] = make_short2((short)px, (short)py);
-    short2 sp[32];
+    // the search finds its points in direction-slot order (di = odi * 4 + ri increases through the
+    // loops), which is also the stage's dvalid order: SPLIT writes each point to its stage slot as it is
+    // found instead of into a dynamically indexed private array (which lived in scratch memory)
+    const size_t wi = (size_t)a.amap[c];
+    short2 sp[SPLIT ? 1 : 32];
     uint32_t dvalid = 0;
-    for (int i = 0; i < 32; ++i) sp[i] = make_short2(-1, -1);
+    if constexpr (!SPLIT)
+        for (int i = 0; i < 32; ++i) sp[i] = make_short2(-1, -1);
     int odi = -1, nsp = 0;
+    auto found = [&](int di, short2 p) {
+        if constexpr (SPLIT) stage[(size_t)(2 + nsp) * wc + wi] = (uint32_t)(uint16_t)p.x | ((uint32_t)(uint16_t)p.y << 16);
+        else sp[di] = p;
+        dvalid |= 1u << di;
+        nsp++;
+    };
     const int rt = a.rotate_time;
     const FastMod fshift((uint32_t)a.anc_shift);
     for (int odx = -1; odx <= 1; ++odx) {
@@ -552,7 +563,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
                             ok = tdx * dx + tdy * dy > a.anc_thr;
                         }
                         g.n += ok ? 4u : 16u;
-                        if (ok) { sp[di] = nn; dvalid |= 1u << di; nsp++; break; }
+                        if (ok) { found(di, nn); break; }
                     }
                 } else
                 for (int radius = 2; radius <= APD_MAX_SEARCH_RADIUS; radius = min(radius * 2, radius + 25)) {
@@ -584,7 +595,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
                         float tdx = (float)(nn[t].x - px), tdy = (float)(nn[t].y - py);
                         normalize2(tdx, tdy);
                         float ca = tdx * dx + tdy * dy;
-                        if (ca > a.anc_thr) { sp[di] = nn[t]; dvalid |= 1u << di; nsp++; used = t + 1; }
+                        if (ca > a.anc_thr) { found(di, nn[t]); used = t + 1; }
                     }
 #ifdef APD_ANCHOR_STATS  // measurement build: steps, the attempt that succeeded, wave-level steps
                     if (a.evals) {
@@ -604,18 +615,11 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
     }
     if (nsp <= 3) {
         a.reliable[c] = 0;
-        if constexpr (SPLIT) stage[a.amap[c]] = 0u;
+        if constexpr (SPLIT) stage[wi] = 0u;
         return;
     }
     if constexpr (SPLIT) {
-        const size_t wi = (size_t)a.amap[c];
-        int vc = 0;
-        for (int i = 0; i < 32; ++i)
-            if ((dvalid >> i) & 1u) {
-                stage[(size_t)(2 + vc) * wc + wi] = (uint32_t)(uint16_t)sp[i].x | ((uint32_t)(uint16_t)sp[i].y << 16);
-                vc++;
-            }
-        stage[wi] = (g.n << 6) | (uint32_t)vc;
+        stage[wi] = (g.n << 6) | (uint32_t)nsp;  // (the points are in stage slots 2 .. 2 + nsp - 1)
         stage[(size_t)wc + wi] = (uint32_t)c;
         return;
     } else {
