@@ -2594,6 +2594,12 @@ __global__ __launch_bounds__(WV_BLOCK, (WvOcc<F16, SA>::occ)) void k_sweep_weak_
 // a table closes once it holds GP_CLOSE keys after a batch; a batch adds <= 8 * GP_CHUNK: load <= 0.75
 #define GP_CLOSE (GP_HS * 3 / 4 - 8 * GP_CHUNK)
 static_assert(GP_CLOSE > 0 && GP_HS >= 256 && 256 % GP_CHUNK == 0, "k_gp_dedup table sizing");
+// window anchors with at most GP_SMALL_N references (most of them) run in a one-wave workgroup with a
+// 1 k-slot table (6 KiB of LDS instead of 48 KiB: many more workgroups per CU, the kernel is latency
+// bound); their references fit one batch, so the table is the large kernel's single table
+#define GP_SMALL_N 64
+#define GP_SMALL_HS 1024
+static_assert(GP_SMALL_HS * 3 / 4 - 8 * GP_SMALL_N > 0 && 8 * GP_SMALL_N <= GP_SMALL_HS / 2, "small k_gp_dedup sizing");
 #define GP_NONE 0xFFFFFFFFu
 
 // profiling: a wave's sum of the lanes' counts, one atomic per wave
@@ -2651,9 +2657,61 @@ __global__ __launch_bounds__(BLOCK) void k_gp_count(Args a, const int *__restric
     }
     if (act) { cbw[wi] = (uint8_t)cb; wmw[wi] = (uint8_t)wm; }
 }
+// k_gp_count with the references' places: the run head's atomic returns the run's first position in
+// its window anchor's segment, and every reference keeps its own (loc[WEAK index * 8 + k - 1]);
+// k_gp_place then writes each reference at segment offset + place -- no second pass of atomics
+// (k_gp_fill, the path APD_GP_FILL=1 keeps)
+__global__ __launch_bounds__(BLOCK) void k_gp_count_loc(Args a, const int *__restrict__ list, int count, int *__restrict__ cnt,
+                                                        uint8_t *__restrict__ cbw, uint8_t *__restrict__ wmw,
+                                                        uint32_t *__restrict__ loc) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool act = i < count;
+    const int c = list[act ? i : count - 1];
+    const int wi = a.amap[c];
+    const int cid = a.sa_any ? (int)a.sa[c] : 0;
+    const APD_G short2 *anc = a.anchors + (size_t)wi * 9;
+    uint32_t cb = 0, wm = 0;
+#pragma unroll 1
+    for (int k = 1; k < 9; ++k) {
+        const short2 ap = anc[k];
+        const bool valid = act && !(ap.x == -1 || ap.y == -1);
+        const int q = valid ? ap.x + ap.y * a.W : -1;
+        if (valid && a.weak[q] == APD_STRONG) cb |= 1u << (k - 1);
+        const bool ok = valid && gp_window_used(a, cid, q);
+        if (ok) wm |= 1u << (k - 1);
+        int hl, rk, len;
+        gp_run(ok, q, hl, rk, len);
+        int pos = 0;
+        if (ok && rk == 0) pos = atomicAdd(&cnt[q], len);
+        pos = __shfl(pos, hl) + rk;
+        if (ok) loc[(size_t)wi * 8 + (k - 1)] = (uint32_t)pos;
+    }
+    if (act) { cbw[wi] = (uint8_t)cb; wmw[wi] = (uint8_t)wm; }
+}
 // references (WEAK index * 8 + window slot k - 1, bit 31: filtered by the SA label) into their
 // window anchor's segment
 #define GP_FILT 0x80000000u
+__global__ __launch_bounds__(BLOCK) void k_gp_place(Args a, const int *__restrict__ list, int count, const int *__restrict__ off,
+                                                    const uint8_t *__restrict__ wmw, const uint32_t *__restrict__ loc,
+                                                    uint32_t *__restrict__ refs) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= count) return;
+    const int c = list[i];
+    const uint32_t wi = (uint32_t)a.amap[c];
+    const uint32_t filt = (a.sa_any && a.sa[c] != 0) ? GP_FILT : 0u;
+    const uint32_t wm = wmw[wi];
+    const APD_G short2 *anc = a.anchors + (size_t)wi * 9;
+    const uint4 l0 = *reinterpret_cast<const uint4 *>(loc + (size_t)wi * 8);
+    const uint4 l1 = *reinterpret_cast<const uint4 *>(loc + (size_t)wi * 8 + 4);
+    const uint32_t l[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+#pragma unroll
+    for (int k = 1; k < 9; ++k) {
+        if (!((wm >> (k - 1)) & 1u)) continue;
+        const short2 ap = anc[k];
+        const int q = ap.x + ap.y * a.W;
+        refs[off[q] + l[k - 1]] = (wi * 8u + (uint32_t)(k - 1)) | filt;
+    }
+}
 __global__ __launch_bounds__(BLOCK) void k_gp_fill(Args a, const int *__restrict__ list, int count, int *__restrict__ cur,
                                                    uint32_t *__restrict__ refs) {
     const int i = blockIdx.x * BLOCK + threadIdx.x;
@@ -2698,22 +2756,28 @@ __global__ __launch_bounds__(BLOCK) void k_gp_tasks(const int *__restrict__ off,
 // counter above pcap, builds the table again with the two passes. PASS 0 counts the distinct pairs
 // per anchor (acnt) and PASS 1 writes them from the scanned bases (abase): the fallback, and the
 // path APD_GP_TWO_PASS=1 forces. Pair ids are labels either way: the costs never depend on them.
-template <int PASS>
-__global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__restrict__ tasks, const int *__restrict__ off,
-                                                       const uint32_t *__restrict__ refs, const uint8_t *__restrict__ cbw,
-                                                       int *__restrict__ acnt,
-                                                       const int *__restrict__ abase, int2 *__restrict__ plist,
-                                                       uint32_t *__restrict__ pidx, int pcap) {
-    __shared__ uint32_t hs[GP_HS];
-    __shared__ uint16_t sid[GP_HS];
-    __shared__ int scan_w[GP_CHUNK / WAVE + 1];
+// SIZE (PASS 2): 0 = every task, 1 = the small ones only (n <= GP_SMALL_N; HS, CHUNK the small table),
+// 2 = the others only.
+template <int PASS, int HS = GP_HS, int CHUNK = GP_CHUNK, int SIZE = 0>
+__global__ __launch_bounds__(CHUNK) void k_gp_dedup(Args a, const int *__restrict__ tasks, const int *__restrict__ off,
+                                                    const uint32_t *__restrict__ refs, const uint8_t *__restrict__ cbw,
+                                                    int *__restrict__ acnt,
+                                                    const int *__restrict__ abase, int2 *__restrict__ plist,
+                                                    uint32_t *__restrict__ pidx, int pcap) {
+    constexpr int CLOSE = HS * 3 / 4 - 8 * CHUNK;
+    static_assert(CLOSE > 0 && HS >= 256 && HS % CHUNK == 0 && 256 % CHUNK == 0, "k_gp_dedup table sizing");
+    __shared__ uint32_t hs[HS];
+    __shared__ uint16_t sid[HS];
+    __shared__ int scan_w[CHUNK / WAVE + 1];
     __shared__ int nfresh, sbase;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid >> 6;
     const int q = tasks[blockIdx.x];
     const int r0 = off[q], n = off[q + 1] - r0;
+    if (SIZE == 1 && n > GP_SMALL_N) return;
+    if (SIZE == 2 && n <= GP_SMALL_N) return;
     const int qx = q % a.W, qy = q / a.W;
     int cap = 256, lg = 8;
-    while (cap < GP_HS && cap < n * 16) { cap <<= 1; ++lg; }
+    while (cap < HS && cap < n * 16) { cap <<= 1; ++lg; }
     const uint32_t msk = (uint32_t)cap - 1u;
     auto slot_of = [&](uint32_t key) { return (key * 0x9E3779B1u) >> (32 - lg); };
     // candidates (valid, STRONG anchors 1..8) of reference r: bits + keys (candidate position + 1,
@@ -2732,12 +2796,12 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
         }
         return cb;
     };
-    for (int i = tid; i < cap; i += GP_CHUNK) hs[i] = 0u;
+    for (int i = tid; i < cap; i += CHUNK) hs[i] = 0u;
     if (tid == 0) nfresh = 0;
     __syncthreads();
     int base = PASS == 1 ? abase[blockIdx.x] : 0, total = 0;
     int run0 = 0;  // first reference of the open table
-    for (int b0 = 0; b0 < n; b0 += GP_CHUNK) {
+    for (int b0 = 0; b0 < n; b0 += CHUNK) {
         const int r = b0 + tid;
         if (r < n) {
             uint32_t wi, k, qh[8];
@@ -2762,7 +2826,7 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
         // every thread has read nfresh before any wave's next-batch inserts can add to it (else
         // `close` and `base` could differ between waves)
         __syncthreads();
-        const bool close = nd >= GP_CLOSE || b0 + GP_CHUNK >= n;
+        const bool close = nd >= CLOSE || b0 + CHUNK >= n;
         if (!close) continue;  // (uniform)
         if (PASS == 2) {
             if (tid == 0) sbase = atomicAdd(acnt, nd);
@@ -2771,7 +2835,7 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
         }
         if (PASS >= 1) {
             // plist[base + id] = (window anchor, candidate anchor)
-            const int per = cap / GP_CHUNK;  // slots per thread (cap >= GP_CHUNK)
+            const int per = cap / CHUNK;  // slots per thread (cap >= CHUNK)
             const int s0 = tid * per, s1 = s0 + per;
             int c = 0;
             for (int sl = s0; sl < s1; ++sl) c += hs[sl] != 0u;
@@ -2798,7 +2862,7 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
             }
             __syncthreads();
             // the table's references: pair ids of their (candidate, window) slots
-            for (int rr = run0 + tid; rr < min(n, b0 + GP_CHUNK); rr += GP_CHUNK) {
+            for (int rr = run0 + tid; rr < min(n, b0 + CHUNK); rr += CHUNK) {
                 uint32_t wi, k, qh[8], pv[8];
                 const uint32_t cb = cands(r0 + rr, wi, k, qh);
 #pragma unroll
@@ -2818,8 +2882,8 @@ __global__ __launch_bounds__(GP_CHUNK) void k_gp_dedup(Args a, const int *__rest
         }
         if (PASS != 2) base += nd;
         total += nd;
-        run0 = b0 + GP_CHUNK;
-        for (int i = tid; i < cap; i += GP_CHUNK) hs[i] = 0u;
+        run0 = b0 + CHUNK;
+        for (int i = tid; i < cap; i += CHUNK) hs[i] = 0u;
         __syncthreads();
         if (tid == 0) nfresh = 0;
         __syncthreads();
@@ -3871,6 +3935,8 @@ struct apd_ctx {
     bool dtex = true;              // DepthToWeak over pre-differenced fp16 texels (FastTexD); APD_NO_DTEX=1 disables
     int gp_np = 0;                 // its distinct pairs
     bool gp_one_pass = true;       // k_gp_dedup in one pass (atomic plist ranges); APD_GP_TWO_PASS=1: count + write
+    bool gp_place = true;          // k_gp_count_loc + k_gp_place; APD_GP_FILL=1: k_gp_count + k_gp_fill (atomics twice)
+    bool gp_small = true;          // one-pass small anchors in one-wave workgroups; APD_GP_NO_SMALL=1: all in 256-thread ones
     int gp_cap_factor = 2;         // one-pass plist capacity in pairs per reference (8 after an overflow)
     bool lr_handover = true;       // LocalRefine reads DepthToWeak's samples; APD_NO_LR_HANDOVER=1 disables
     bool wcur_on = true;           // RandomInit keeps WEAK current-plane costs for iteration 0; APD_NO_WCUR=1 disables
@@ -4114,6 +4180,8 @@ apd_ctx *apd_create(int32_t device) {
     ctx->wcur_on = getenv("APD_NO_WCUR") == nullptr;
     ctx->dtex = getenv("APD_NO_DTEX") == nullptr;
     ctx->gp_one_pass = getenv("APD_GP_TWO_PASS") == nullptr;
+    ctx->gp_small = getenv("APD_GP_NO_SMALL") == nullptr;
+    ctx->gp_place = getenv("APD_GP_FILL") == nullptr;
     if (const char *e = getenv("APD_GP_CAP_FACTOR")) ctx->gp_cap_factor = std::max(0, std::min(8, atoi(e)));  // test hook
 
     // tile_pix needs the tile width to divide the 64-pixel tile (otherwise two workgroups share pixels)
@@ -4488,15 +4556,26 @@ static int build_global_pairs(apd_ctx *ctx, int nw) {
     int *cnt = (int *)ctx->gp_cnt.p, *cur = (int *)ctx->gp_cur.p;
     HIP_OK(ctx, hipMemsetAsync(cnt, 0, (HW + 1) * sizeof(int), s));
     // gp_cb: candidate bits [wc], then used windows [wc]
-    hipLaunchKernelGGL(k_gp_count, dim3(blocks_for((size_t)nw, BLOCK)), dim3(BLOCK), 0, s, a, (const int *)ctx->wlist.p, nw, cnt,
-                       (uint8_t *)ctx->gp_cb.p, (uint8_t *)ctx->gp_cb.p + wc);
+    // (the references' places live in gp_pidx until k_gp_dedup writes the pair ids there)
+    uint32_t *loc = (uint32_t *)ctx->gp_pidx.p;
+    if (ctx->gp_place)
+        hipLaunchKernelGGL(k_gp_count_loc, dim3(blocks_for((size_t)nw, BLOCK)), dim3(BLOCK), 0, s, a, (const int *)ctx->wlist.p, nw,
+                           cnt, (uint8_t *)ctx->gp_cb.p, (uint8_t *)ctx->gp_cb.p + wc, loc);
+    else
+        hipLaunchKernelGGL(k_gp_count, dim3(blocks_for((size_t)nw, BLOCK)), dim3(BLOCK), 0, s, a, (const int *)ctx->wlist.p, nw, cnt,
+                           (uint8_t *)ctx->gp_cb.p, (uint8_t *)ctx->gp_cb.p + wc);
     int st;
     if ((st = exclusive_scan_int(ctx, cnt, cur, HW + 1))) return st == APD_ENOMEM ? APD_OK : st;
     int nrefs = 0;
     HIP_OK(ctx, hipMemcpyAsync(&nrefs, cur + HW, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_OK(ctx, hipMemcpyAsync(cnt, cur, HW * sizeof(int), hipMemcpyDeviceToDevice, s));  // fill cursors
-    hipLaunchKernelGGL(k_gp_fill, dim3(blocks_for((size_t)nw, BLOCK)), dim3(BLOCK), 0, s, a, (const int *)ctx->wlist.p, nw, cnt,
-                       (uint32_t *)ctx->gp_refs.p);
+    if (ctx->gp_place) {
+        hipLaunchKernelGGL(k_gp_place, dim3(blocks_for((size_t)nw, BLOCK)), dim3(BLOCK), 0, s, a, (const int *)ctx->wlist.p, nw,
+                           (const int *)cur, (const uint8_t *)ctx->gp_cb.p + wc, (const uint32_t *)loc, (uint32_t *)ctx->gp_refs.p);
+    } else {
+        HIP_OK(ctx, hipMemcpyAsync(cnt, cur, HW * sizeof(int), hipMemcpyDeviceToDevice, s));  // fill cursors
+        hipLaunchKernelGGL(k_gp_fill, dim3(blocks_for((size_t)nw, BLOCK)), dim3(BLOCK), 0, s, a, (const int *)ctx->wlist.p, nw, cnt,
+                           (uint32_t *)ctx->gp_refs.p);
+    }
     HIP_OK(ctx, hipStreamSynchronize(s));
     if (nrefs <= 0) { ctx->gp_on = true; return check_launch(ctx, "pair table"); }
     // window anchors with references -> one dedup workgroup each
@@ -4519,9 +4598,18 @@ static int build_global_pairs(apd_ctx *ctx, int nw) {
         const size_t pcap = std::min<size_t>((size_t)nrefs * ctx->gp_cap_factor, (size_t)INT32_MAX);
         if (try_ensure(ctx, ctx->gp_plist, pcap * sizeof(int2))) {
             HIP_OK(ctx, hipMemsetAsync(acnt, 0, sizeof(int), s));
-            hipLaunchKernelGGL((k_gp_dedup<2>), dim3(ntask), dim3(GP_CHUNK), 0, s, a, (const int *)tasks, (const int *)cur,
-                               (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, acnt, (const int *)nullptr,
-                               (int2 *)ctx->gp_plist.p, (uint32_t *)ctx->gp_pidx.p, (int)pcap);
+            if (ctx->gp_small) {
+                hipLaunchKernelGGL((k_gp_dedup<2, GP_SMALL_HS, WAVE, 1>), dim3(ntask), dim3(WAVE), 0, s, a, (const int *)tasks,
+                                   (const int *)cur, (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, acnt,
+                                   (const int *)nullptr, (int2 *)ctx->gp_plist.p, (uint32_t *)ctx->gp_pidx.p, (int)pcap);
+                hipLaunchKernelGGL((k_gp_dedup<2, GP_HS, GP_CHUNK, 2>), dim3(ntask), dim3(GP_CHUNK), 0, s, a, (const int *)tasks,
+                                   (const int *)cur, (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, acnt,
+                                   (const int *)nullptr, (int2 *)ctx->gp_plist.p, (uint32_t *)ctx->gp_pidx.p, (int)pcap);
+            } else {
+                hipLaunchKernelGGL((k_gp_dedup<2>), dim3(ntask), dim3(GP_CHUNK), 0, s, a, (const int *)tasks, (const int *)cur,
+                                   (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, acnt, (const int *)nullptr,
+                                   (int2 *)ctx->gp_plist.p, (uint32_t *)ctx->gp_pidx.p, (int)pcap);
+            }
             HIP_OK(ctx, hipMemcpyAsync(&npairs, acnt, sizeof(int), hipMemcpyDeviceToHost, s));
             HIP_OK(ctx, hipStreamSynchronize(s));
             if ((st = check_launch(ctx, "pair table"))) return st;
