@@ -13,7 +13,11 @@ median over a fresh run's iterations): before every block of (up to) 3 steps the
 re-uploaded and re-initialised (apd_set_problem + apd_stage_prepare, outside the timed region), so
 no step repeats an iteration on an already-converged view. Each block is bracketed by a barrier and
 a device synchronisation, and the blocks' times are summed; inputs are resident in HBM throughout.
-value = W*H*steps summed over ranks / max-over-ranks time.
+The per-pass image-wide pair table (built in apd_stage_prepare; it replaces candidate work the
+reference does inside every CheckerboardPropagationWeak, APD.cu:1442-1615) is charged to the steps:
+each block adds its own build's HIP-event time x (its steps / 3).
+value = W*H*steps summed over ranks / max-over-ranks (timed steps + charged pair tables);
+mpix_s_iter_loop is the same without the pair tables (the loop body alone).
 
 Multi-GPU (weak scaling): one process per GPU. `python3 bench.py --gpus N` outside a
 torch.distributed launch starts its N ranks itself (a torch.distributed.run child on 127.0.0.1,
@@ -22,9 +26,10 @@ driver's own torch.distributed.run it runs as one rank. Each rank runs its own r
 (rank mod #views) of the same final-round pass with its own priors. Within a pass the reference
 views are independent given the previous pass's view states (APD.cpp:592-610), and
 the scan runner (apde-mvs_amd/scan_runner.py) ends every pass with ONE all-gather of the
-new states ([6, H, W] fp32 per view: depth, normal xyz, pixel state, confidence). The bench does the
-same inside the timed region: every block of fresh iterations (one pass's loop body) ends with that
-all-gather over RCCL (xGMI), so `value` at N > 1 pays the exchange; `exchange_ms` is the median of
+new states (18 B/px on the wire: depth + normal xyz f32, pixel state + confidence u8). The bench does
+the same inside the timed region: a scan pass gives every rank ceil(scan_views / N) problems, so after
+that many blocks of fresh iterations (and after the last block) the ranks all-gather the states they
+produced over RCCL (xGMI), and `value` at N > 1 pays the exchange; `exchange_ms` is the median of
 separately timed all-gathers (barrier, then the collective alone) and `rank_ms_per_step` the ranks'
 own per-step times (the value uses the max over ranks).
 
@@ -35,7 +40,8 @@ Besides the headline the JSON line carries:
                 geometric terms x 80, both counted on the device for the evaluations
                 CheckerboardPropagationWeak uses (apd_profile_counters), / their summed launch time from
                 HIP events on the engine stream, against the FP32 vector peak; HBM bytes per launch from
-                the newest rocprofv3 PMC summary of k_sweep_weak_vm at this shape under profiles/.
+                the rocprofv3 PMC summary of k_sweep_weak_vm at this shape under profiles/ whose
+                source_hash matches this tree's kernel sources (else traffic is null).
   cpu_baseline  the C oracle (oracle/liboracle.so) on a bounded sample of the same workload: the
                 same scene rendered at W/4 x H/4 (1512x1008) with its textures scaled 4x in world
                 units (the headline's texture per pixel and WEAK fraction), N = 10, one APD iteration
@@ -164,6 +170,9 @@ def final_round_problem(sc, priors, ref, N, sa=False):
     return arr
 
 
+PREP_LOG = []  # the timed blocks' prepare-phase timings (apd_get_prepare_timing), reported in the line
+
+
 def timed_fresh_iterations(eng, arr, steps, warmup, barrier, exchange=None, exchange_every=1):
     """Warm-up, then `steps` loop-body iterations taken in blocks of one fresh run's iterations
     0..max_iterations-1; each block re-uploads and re-initialises the problem untimed, and is timed
@@ -188,11 +197,15 @@ def timed_fresh_iterations(eng, arr, steps, warmup, barrier, exchange=None, exch
     eng.synchronize()
     eng.profile_reset(True)
     elapsed, step_ms, done, pairs_ms, pending = 0.0, [], 0, 0.0, 0
+    PREP_LOG.clear()
     while done < steps:
         eng.set_problem(arr)
         eng.prepare()
         eng.synchronize()
-        pairs_ms += eng.prepare_timing().pairs_ms * min(iters, steps - done) / iters
+        pt = eng.prepare_timing()
+        PREP_LOG.append({"pairs_ms": round(pt.pairs_ms, 2), "lists_ms": round(pt.lists_ms, 2), "init_ms": round(pt.init_ms, 2),
+                         "prepare_ms": round(pt.prepare_ms, 2)})
+        pairs_ms += pt.pairs_ms * min(iters, steps - done) / iters
         barrier()
         t_block = time.perf_counter()
         t_prev = t_block
@@ -565,6 +578,7 @@ def main():
         exchange, exchange_timed, wire_bytes = state_exchange(tdist, torch, state, world, per_rank)
         exchange(per_rank)  # (first use: communicator setup out of the timed region)
     elapsed, step_ms, pairs_ms = timed_fresh_iterations(eng, arr, args.steps, args.warmup, barrier, exchange, per_rank)
+    PREP_LOG_HEADLINE = list(PREP_LOG)
     roof = weak_roofline(eng, args.steps, W, N)
     roof_strong_apd = strong_roofline(eng, W, N)
     eng.profile_reset(False)
@@ -652,6 +666,7 @@ def main():
             # cost) spread over the pass's iterations; the loop body alone:
             "mpix_s_iter_loop": round(value_loop, 3),
             "pairs_ms_per_pass": round(pairs_ms / args.steps * max(1, arr_iters()), 3),
+            "prepare_blocks": PREP_LOG_HEADLINE,
             "value_basis": "W*H*steps*n_gpus / (timed loop-body iterations + each pass's pair-table build "
                            "charged per iteration, max over ranks)",
             "multi_gpu": exch,
