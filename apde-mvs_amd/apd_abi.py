@@ -225,7 +225,7 @@ EXPORTS = ["apd_abi_version", "apd_device_count", "apd_create", "apd_destroy", "
            "apd_set_problem", "apd_run_patchmatch", "apd_stage_prepare", "apd_stage_iteration",
            "apd_stage_finish", "apd_synchronize", "apd_get_results", "apd_get_timing", "apd_get_prepare_timing", "apd_profile_reset",
            "apd_profile_query", "apd_profile_kernel", "apd_profile_counters", "apd_profile_evaluations", "apd_epilogue", "apd_device_alloc", "apd_device_free",
-           "apd_device_copy", "apd_device_copy_peer", "apd_device_mem_info", "apd_device_resize_nearest", "apd_result_device", "apd_fusion_create", "apd_fusion_destroy",
+           "apd_device_copy", "apd_device_copy_peer", "apd_device_bytes", "apd_device_mem_info", "apd_device_resize_nearest", "apd_result_device", "apd_fusion_create", "apd_fusion_destroy",
            "apd_fusion_last_error", "apd_fusion_set_views", "apd_fusion_weak_filter", "apd_fusion_consistency",
            "apd_fusion_tat_levels"]
 

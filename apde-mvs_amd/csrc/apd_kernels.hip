@@ -500,9 +500,12 @@ struct FastMod {
         return (uint32_t)__umul64hi(low, (uint64_t)d);
     }
 };
-// stage (SPLIT, [34][wc] words per WEAK index wi): [wi] the stream position << 6 | the number of
-// points (0: no RANSAC), [wc + wi] the pixel, [(2 + i) * wc + wi] point i (short2, dvalid order):
-// k_gen_anchors_fit runs the RANSAC
+// stage (SPLIT, one GA_STAGE_W-word row per WEAK index wi, so that k_gen_anchors_fit's wave reads its
+// pixel's row in one round trip): [0] the stream position << 6 | the number of points (0: no RANSAC),
+// [1] the pixel, [2 + 2 i] point i (short2, dvalid order) and [3 + 2 i] its depth (the plane's w, which
+// the RANSAC's get3d reads; nothing writes planes between the two kernels): k_gen_anchors_fit runs
+// the RANSAC
+#define GA_STAGE_W 66
 template <bool SPLIT>
 __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restrict__ stage, int wc) {
     const int c = blockIdx.x * BLOCK + threadIdx.x;
@@ -521,13 +524,16 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
     // loops), which is also the stage's dvalid order: SPLIT writes each point to its stage slot as it is
     // found instead of into a dynamically indexed private array (which lived in scratch memory)
     const size_t wi = (size_t)a.amap[c];
+    uint32_t *row = SPLIT ? stage + wi * GA_STAGE_W : nullptr;
     short2 sp[SPLIT ? 1 : 32];
     uint32_t dvalid = 0;
     if constexpr (!SPLIT)
         for (int i = 0; i < 32; ++i) sp[i] = make_short2(-1, -1);
     int odi = -1, nsp = 0;
     auto found = [&](int di, short2 p) {
-        if constexpr (SPLIT) stage[(size_t)(2 + nsp) * wc + wi] = (uint32_t)(uint16_t)p.x | ((uint32_t)(uint16_t)p.y << 16);
+        if constexpr (SPLIT)
+            *reinterpret_cast<uint2 *>(row + 2 + 2 * nsp) =
+                make_uint2((uint32_t)(uint16_t)p.x | ((uint32_t)(uint16_t)p.y << 16), __float_as_uint(a.plane[p.x + p.y * W].w));
         else sp[di] = p;
         dvalid |= 1u << di;
         nsp++;
@@ -615,12 +621,11 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
     }
     if (nsp <= 3) {
         a.reliable[c] = 0;
-        if constexpr (SPLIT) stage[wi] = 0u;
+        if constexpr (SPLIT) row[0] = 0u;
         return;
     }
     if constexpr (SPLIT) {
-        stage[wi] = (g.n << 6) | (uint32_t)nsp;  // (the points are in stage slots 2 .. 2 + nsp - 1)
-        stage[(size_t)wc + wi] = (uint32_t)c;
+        *reinterpret_cast<uint2 *>(row) = make_uint2((g.n << 6) | (uint32_t)nsp, (uint32_t)c);
         return;
     } else {
         short2 vp[32];
@@ -712,21 +717,25 @@ __global__ __launch_bounds__(GA_FIT_WAVES * WAVE) void k_gen_anchors_fit(Args a,
     const int lane = threadIdx.x & (WAVE - 1);
     const int wi = __builtin_amdgcn_readfirstlane(blockIdx.x * GA_FIT_WAVES + (int)(threadIdx.x >> 6));
     if (wi >= wc) return;
-    const uint32_t hdr = __builtin_amdgcn_readfirstlane(stage[wi]);
+    const uint32_t *row = stage + (size_t)wi * GA_STAGE_W;
+    // the row in one round trip: lane 0 the header and pixel, lane i + 1 point i and its depth
+    const uint2 rv = (lane <= 32) ? *reinterpret_cast<const uint2 *>(row + 2 * lane) : make_uint2(0u, 0u);
+    const uint32_t hdr = __builtin_amdgcn_readfirstlane(rv.x);
     const int vc = (int)(hdr & 63u);
     if (vc == 0) return;
-    const int c = __builtin_amdgcn_readfirstlane((int)stage[(size_t)wc + wi]);
+    const int c = __builtin_amdgcn_readfirstlane((int)rv.y);
     const int W = a.W;
     const int py = c / W, px = c - py * W;
     const float depth_diff = a.dmax - a.dmin;
     const APD_C Cam &cam = a.cams[0];
     // lane i: point i (X, Y, Z, packed position)
+    const uint32_t qi = (uint32_t)__shfl((int)rv.x, lane + 1), di = (uint32_t)__shfl((int)rv.y, lane + 1);
     float X[3] = {0.0f, 0.0f, 0.0f};
     uint32_t q = 0xFFFFFFFFu;
     if (lane < vc) {
-        q = stage[(size_t)(2 + lane) * wc + wi];
+        q = qi;
         const int qx = (int)(int16_t)(q & 0xFFFFu), qy = (int)(int16_t)(q >> 16);
-        get3d(cam, (float)qx, (float)qy, a.plane[qx + qy * W].w, X);
+        get3d(cam, (float)qx, (float)qy, __uint_as_float(di), X);
     }
     const float X0 = X[0], X1 = X[1], X2 = X[2];
     float Cw[3];
@@ -2599,6 +2608,7 @@ static_assert(GP_CLOSE > 0 && GP_HS >= 256 && 256 % GP_CHUNK == 0, "k_gp_dedup t
 // bound); their references fit one batch, so the table is the large kernel's single table
 #define GP_SMALL_N 64
 #define GP_SMALL_HS 1024
+#define GP_MEDIUM_HS 4096  // the medium class (GP_SMALL_N < n <= GP_CHUNK: one batch, <= 8 GP_CHUNK keys)
 static_assert(GP_SMALL_HS * 3 / 4 - 8 * GP_SMALL_N > 0 && 8 * GP_SMALL_N <= GP_SMALL_HS / 2, "small k_gp_dedup sizing");
 #define GP_NONE 0xFFFFFFFFu
 
@@ -2756,9 +2766,10 @@ __global__ __launch_bounds__(BLOCK) void k_gp_tasks(const int *__restrict__ off,
 // counter above pcap, builds the table again with the two passes. PASS 0 counts the distinct pairs
 // per anchor (acnt) and PASS 1 writes them from the scanned bases (abase): the fallback, and the
 // path APD_GP_TWO_PASS=1 forces. Pair ids are labels either way: the costs never depend on them.
-// SIZE (PASS 2): 0 = every task, 1 = the small ones only (n <= GP_SMALL_N; HS, CHUNK the small table),
-// 2 = the others only.
-template <int PASS, int HS = GP_HS, int CHUNK = GP_CHUNK, int SIZE = 0>
+// (PASS 2) the tasks with NLO < n <= NHI references only: the small ones (n <= GP_SMALL_N) in a one-wave
+// workgroup with a 1 k-slot table, the medium ones (n <= GP_CHUNK, one batch) in a 4 k-slot table
+// (24 KiB instead of 48 KiB of LDS), the others as before.
+template <int PASS, int HS = GP_HS, int CHUNK = GP_CHUNK, int NLO = -1, int NHI = 0x7fffffff>
 __global__ __launch_bounds__(CHUNK) void k_gp_dedup(Args a, const int *__restrict__ tasks, const int *__restrict__ off,
                                                     const uint32_t *__restrict__ refs, const uint8_t *__restrict__ cbw,
                                                     int *__restrict__ acnt,
@@ -2773,8 +2784,7 @@ __global__ __launch_bounds__(CHUNK) void k_gp_dedup(Args a, const int *__restric
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid >> 6;
     const int q = tasks[blockIdx.x];
     const int r0 = off[q], n = off[q + 1] - r0;
-    if (SIZE == 1 && n > GP_SMALL_N) return;
-    if (SIZE == 2 && n <= GP_SMALL_N) return;
+    if (n <= NLO || n > NHI) return;
     const int qx = q % a.W, qy = q / a.W;
     int cap = 256, lg = 8;
     while (cap < HS && cap < n * 16) { cap <<= 1; ++lg; }
@@ -3923,6 +3933,7 @@ struct apd_ctx {
     int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
     Args args{};
     bool loaded = false, prepared = false;
+    int optional_fallbacks = 0;    // optional buffers try_ensure could not allocate
     bool prep_timed = false;       // the prepare events (ev[0..3], ev[14], ev[15]) of the last apd_stage_prepare
     int dw_tile_w = 8;             // DepthToWeak pixel tile width (64 / tile height); APD_DW_TILE_W
     int tile_w = 16;               // sweep list tile width (tile = tile_w x 256/tile_w positions); APD_TILE_W
@@ -3936,7 +3947,7 @@ struct apd_ctx {
     int gp_np = 0;                 // its distinct pairs
     bool gp_one_pass = true;       // k_gp_dedup in one pass (atomic plist ranges); APD_GP_TWO_PASS=1: count + write
     bool gp_place = true;          // k_gp_count_loc + k_gp_place; APD_GP_FILL=1: k_gp_count + k_gp_fill (atomics twice)
-    bool gp_small = true;          // one-pass small anchors in one-wave workgroups; APD_GP_NO_SMALL=1: all in 256-thread ones
+    bool gp_small = true;          // one-pass small / medium anchors in smaller-table workgroups; APD_GP_NO_SMALL=1: all in the 48 KiB one
     int gp_cap_factor = 2;         // one-pass plist capacity in pairs per reference (8 after an overflow)
     bool lr_handover = true;       // LocalRefine reads DepthToWeak's samples; APD_NO_LR_HANDOVER=1 disables
     bool wcur_on = true;           // RandomInit keeps WEAK current-plane costs for iteration 0; APD_NO_WCUR=1 disables
@@ -4236,11 +4247,16 @@ void apd_destroy(apd_ctx *ctx) {
 
 const char *apd_last_error(const apd_ctx *ctx) { return ctx ? ctx->err.c_str() : g_global_err; }
 
-// ensure() for optional buffers: a failed allocation leaves no error behind (the caller falls back)
+// ensure() for optional buffers: a failed allocation leaves no error behind (the caller falls back to
+// a slower exact path); the first few are reported on stderr, since a device store sized too greedily
+// by the caller shows up here first
 static bool try_ensure(apd_ctx *ctx, DevBuf &b, size_t bytes) {
     if (ensure(ctx, b, bytes) == APD_OK) return true;
     (void)hipGetLastError();
     ctx->err.clear();
+    if (ctx->optional_fallbacks++ < 8)
+        fprintf(stderr, "apd: optional device buffer of %zu bytes not allocated on device %d: its exact fallback path runs\n",
+                bytes, ctx->device);
     return false;
 }
 
@@ -4599,12 +4615,14 @@ static int build_global_pairs(apd_ctx *ctx, int nw) {
         if (try_ensure(ctx, ctx->gp_plist, pcap * sizeof(int2))) {
             HIP_OK(ctx, hipMemsetAsync(acnt, 0, sizeof(int), s));
             if (ctx->gp_small) {
-                hipLaunchKernelGGL((k_gp_dedup<2, GP_SMALL_HS, WAVE, 1>), dim3(ntask), dim3(WAVE), 0, s, a, (const int *)tasks,
-                                   (const int *)cur, (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, acnt,
-                                   (const int *)nullptr, (int2 *)ctx->gp_plist.p, (uint32_t *)ctx->gp_pidx.p, (int)pcap);
-                hipLaunchKernelGGL((k_gp_dedup<2, GP_HS, GP_CHUNK, 2>), dim3(ntask), dim3(GP_CHUNK), 0, s, a, (const int *)tasks,
-                                   (const int *)cur, (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, acnt,
-                                   (const int *)nullptr, (int2 *)ctx->gp_plist.p, (uint32_t *)ctx->gp_pidx.p, (int)pcap);
+#define GP_DEDUP_ARGS                                                                                                        \
+    s, a, (const int *)tasks, (const int *)cur, (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, acnt,      \
+        (const int *)nullptr, (int2 *)ctx->gp_plist.p, (uint32_t *)ctx->gp_pidx.p, (int)pcap
+                hipLaunchKernelGGL((k_gp_dedup<2, GP_SMALL_HS, WAVE, -1, GP_SMALL_N>), dim3(ntask), dim3(WAVE), 0, GP_DEDUP_ARGS);
+                hipLaunchKernelGGL((k_gp_dedup<2, GP_MEDIUM_HS, GP_CHUNK, GP_SMALL_N, GP_CHUNK>), dim3(ntask), dim3(GP_CHUNK), 0,
+                                   GP_DEDUP_ARGS);
+                hipLaunchKernelGGL((k_gp_dedup<2, GP_HS, GP_CHUNK, GP_CHUNK>), dim3(ntask), dim3(GP_CHUNK), 0, GP_DEDUP_ARGS);
+#undef GP_DEDUP_ARGS
             } else {
                 hipLaunchKernelGGL((k_gp_dedup<2>), dim3(ntask), dim3(GP_CHUNK), 0, s, a, (const int *)tasks, (const int *)cur,
                                    (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, acnt, (const int *)nullptr,
@@ -4667,9 +4685,10 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         {
             Args ag = a;  // (profiling counters: instrumented builds of k_gen_anchors only)
             ag.evals = (ctx->prof && ctx->evals.p) ? (APD_G unsigned long long *)ctx->evals.p : nullptr;
-            // the RANSAC in its own kernel when the stage fits (34 words per WEAK pixel); else in k_gen_anchors
+            // the RANSAC in its own kernel when the stage fits (GA_STAGE_W words per WEAK pixel); else in k_gen_anchors
             const size_t wc = (size_t)std::max(ctx->weak_count, 1);
-            uint32_t *stage = (ctx->ga_split && ctx->weak_count > 0 && try_ensure(ctx, ctx->ga_stage, 34 * wc * sizeof(uint32_t)))
+            uint32_t *stage = (ctx->ga_split && ctx->weak_count > 0 &&
+                               try_ensure(ctx, ctx->ga_stage, (size_t)GA_STAGE_W * wc * sizeof(uint32_t)))
                                   ? (uint32_t *)ctx->ga_stage.p : nullptr;
             if (stage) {
                 hipLaunchKernelGGL(k_gen_anchors<true>, dim3(gpx), dim3(BLOCK), 0, s, ag, stage, (int)wc);
@@ -5168,6 +5187,21 @@ int32_t apd_device_copy_peer(apd_ctx *dst_ctx, void *dst, apd_ctx *src_ctx, cons
         HIP_OK(dst_ctx, hipMemcpyPeerAsync(dst, dst_ctx->device, src, src_ctx->device, bytes, dst_ctx->stream));
     }
     HIP_OK(dst_ctx, hipStreamSynchronize(dst_ctx->stream));
+    return APD_OK;
+}
+
+int32_t apd_device_bytes(apd_ctx *ctx, size_t *bytes) {
+    if (!ctx || !bytes) return APD_EINVAL;
+    const DevBuf *bufs[] = {&ctx->imgs, &ctx->quad, &ctx->depth, &ctx->views, &ctx->cams, &ctx->plane, &ctx->cost,
+                            &ctx->sel, &ctx->sel2, &ctx->vw, &ctx->weak, &ctx->conf, &ctx->sa, &ctx->amap, &ctx->anchors,
+                            &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
+                            &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g,
+                            &ctx->wcand, &ctx->arec, &ctx->ga_stage, &ctx->lrs, &ctx->wcur, &ctx->wlist, &ctx->gp_cb, &ctx->gp_cnt,
+                            &ctx->gp_cur, &ctx->gp_refs, &ctx->gp_ccnt, &ctx->gp_cbase, &ctx->gp_plist, &ctx->gp_pidx,
+                            &ctx->gp_pcost, &ctx->gp_tmp, &ctx->dpairs};
+    size_t t = 0;
+    for (const DevBuf *b : bufs) t += b->bytes;
+    *bytes = t;
     return APD_OK;
 }
 

@@ -272,6 +272,20 @@ struct DevStore {
     // bytes held; an allocation that fails (or would pass APD_DEVICE_STATE_CAP_MB, a test hook) makes
     // the caller fall back to the host path for that image / problem / view
     size_t used = 0, cap = (size_t)-1;
+    int share = 1;             // contexts on this store's device (they share its free memory)
+    size_t lib_peak = 0;       // the most device memory the library's own buffers held after a problem
+    bool cap_fixed = false;    // APD_DEVICE_STATE_CAP_MB (test hook): the cap is not resized
+    // After a problem: the cap follows the real footprint -- what the store holds plus this context's
+    // share of the free memory, less room for the library's buffers to grow on later problems (half
+    // of their peak, at least 2 GiB: the pair table and the hand-over vary with the WEAK fraction)
+    void resize_cap() {
+        size_t lb = 0, fb = 0, tb = 0;
+        if (cap_fixed || apd_device_bytes(ctx, &lb) != APD_OK || apd_device_mem_info(ctx, &fb, &tb) != APD_OK) return;
+        lib_peak = std::max(lib_peak, lb);
+        const size_t margin = std::max<size_t>((size_t)2 << 30, lib_peak / 2);
+        const size_t avail = fb / (size_t)std::max(1, share);
+        cap = used + (avail > margin ? avail - margin : 0);
+    }
 
     bool reserve(Map &m, size_t bytes) {
         if (m.p && m.bytes >= bytes) return true;
@@ -737,6 +751,7 @@ bool Driver::process(apd_ctx *ctx, Job &job) {
         return process(ctx, job);
     }
     if (st != APD_OK) { SAY("RunPatchMatch failed: " << apd_last_error(ctx)); return false; }
+    if (dev) dev->resize_cap();
     const long ms = (long)std::chrono::duration_cast<std::chrono::milliseconds>(t1 - t0).count();
     {
         std::lock_guard<std::mutex> g(g_print);
@@ -992,6 +1007,7 @@ int main(int argc, char **argv) {
         // still runs out releases its context's store (process())
         std::map<int, int> per_dev;
         for (int d : gpus) per_dev[d]++;
+        auto share_of = [&](int dev_id) { return per_dev[dev_id]; };
         for (size_t k = 0; k < ctxs.size(); ++k) {
             auto d = std::make_unique<DevStore>();
             d->ctx = ctxs[k];
@@ -1001,7 +1017,11 @@ int main(int argc, char **argv) {
                 const size_t room = std::max<size_t>((size_t)16 << 30, fb / 4) * share;
                 d->cap = fb > room ? (fb - room) / share : 0;
             }
-            if (const char *e = getenv("APD_DEVICE_STATE_CAP_MB")) d->cap = (size_t)std::max(0L, atol(e)) << 20;
+            d->share = share_of(gpus[k]);
+            if (const char *e = getenv("APD_DEVICE_STATE_CAP_MB")) {
+                d->cap = (size_t)std::max(0L, atol(e)) << 20;
+                d->cap_fixed = true;
+            }
             drv.devs.push_back(std::move(d));
         }
     }

@@ -219,8 +219,11 @@ int32_t apd_get_prepare_timing(apd_ctx *ctx, apd_timing *timing);
    kind since the reset. apd_profile_query == apd_profile_kernel(APD_PROF_STRONG_SWEEP). */
 #define APD_PROF_STRONG_SWEEP 0 /* k_sweep_strong_vm (CheckerboardPropagationStrong, APD.cu:1098-1440) */
 #define APD_PROF_RANSAC_FIT 1   /* k_ransac_fit (RANSACToGetFitPlane, APD.cu:2486-2598)             */
-#define APD_PROF_WEAK_CAND 2    /* the Weak sweep's anchor candidates: k_gp_cost + k_weak_cand_g +
-                                   k_weak_cand_comb (the image-wide pair table)                      */
+#define APD_PROF_WEAK_CAND 2    /* the Weak sweep's anchor candidates: the SUM of the kernel brackets
+                                   of k_gp_cost + k_weak_cand_g + k_weak_cand_comb (the image-wide pair
+                                   table). k_gp_cost runs on side stream 1 beside k_weak_cand_g, so
+                                   with overlap this counts the overlapped time twice: it is not an
+                                   elapsed time -- rate math uses APD_PROF_WEAK_PATH              */
 #define APD_PROF_WEAK_SWEEP 3   /* k_sweep_weak_vm (CheckerboardPropagationWeak, APD.cu:1442-1615)   */
 #define APD_PROF_DEPTH_TO_WEAK 4 /* k_depth_to_weak_vm (DepthToWeak, APD.cu:2103-2250)                */
 #define APD_PROF_GP_COST 5      /* k_gp_cost alone (pair windows, inside APD_PROF_WEAK_CAND)         */
@@ -267,6 +270,9 @@ int32_t apd_device_free(apd_ctx *ctx, void *ptr);
 int32_t apd_device_copy(apd_ctx *ctx, void *dst, const void *src, size_t bytes);
 /* Free and total bytes of the ctx's device (hipMemGetInfo): the `apd` binary sizes its
    device-resident store from it, leaving room for the library's per-problem buffers. */
+/* Device memory the ctx's own buffers hold (bytes): the `apd` binary sizes its device store from it. */
+int32_t apd_device_bytes(apd_ctx *ctx, size_t *bytes);
+
 /* Copy `bytes` from device memory of src_ctx's device to device memory of dst_ctx's device (the same
    device, or a peer over xGMI with peer access enabled on first use); waits for the copy. The `apd`
    binary moves a Jacobi pass's new view maps between its contexts' device stores with it. */

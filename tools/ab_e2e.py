@@ -21,7 +21,7 @@ for r in range(ROUNDS):
         e.set_problem(arr)
         e.run()
         t = e.timing()
-        res[name].append((t.total_ms, t.init_ms, t.sweep_ms, t.post_ms))
+        res[name].append((t.total_ms, t.prepare_ms, t.sweep_ms, t.post_ms))  # (total = prepare + sweep + post)
 for name, v in res.items():
     med = [statistics.median(x[i] for x in v) for i in range(4)]
-    print(f"{name}: total {med[0]:.2f} ms  init {med[1]:.2f}  sweep {med[2]:.2f}  post {med[3]:.2f}", flush=True)
+    print(f"{name}: total {med[0]:.2f} ms  prepare {med[1]:.2f}  sweep {med[2]:.2f}  post {med[3]:.2f}", flush=True)

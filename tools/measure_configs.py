@@ -47,7 +47,8 @@ def time_problem(eng, arr, gt):
     iters = list(t.iter_ms)[: t.iterations]
     hw = arr.width * arr.height
     r = {"run_patchmatch_ms": round(t.total_ms, 1), "iter_ms": [round(x, 2) for x in iters],
-         "init_ms": round(t.init_ms, 1), "anchors_ms": round(t.anchors_ms, 1), "sweep_ms": round(t.sweep_ms, 1),
+         "prepare_ms": round(t.prepare_ms, 1), "init_ms_beside": round(t.init_ms, 1), "anchors_ms": round(t.anchors_ms, 1),
+         "sweep_ms": round(t.sweep_ms, 1),
          "post_ms": round(t.post_ms, 1),
          "mpix_s_iter": round(hw / (statistics.median(iters) * 1e-3) / 1e6, 2) if iters else None,
          "mpix_s_e2e": round(hw * t.iterations / (t.total_ms * 1e-3) / 1e6, 2)}
