@@ -518,8 +518,10 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
     const APD_C Cam &cam = a.cams[0];
     APD_G short2 *anc = a.anchors + (size_t)a.amap[c] * 9;
     Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_ANCHORS);
-    for (int i = 0; i < 9; ++i) anc[i] = make_short2(-1, -1);
-    anc[0] = make_short2((short)px, (short)py);
+    if constexpr (!SPLIT) {  // (SPLIT: k_gen_anchors_fit writes the whole row, coalesced)
+        for (int i = 0; i < 9; ++i) anc[i] = make_short2(-1, -1);
+        anc[0] = make_short2((short)px, (short)py);
+    }
     // the search finds its points in direction-slot order (di = odi * 4 + ri increases through the
     // loops), which is also the stage's dvalid order: SPLIT writes each point to its stage slot as it is
     // found instead of into a dynamically indexed private array (which lived in scratch memory)
@@ -555,21 +557,39 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
                     // (attempt 1 succeeds) or 16 (all fail), exactly as the general search below.
                     float ddx = dx * 20 + (float)0, ddy = dy * 20 + (float)0;
                     normalize2(ddx, ddy);
-                    for (int radius = 2; radius <= APD_MAX_SEARCH_RADIUS; radius = min(radius * 2, radius + 25)) {
-                        float tx = (float)px + dx * (float)radius, ty = (float)py + dy * (float)radius;
-                        if (tx < 0 || ty < 0 || tx >= (float)W || ty >= (float)H) break;
-                        const int ax = (int16_t)(int)((float)px + ddx * (float)radius);
-                        const int ay = (int16_t)(int)((float)py + ddy * (float)radius);
-                        bool ok = !(ax < margin || ay < margin || ax >= W - margin || ay >= H - margin);
-                        const short2 nn = ok ? a.nearest[ax + ay * W] : make_short2(-1, -1);
-                        ok = ok && !(nn.x == -1 || nn.y == -1);
-                        if (ok) {
-                            float tdx = (float)(nn.x - px), tdy = (float)(nn.y - py);
-                            normalize2(tdx, tdy);
-                            ok = tdx * dx + tdy * dy > a.anc_thr;
+                    // the radii in groups of GA_RADII: their lookups are issued together (the later ones
+                    // speculatively -- 95 % of the steps fail at C3, so they are almost always needed),
+                    // then judged in radius order with the sequential loop's stop rules
+                    constexpr int GA_RADII = 4;
+                    bool done_dir = false;
+                    for (int r0 = 2; !done_dir && r0 <= APD_MAX_SEARCH_RADIUS;) {
+                        int rad[GA_RADII];
+                        bool inimg[GA_RADII], inm[GA_RADII];
+                        short2 nn[GA_RADII];
+#pragma unroll
+                        for (int t = 0; t < GA_RADII; ++t) {
+                            rad[t] = (t == 0) ? r0 : min(rad[t - 1] * 2, rad[t - 1] + 25);
+                            const float tx = (float)px + dx * (float)rad[t], ty = (float)py + dy * (float)rad[t];
+                            inimg[t] = rad[t] <= APD_MAX_SEARCH_RADIUS && !(tx < 0 || ty < 0 || tx >= (float)W || ty >= (float)H);
+                            const int ax = (int16_t)(int)((float)px + ddx * (float)rad[t]);
+                            const int ay = (int16_t)(int)((float)py + ddy * (float)rad[t]);
+                            inm[t] = inimg[t] && !(ax < margin || ay < margin || ax >= W - margin || ay >= H - margin);
+                            nn[t] = inm[t] ? a.nearest[ax + ay * W] : make_short2(-1, -1);
                         }
-                        g.n += ok ? 4u : 16u;
-                        if (ok) { found(di, nn); break; }
+#pragma unroll
+                        for (int t = 0; t < GA_RADII; ++t) {
+                            if (done_dir) continue;
+                            if (!inimg[t]) { done_dir = true; continue; }  // (the loop's break / end of radii)
+                            bool ok = inm[t] && !(nn[t].x == -1 || nn[t].y == -1);
+                            if (ok) {
+                                float tdx = (float)(nn[t].x - px), tdy = (float)(nn[t].y - py);
+                                normalize2(tdx, tdy);
+                                ok = tdx * dx + tdy * dy > a.anc_thr;
+                            }
+                            g.n += ok ? 4u : 16u;
+                            if (ok) { found(di, nn[t]); done_dir = true; }
+                        }
+                        r0 = min(rad[GA_RADII - 1] * 2, rad[GA_RADII - 1] + 25);
                     }
                 } else
                 for (int radius = 2; radius <= APD_MAX_SEARCH_RADIUS; radius = min(radius * 2, radius + 25)) {
@@ -621,7 +641,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
     }
     if (nsp <= 3) {
         a.reliable[c] = 0;
-        if constexpr (SPLIT) row[0] = 0u;
+        if constexpr (SPLIT) *reinterpret_cast<uint2 *>(row) = make_uint2(0u, (uint32_t)c);
         return;
     }
     if constexpr (SPLIT) {
@@ -722,10 +742,14 @@ __global__ __launch_bounds__(GA_FIT_WAVES * WAVE) void k_gen_anchors_fit(Args a,
     const uint2 rv = (lane <= 32) ? *reinterpret_cast<const uint2 *>(row + 2 * lane) : make_uint2(0u, 0u);
     const uint32_t hdr = __builtin_amdgcn_readfirstlane(rv.x);
     const int vc = (int)(hdr & 63u);
-    if (vc == 0) return;
     const int c = __builtin_amdgcn_readfirstlane((int)rv.y);
     const int W = a.W;
     const int py = c / W, px = c - py * W;
+    // the pixel's anchor row (APD.cu:1890-1893: anchor 0 the pixel, the others none until the RANSAC
+    // orders its inliers below), one coalesced store instead of the search kernel's nine
+    APD_G short2 *anc = a.anchors + (size_t)wi * 9;
+    if (lane < 9) anc[lane] = lane == 0 ? make_short2((short)px, (short)py) : make_short2(-1, -1);
+    if (vc == 0) return;
     const float depth_diff = a.dmax - a.dmin;
     const APD_C Cam &cam = a.cams[0];
     // lane i: point i (X, Y, Z, packed position)
@@ -744,9 +768,16 @@ __global__ __launch_bounds__(GA_FIT_WAVES * WAVE) void k_gen_anchors_fit(Args a,
     const Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_ANCHORS);
     const FastMod fm((uint32_t)vc);
     const uint32_t d0 = (hdr >> 6) + 3u * (uint32_t)lane;
-    const int ia = (int)fm.mod(rng_draw(g, d0));
-    const int ib = (int)fm.mod(rng_draw(g, d0 + 1u));
-    const int ic = (int)fm.mod(rng_draw(g, d0 + 2u));
+    // the three draws d0 .. d0 + 2 lie in Philox blocks d0 / 4 and (d0 + 2) / 4: two blocks, not three
+    const uint4 b0 = g.block(d0 >> 2), b1 = g.block((d0 + 2u) >> 2);
+    auto pick = [&](uint32_t d) {
+        const uint4 b = (d >> 2) == (d0 >> 2) ? b0 : b1;
+        const uint32_t j = d & 3u;
+        return j == 0 ? b.x : (j == 1 ? b.y : (j == 2 ? b.z : b.w));
+    };
+    const int ia = (int)fm.mod(pick(d0));
+    const int ib = (int)fm.mod(pick(d0 + 1u));
+    const int ic = (int)fm.mod(pick(d0 + 2u));
     bool ok = lane < 50 && !(ia == ib || ib == ic || ia == ic);
     const float Ax = __shfl(X0, ia), Ay = __shfl(X1, ia), Az = __shfl(X2, ia);
     const float Bx = __shfl(X0, ib), By = __shfl(X1, ib), Bz = __shfl(X2, ib);
@@ -810,7 +841,6 @@ __global__ __launch_bounds__(GA_FIT_WAVES * WAVE) void k_gen_anchors_fit(Args a,
         const float wj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wgt), j));
         rank += (wj < wgt || (wj == wgt && j < lane)) ? 1 : 0;
     }
-    APD_G short2 *anc = a.anchors + (size_t)wi * 9;
     if (lane < vc && rank < 8) anc[1 + rank] = make_short2((short)(vq & 0xFFFFu), (short)(vq >> 16));
     if (lane == 0) a.reliable[c] = 1;
 }

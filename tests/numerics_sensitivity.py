@@ -45,6 +45,19 @@ def epilogue_depth(out, arr):
     return d, n, w
 
 
+def flat_window_frac(arr, sel):
+    """Fraction of the pixels in `sel` whose 6x6 step-2 reference window (clamped) is constant."""
+    ys, xs = np.nonzero(sel)
+    if ys.size == 0:
+        return None
+    img = np.asarray(arr.images[0], np.float32).reshape(arr.height, arr.width)
+    off = np.arange(-5, 6, 2)
+    yy = np.clip(ys[:, None, None] + off[None, :, None], 0, arr.height - 1)
+    xx = np.clip(xs[:, None, None] + off[None, None, :], 0, arr.width - 1)
+    w = img[yy, xx].reshape(ys.size, -1)
+    return round(float((w.max(1) == w.min(1)).mean()), 6)
+
+
 def metrics(c, f, arr, gt=None):
     dc, nc, wc = epilogue_depth(c, arr)
     df, nf, wf = epilogue_depth(f, arr)
@@ -70,6 +83,10 @@ def metrics(c, f, arr, gt=None):
         "validity_mask_identical": bool((mc == mf).all()),
         "validity_mask_agree_frac": round(float((mc == mf).mean()), 6),
         "validity_mask_differing_pixels": int((mc != mf).sum()),
+        # of those, the pixels whose reference window (NCC-Old's 6x6 taps, step 2) is exactly flat: its
+        # variance is 0 in IEEE arithmetic, the NCC 0/0, while an approximate reciprocal leaves a tiny
+        # variance and a finite cost (the synthetic scenes' constant-intensity patches)
+        "validity_mask_differing_flat_window_frac": flat_window_frac(arr, mc != mf),
         "validity_frac": round(float(mc.mean()), 6),
         "depth_in_range_identical": bool((vc == vf).all()),
         "depth_in_range_agree_frac": round(float((vc == vf).mean()), 6),
