@@ -2710,23 +2710,46 @@ __global__ __launch_bounds__(BLOCK) void k_gp_count_loc(Args a, const int *__res
     const int wi = a.amap[c];
     const int cid = a.sa_any ? (int)a.sa[c] : 0;
     const APD_G short2 *anc = a.anchors + (size_t)wi * 9;
-    uint32_t cb = 0, wm = 0;
-#pragma unroll 1
-    for (int k = 1; k < 9; ++k) {
-        const short2 ap = anc[k];
-        const bool valid = act && !(ap.x == -1 || ap.y == -1);
-        const int q = valid ? ap.x + ap.y * a.W : -1;
-        if (valid && a.weak[q] == APD_STRONG) cb |= 1u << (k - 1);
-        const bool ok = valid && gp_window_used(a, cid, q);
-        if (ok) wm |= 1u << (k - 1);
-        int hl, rk, len;
-        gp_run(ok, q, hl, rk, len);
-        int pos = 0;
-        if (ok && rk == 0) pos = atomicAdd(&cnt[q], len);
-        pos = __shfl(pos, hl) + rk;
-        if (ok) loc[(size_t)wi * 8 + (k - 1)] = (uint32_t)pos;
+    // every load of the 8 windows first (anchors, their states and labels), then the 8 runs and their
+    // atomics, all in flight together: the kernel is latency bound (counters: 1 % of wave time active)
+    short2 ap[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ap[k] = anc[k + 1];
+    int q[8];
+    bool valid[8];
+    uint8_t wst[8];
+    int lab[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        valid[k] = act && !(ap[k].x == -1 || ap[k].y == -1);
+        q[k] = valid[k] ? ap[k].x + ap[k].y * a.W : -1;
+        wst[k] = valid[k] ? a.weak[q[k]] : (uint8_t)0;
+        lab[k] = (valid[k] && a.sa_any) ? (int)a.sa[q[k]] : 0;
     }
-    if (act) { cbw[wi] = (uint8_t)cb; wmw[wi] = (uint8_t)wm; }
+    uint32_t cb = 0, wm = 0;
+    int pos[8];
+    bool okk[8];
+    int hl[8], rk[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (valid[k] && wst[k] == APD_STRONG) cb |= 1u << k;
+        okk[k] = valid[k] && (cid == 0 || lab[k] == cid);  // (gp_window_used)
+        if (okk[k]) wm |= 1u << k;
+        int len;
+        gp_run(okk[k], q[k], hl[k], rk[k], len);
+        pos[k] = 0;
+        if (okk[k] && rk[k] == 0) pos[k] = atomicAdd(&cnt[q[k]], len);
+    }
+    uint32_t l[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) l[k] = (uint32_t)(__shfl(pos[k], hl[k]) + rk[k]);  // (k_gp_place reads used windows only)
+    if (act) {
+        uint4 *d = reinterpret_cast<uint4 *>(loc + (size_t)wi * 8);
+        d[0] = make_uint4(l[0], l[1], l[2], l[3]);
+        d[1] = make_uint4(l[4], l[5], l[6], l[7]);
+        cbw[wi] = (uint8_t)cb;
+        wmw[wi] = (uint8_t)wm;
+    }
 }
 // references (WEAK index * 8 + window slot k - 1, bit 31: filtered by the SA label) into their
 // window anchor's segment
@@ -2853,9 +2876,15 @@ __global__ __launch_bounds__(CHUNK) void k_gp_dedup(Args a, const int *__restric
                 const uint32_t key = qh[h];
                 uint32_t sl = slot_of(key);
                 for (;;) {
-                    const uint32_t old = atomicCAS(&hs[sl], 0u, key);
-                    if (old == 0u) { ++fresh; break; }
-                    if (old == key) break;
+                    // most of an anchor's references share their candidates: a plain read finds the key
+                    // already inserted without an LDS atomic (same-address atomics serialise)
+                    const uint32_t cur = hs[sl];
+                    if (cur == key) break;
+                    if (cur == 0u) {
+                        const uint32_t old = atomicCAS(&hs[sl], 0u, key);
+                        if (old == 0u) { ++fresh; break; }
+                        if (old == key) break;
+                    }
                     sl = (sl + 1) & msk;
                 }
             }
