@@ -557,39 +557,23 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
                     // (attempt 1 succeeds) or 16 (all fail), exactly as the general search below.
                     float ddx = dx * 20 + (float)0, ddy = dy * 20 + (float)0;
                     normalize2(ddx, ddy);
-                    // the radii in groups of GA_RADII: their lookups are issued together (the later ones
-                    // speculatively -- 95 % of the steps fail at C3, so they are almost always needed),
-                    // then judged in radius order with the sequential loop's stop rules
-                    constexpr int GA_RADII = 4;
-                    bool done_dir = false;
-                    for (int r0 = 2; !done_dir && r0 <= APD_MAX_SEARCH_RADIUS;) {
-                        int rad[GA_RADII];
-                        bool inimg[GA_RADII], inm[GA_RADII];
-                        short2 nn[GA_RADII];
-#pragma unroll
-                        for (int t = 0; t < GA_RADII; ++t) {
-                            rad[t] = (t == 0) ? r0 : min(rad[t - 1] * 2, rad[t - 1] + 25);
-                            const float tx = (float)px + dx * (float)rad[t], ty = (float)py + dy * (float)rad[t];
-                            inimg[t] = rad[t] <= APD_MAX_SEARCH_RADIUS && !(tx < 0 || ty < 0 || tx >= (float)W || ty >= (float)H);
-                            const int ax = (int16_t)(int)((float)px + ddx * (float)rad[t]);
-                            const int ay = (int16_t)(int)((float)py + ddy * (float)rad[t]);
-                            inm[t] = inimg[t] && !(ax < margin || ay < margin || ax >= W - margin || ay >= H - margin);
-                            nn[t] = inm[t] ? a.nearest[ax + ay * W] : make_short2(-1, -1);
+                    // (measured: lookups of four radii issued together, judged in order, made this
+                    // kernel slower at C3, 24.4 -> 32.1 ms: more registers, fewer waves in flight)
+                    for (int radius = 2; radius <= APD_MAX_SEARCH_RADIUS; radius = min(radius * 2, radius + 25)) {
+                        float tx = (float)px + dx * (float)radius, ty = (float)py + dy * (float)radius;
+                        if (tx < 0 || ty < 0 || tx >= (float)W || ty >= (float)H) break;
+                        const int ax = (int16_t)(int)((float)px + ddx * (float)radius);
+                        const int ay = (int16_t)(int)((float)py + ddy * (float)radius);
+                        bool ok = !(ax < margin || ay < margin || ax >= W - margin || ay >= H - margin);
+                        const short2 nn = ok ? a.nearest[ax + ay * W] : make_short2(-1, -1);
+                        ok = ok && !(nn.x == -1 || nn.y == -1);
+                        if (ok) {
+                            float tdx = (float)(nn.x - px), tdy = (float)(nn.y - py);
+                            normalize2(tdx, tdy);
+                            ok = tdx * dx + tdy * dy > a.anc_thr;
                         }
-#pragma unroll
-                        for (int t = 0; t < GA_RADII; ++t) {
-                            if (done_dir) continue;
-                            if (!inimg[t]) { done_dir = true; continue; }  // (the loop's break / end of radii)
-                            bool ok = inm[t] && !(nn[t].x == -1 || nn[t].y == -1);
-                            if (ok) {
-                                float tdx = (float)(nn[t].x - px), tdy = (float)(nn[t].y - py);
-                                normalize2(tdx, tdy);
-                                ok = tdx * dx + tdy * dy > a.anc_thr;
-                            }
-                            g.n += ok ? 4u : 16u;
-                            if (ok) { found(di, nn[t]); done_dir = true; }
-                        }
-                        r0 = min(rad[GA_RADII - 1] * 2, rad[GA_RADII - 1] + 25);
+                        g.n += ok ? 4u : 16u;
+                        if (ok) { found(di, nn); break; }
                     }
                 } else
                 for (int radius = 2; radius <= APD_MAX_SEARCH_RADIUS; radius = min(radius * 2, radius + 25)) {
@@ -793,12 +777,18 @@ __global__ __launch_bounds__(GA_FIT_WAVES * WAVE) void k_gen_anchors_fit(Args a,
         normalize3(cr);
         cr.w = -(cr.x * Ax + cr.y * Ay + cr.z * Az);
     }
+    // the points broadcast from LDS (one uniform-address read per point; v_readlane's SGPR results
+    // stalled the loop on their read-after-write hazards)
+    __shared__ float4 spts[GA_FIT_WAVES][WAVE];
+    __shared__ float swgt[GA_FIT_WAVES][WAVE];
+    const int wv = threadIdx.x >> 6;
+    spts[wv][lane] = make_float4(X0, X1, X2, 0.0f);
+    __builtin_amdgcn_wave_barrier();  // (LDS operations of one wave complete in order)
     int tcnt = 0;
-    for (int k = 0; k < vc; ++k) {  // (k uniform: the point's coordinates by readlane)
-        const float P0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(X0), k));
-        const float P1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(X1), k));
-        const float P2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(X2), k));
-        float d = fabsf(cr.x * P0 + cr.y * P1 + cr.z * P2 + cr.w);
+#pragma unroll 4
+    for (int k = 0; k < vc; ++k) {
+        const float4 P = spts[wv][k];
+        float d = fabsf(cr.x * P.x + cr.y * P.y + cr.z * P.z + cr.w);
         if (anc_inlier(a, d, depth_diff)) tcnt++;
     }
     ok = ok && tcnt >= 6;
@@ -836,9 +826,12 @@ __global__ __launch_bounds__(GA_FIT_WAVES * WAVE) void k_gen_anchors_fit(Args a,
             vq = q;
         }
     }
+    swgt[wv][lane] = wgt;
+    __builtin_amdgcn_wave_barrier();
     int rank = 0;
+#pragma unroll 4
     for (int j = 0; j < vc; ++j) {
-        const float wj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wgt), j));
+        const float wj = swgt[wv][j];
         rank += (wj < wgt || (wj == wgt && j < lane)) ? 1 : 0;
     }
     if (lane < vc && rank < 8) anc[1 + rank] = make_short2((short)(vq & 0xFFFFu), (short)(vq >> 16));
