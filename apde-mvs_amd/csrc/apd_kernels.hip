@@ -2815,22 +2815,24 @@ __global__ __launch_bounds__(BLOCK) void k_gp_tasks(const int *__restrict__ off,
 // (PASS 2) the tasks with NLO < n <= NHI references only: the small ones (n <= GP_SMALL_N) in a one-wave
 // workgroup with a 1 k-slot table, the medium ones (n <= GP_CHUNK, one batch) in a 4 k-slot table
 // (24 KiB instead of 48 KiB of LDS), the others as before.
-template <int PASS, int HS = GP_HS, int CHUNK = GP_CHUNK, int NLO = -1, int NHI = 0x7fffffff>
-__global__ __launch_bounds__(CHUNK) void k_gp_dedup(Args a, const int *__restrict__ tasks, const int *__restrict__ off,
-                                                    const uint32_t *__restrict__ refs, const uint8_t *__restrict__ cbw,
-                                                    int *__restrict__ acnt,
-                                                    const int *__restrict__ abase, int2 *__restrict__ plist,
-                                                    uint32_t *__restrict__ pidx, int pcap) {
+template <int HS, int CHUNK>
+struct GpLds {
+    uint32_t hs[HS];
+    uint16_t sid[HS];
+    int scan_w[CHUNK / WAVE + 1];
+    int nfresh, sbase, task;
+};
+// One window anchor q's references [r0, r0 + n) (see k_gp_dedup); `base` is PASS 1's first pair id.
+// Returns the distinct pairs of its tables (PASS 0). Every thread of the workgroup calls it; it ends
+// with a barrier, so a workgroup may run it for several anchors in turn.
+template <int PASS, int HS, int CHUNK>
+__device__ __forceinline__ int gp_dedup_task(const Args &a, GpLds<HS, CHUNK> &S, int q, int r0, int n, int base,
+                                             const uint32_t *__restrict__ refs, const uint8_t *__restrict__ cbw,
+                                             int *__restrict__ acnt, int2 *__restrict__ plist, uint32_t *__restrict__ pidx,
+                                             int pcap) {
     constexpr int CLOSE = HS * 3 / 4 - 8 * CHUNK;
     static_assert(CLOSE > 0 && HS >= 256 && HS % CHUNK == 0 && 256 % CHUNK == 0, "k_gp_dedup table sizing");
-    __shared__ uint32_t hs[HS];
-    __shared__ uint16_t sid[HS];
-    __shared__ int scan_w[CHUNK / WAVE + 1];
-    __shared__ int nfresh, sbase;
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid >> 6;
-    const int q = tasks[blockIdx.x];
-    const int r0 = off[q], n = off[q + 1] - r0;
-    if (n <= NLO || n > NHI) return;
     const int qx = q % a.W, qy = q / a.W;
     int cap = 256, lg = 8;
     while (cap < HS && cap < n * 16) { cap <<= 1; ++lg; }
@@ -2852,10 +2854,10 @@ __global__ __launch_bounds__(CHUNK) void k_gp_dedup(Args a, const int *__restric
         }
         return cb;
     };
-    for (int i = tid; i < cap; i += CHUNK) hs[i] = 0u;
-    if (tid == 0) nfresh = 0;
+    for (int i = tid; i < cap; i += CHUNK) S.hs[i] = 0u;
+    if (tid == 0) S.nfresh = 0;
     __syncthreads();
-    int base = PASS == 1 ? abase[blockIdx.x] : 0, total = 0;
+    int total = 0;
     int run0 = 0;  // first reference of the open table
     for (int b0 = 0; b0 < n; b0 += CHUNK) {
         const int r = b0 + tid;
@@ -2871,55 +2873,55 @@ __global__ __launch_bounds__(CHUNK) void k_gp_dedup(Args a, const int *__restric
                 for (;;) {
                     // most of an anchor's references share their candidates: a plain read finds the key
                     // already inserted without an LDS atomic (same-address atomics serialise)
-                    const uint32_t cur = hs[sl];
+                    const uint32_t cur = S.hs[sl];
                     if (cur == key) break;
                     if (cur == 0u) {
-                        const uint32_t old = atomicCAS(&hs[sl], 0u, key);
+                        const uint32_t old = atomicCAS(&S.hs[sl], 0u, key);
                         if (old == 0u) { ++fresh; break; }
                         if (old == key) break;
                     }
                     sl = (sl + 1) & msk;
                 }
             }
-            if (fresh) atomicAdd(&nfresh, fresh);
+            if (fresh) atomicAdd(&S.nfresh, fresh);
         }
         __syncthreads();
-        const int nd = nfresh;
-        // every thread has read nfresh before any wave's next-batch inserts can add to it (else
+        const int nd = S.nfresh;
+        // every thread has read S.nfresh before any wave's next-batch inserts can add to it (else
         // `close` and `base` could differ between waves)
         __syncthreads();
         const bool close = nd >= CLOSE || b0 + CHUNK >= n;
         if (!close) continue;  // (uniform)
         if (PASS == 2) {
-            if (tid == 0) sbase = atomicAdd(acnt, nd);
+            if (tid == 0) S.sbase = atomicAdd(acnt, nd);
             __syncthreads();
-            base = sbase;
+            base = S.sbase;
         }
         if (PASS >= 1) {
             // plist[base + id] = (window anchor, candidate anchor)
             const int per = cap / CHUNK;  // slots per thread (cap >= CHUNK)
             const int s0 = tid * per, s1 = s0 + per;
             int c = 0;
-            for (int sl = s0; sl < s1; ++sl) c += hs[sl] != 0u;
+            for (int sl = s0; sl < s1; ++sl) c += S.hs[sl] != 0u;
             int x = c;
 #pragma unroll
             for (int o = 1; o < WAVE; o <<= 1) {
                 const int y = __shfl_up(x, o);
                 if (lane >= o) x += y;
             }
-            if (lane == WAVE - 1) scan_w[wave] = x;
+            if (lane == WAVE - 1) S.scan_w[wave] = x;
             __syncthreads();
             int next = x - c;
-            for (int w = 0; w < wave; ++w) next += scan_w[w];
+            for (int w = 0; w < wave; ++w) next += S.scan_w[w];
             // ids in slot order (ranking the candidates by raster position, so that a group's pixels
             // read neighbouring rows of pcost, measured: k_weak_cand_g -1 %, this pass +93 %)
             for (int sl = s0; sl < s1; ++sl) {
-                const uint32_t key = hs[sl];
+                const uint32_t key = S.hs[sl];
                 if (!key) continue;
                 // (window anchor x | SA-filtered << 15 | y << 16, candidate anchor position)
                 if (PASS == 1 || base + next < pcap)
                     plist[base + next] = make_int2(qx | ((key & GP_FILT) ? 0x8000 : 0) | (qy << 16), (int)((key & ~GP_FILT) - 1u));
-                sid[sl] = (uint16_t)next;
+                S.sid[sl] = (uint16_t)next;
                 ++next;
             }
             __syncthreads();
@@ -2933,8 +2935,8 @@ __global__ __launch_bounds__(CHUNK) void k_gp_dedup(Args a, const int *__restric
                     if (!((cb >> h) & 1u)) continue;
                     const uint32_t key = qh[h];
                     uint32_t sl = slot_of(key);
-                    while (hs[sl] != key) sl = (sl + 1) & msk;
-                    pv[h] = (uint32_t)(base + sid[sl]);
+                    while (S.hs[sl] != key) sl = (sl + 1) & msk;
+                    pv[h] = (uint32_t)(base + S.sid[sl]);
                 }
                 uint4 *dst = reinterpret_cast<uint4 *>(pidx + ((size_t)wi * 8 + k) * 8);  // [WEAK index][window k][candidate h]
                 dst[0] = make_uint4(pv[0], pv[1], pv[2], pv[3]);
@@ -2945,12 +2947,75 @@ __global__ __launch_bounds__(CHUNK) void k_gp_dedup(Args a, const int *__restric
         if (PASS != 2) base += nd;
         total += nd;
         run0 = b0 + CHUNK;
-        for (int i = tid; i < cap; i += CHUNK) hs[i] = 0u;
+        for (int i = tid; i < cap; i += CHUNK) S.hs[i] = 0u;
         __syncthreads();
-        if (tid == 0) nfresh = 0;
+        if (tid == 0) S.nfresh = 0;
         __syncthreads();
     }
-    if (PASS == 0 && tid == 0) acnt[blockIdx.x] = total;
+    return total;
+}
+template <int PASS, int HS = GP_HS, int CHUNK = GP_CHUNK, int NLO = -1, int NHI = 0x7fffffff>
+__global__ __launch_bounds__(CHUNK) void k_gp_dedup(Args a, const int *__restrict__ tasks, const int *__restrict__ off,
+                                                    const uint32_t *__restrict__ refs, const uint8_t *__restrict__ cbw,
+                                                    int *__restrict__ acnt,
+                                                    const int *__restrict__ abase, int2 *__restrict__ plist,
+                                                    uint32_t *__restrict__ pidx, int pcap) {
+    __shared__ GpLds<HS, CHUNK> S;
+    const int q = tasks[blockIdx.x];
+    const int r0 = off[q], n = off[q + 1] - r0;
+    if (n <= NLO || n > NHI) return;
+    const int total = gp_dedup_task<PASS, HS, CHUNK>(a, S, q, r0, n, PASS == 1 ? abase[blockIdx.x] : 0, refs, cbw, acnt, plist,
+                                                     pidx, pcap);
+    if (PASS == 0 && threadIdx.x == 0) acnt[blockIdx.x] = total;
+}
+// The one-pass table without host round trips (apd_stage_prepare enqueues it whole, and
+// RandomInitialization runs beside it): the window anchors with references are dealt into three
+// size classes by k_gp_classes, and each class runs in a grid that fills the GPU, its workgroups
+// taking the class's anchors in turn -- DYN (the large class, whose anchors differ most in size): the
+// next anchor from an atomic counter; else every gridDim-th. The class's count is read from device
+// memory, and every workgroup leaves the loop when it passes it.
+#define GP_CLASSES 3
+__global__ __launch_bounds__(BLOCK) void k_gp_classes(const int *__restrict__ off, int HW, int cap, int *__restrict__ lists,
+                                                      int *__restrict__ counts) {
+    const int q = blockIdx.x * BLOCK + threadIdx.x;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int n = q < HW ? off[q + 1] - off[q] : 0;
+    const int cls = n <= GP_SMALL_N ? 0 : (n <= GP_CHUNK ? 1 : 2);
+#pragma unroll
+    for (int c = 0; c < GP_CLASSES; ++c) {
+        const uint64_t m = __ballot(n > 0 && cls == c);
+        if (!m) continue;
+        const int leader = __builtin_ctzll(m);
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&counts[c], __builtin_popcountll(m));
+        base = __shfl(base, leader);
+        if (n > 0 && cls == c) {
+            const int pos = base + __builtin_popcountll(m & ((1ull << lane) - 1ull));
+            if (pos < cap) lists[(size_t)c * cap + pos] = q;
+            else atomicOr(&counts[GP_CLASSES + 1], 1);  // (overflow: the host rebuilds synchronously)
+        }
+    }
+}
+template <int HS, int CHUNK, bool DYN>
+__global__ __launch_bounds__(CHUNK) void k_gp_dedup_q(Args a, const int *__restrict__ list, const int *__restrict__ count,
+                                                      int *__restrict__ next, const int *__restrict__ off,
+                                                      const uint32_t *__restrict__ refs, const uint8_t *__restrict__ cbw,
+                                                      int *__restrict__ acnt, int2 *__restrict__ plist, uint32_t *__restrict__ pidx,
+                                                      int pcap) {
+    __shared__ GpLds<HS, CHUNK> S;
+    const int ntask = *count;
+    for (int t = blockIdx.x;; t += gridDim.x) {
+        if (DYN) {
+            if (threadIdx.x == 0) S.task = atomicAdd(next, 1);
+            __syncthreads();
+            t = S.task;
+            __syncthreads();
+        }
+        if (t >= ntask) break;  // (uniform)
+        const int q = list[t];
+        const int r0 = off[q], n = off[q + 1] - r0;
+        (void)gp_dedup_task<2, HS, CHUNK>(a, S, q, r0, n, 0, refs, cbw, acnt, plist, pidx, pcap);
+    }
 }
 
 // every pair in every view: ComputeBilateralNCCNew's k >= 1 window (APD.cu:500-575), the same
@@ -3979,7 +4044,7 @@ struct apd_ctx {
     // buffers
     DevBuf imgs, quad, depth, views, cams, plane, cost, sel, sel2, vw, weak, conf, sa, amap, anchors, reliable, nearest,
         fit, curve, lists, rowcnt, rowoff, totals, near_off, dargs, evals, near_ring, near_g, wcand, lrs, wcur, arec, ga_stage,
-        wlist, gp_cb, gp_cnt, gp_cur, gp_refs, gp_ccnt, gp_cbase, gp_plist, gp_pidx, gp_pcost, gp_tmp, dpairs;
+        wlist, gp_cb, gp_cnt, gp_cur, gp_refs, gp_ccnt, gp_cbase, gp_plist, gp_pidx, gp_pcost, gp_tmp, dpairs, gp_cls;
     int n_near = 0;
     int host_stat[4] = {0, 0, 0, 0};  // apd_set_problem's read-back (see there)
     int near_levels = 0;  // confidence levels of k_near_columns (max confidence + 1), 0 = ring search
@@ -3998,6 +4063,10 @@ struct apd_ctx {
     bool dtex = true;              // DepthToWeak over pre-differenced fp16 texels (FastTexD); APD_NO_DTEX=1 disables
     int gp_np = 0;                 // its distinct pairs
     bool gp_one_pass = true;       // k_gp_dedup in one pass (atomic plist ranges); APD_GP_TWO_PASS=1: count + write
+    bool gp_async = true;          // the one-pass table enqueued without host round trips; APD_GP_SYNC=1: build_global_pairs
+    bool gp_pending = false;       // an async table is in flight (finish_global_pairs completes it)
+    size_t gp_pcap = 0;            // its pair-list capacity
+    int ncu = 256;                 // compute units of the device (persistent grids)
     bool gp_place = true;          // k_gp_count_loc + k_gp_place; APD_GP_FILL=1: k_gp_count + k_gp_fill (atomics twice)
     bool gp_small = true;          // one-pass small / medium anchors in smaller-table workgroups; APD_GP_NO_SMALL=1: all in the 48 KiB one
     int gp_cap_factor = 2;         // one-pass plist capacity in pairs per reference (8 after an overflow)
@@ -4245,6 +4314,11 @@ apd_ctx *apd_create(int32_t device) {
     ctx->gp_one_pass = getenv("APD_GP_TWO_PASS") == nullptr;
     ctx->gp_small = getenv("APD_GP_NO_SMALL") == nullptr;
     ctx->gp_place = getenv("APD_GP_FILL") == nullptr;
+    ctx->gp_async = getenv("APD_GP_SYNC") == nullptr && ctx->gp_one_pass && ctx->gp_small && ctx->gp_place;
+    {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n > 0) ctx->ncu = n;
+    }
     if (const char *e = getenv("APD_GP_CAP_FACTOR")) ctx->gp_cap_factor = std::max(0, std::min(8, atoi(e)));  // test hook
 
     // tile_pix needs the tile width to divide the 64-pixel tile (otherwise two workgroups share pixels)
@@ -4284,7 +4358,7 @@ void apd_destroy(apd_ctx *ctx) {
                       &ctx->reliable, &ctx->nearest, &ctx->fit, &ctx->curve, &ctx->lists, &ctx->rowcnt,
                       &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g, &ctx->wcand, &ctx->arec, &ctx->ga_stage,
                       &ctx->lrs, &ctx->wcur, &ctx->wlist, &ctx->gp_cb, &ctx->gp_cnt, &ctx->gp_cur, &ctx->gp_refs, &ctx->gp_ccnt,
-                      &ctx->gp_cbase, &ctx->gp_plist, &ctx->gp_pidx, &ctx->gp_pcost, &ctx->gp_tmp, &ctx->dpairs};
+                      &ctx->gp_cbase, &ctx->gp_plist, &ctx->gp_pidx, &ctx->gp_pcost, &ctx->gp_tmp, &ctx->dpairs, &ctx->gp_cls};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
@@ -4709,6 +4783,84 @@ static int build_global_pairs(apd_ctx *ctx, int nw) {
     return APD_OK;
 }
 
+// The same pair table without a host round trip (the default): everything is enqueued at once and
+// RandomInitialization, on the low-priority side stream, fills what the pair-table kernels leave free.
+// The window anchors are dealt into size classes on the device (k_gp_classes; at most HW - WEAK
+// anchors, all STRONG) and k_gp_dedup_q runs each class in a grid that fills the GPU; the pair list's
+// capacity is an upper bound from the WEAK count. apd_stage_prepare's end (finish_global_pairs) reads
+// the pair count back once, allocates the costs, and rebuilds the table with the synchronous path
+// above if a bound was exceeded.
+static int build_global_pairs_async(apd_ctx *ctx, int nw) {
+    Args &a = ctx->args;
+    hipStream_t s = ctx->stream;
+    const size_t HW = (size_t)a.HW, wc = (size_t)std::max(ctx->weak_count, 1);
+    ctx->gp_on = false;
+    ctx->gp_np = 0;
+    ctx->gp_pending = false;
+    const size_t U = HW > (size_t)ctx->weak_count ? HW - (size_t)ctx->weak_count : 1;  // anchors: STRONG pixels
+    const size_t pcap = std::min<size_t>((size_t)nw * 4 * (size_t)ctx->gp_cap_factor, (size_t)INT32_MAX);
+    if (!try_ensure(ctx, ctx->gp_cnt, (HW + 1) * sizeof(int)) || !try_ensure(ctx, ctx->gp_cur, (HW + 1) * sizeof(int)) ||
+        !try_ensure(ctx, ctx->gp_refs, (size_t)nw * 8 * sizeof(uint32_t)) ||
+        !try_ensure(ctx, ctx->gp_pidx, wc * 64 * sizeof(uint32_t)) || !try_ensure(ctx, ctx->gp_cb, 2 * wc) ||
+        !try_ensure(ctx, ctx->gp_cls, (GP_CLASSES * (U + 1) + 8) * sizeof(int)) ||
+        !try_ensure(ctx, ctx->gp_plist, std::max<size_t>(pcap, 1) * sizeof(int2)))
+        return APD_OK;
+    int *cnt = (int *)ctx->gp_cnt.p, *cur = (int *)ctx->gp_cur.p;
+    int *lists = (int *)ctx->gp_cls.p, *ctr = lists + GP_CLASSES * (U + 1);  // ctr: [3] class counts, [3] next, [4] overflow, [5] pairs
+    uint32_t *loc = (uint32_t *)ctx->gp_pidx.p;
+    HIP_OK(ctx, hipMemsetAsync(cnt, 0, (HW + 1) * sizeof(int), s));
+    HIP_OK(ctx, hipMemsetAsync(ctr, 0, 8 * sizeof(int), s));
+    hipLaunchKernelGGL(k_gp_count_loc, dim3(blocks_for((size_t)nw, BLOCK)), dim3(BLOCK), 0, s, a, (const int *)ctx->wlist.p, nw,
+                       cnt, (uint8_t *)ctx->gp_cb.p, (uint8_t *)ctx->gp_cb.p + wc, loc);
+    int st;
+    if ((st = exclusive_scan_int(ctx, cnt, cur, HW + 1))) return st == APD_ENOMEM ? APD_OK : st;
+    hipLaunchKernelGGL(k_gp_place, dim3(blocks_for((size_t)nw, BLOCK)), dim3(BLOCK), 0, s, a, (const int *)ctx->wlist.p, nw,
+                       (const int *)cur, (const uint8_t *)ctx->gp_cb.p + wc, (const uint32_t *)loc, (uint32_t *)ctx->gp_refs.p);
+    hipLaunchKernelGGL(k_gp_classes, dim3(blocks_for(HW, BLOCK)), dim3(BLOCK), 0, s, (const int *)cur, (int)HW, (int)(U + 1), lists, ctr);
+    const int ncu = ctx->ncu;
+#define GP_Q_ARGS(c)                                                                                                         \
+    s, a, (const int *)(lists + (size_t)(c) * (U + 1)), (const int *)(ctr + (c)), ctr + 3, (const int *)cur,                \
+        (const uint32_t *)ctx->gp_refs.p, (const uint8_t *)ctx->gp_cb.p, ctr + 5, (int2 *)ctx->gp_plist.p,                  \
+        (uint32_t *)ctx->gp_pidx.p, (int)pcap
+    hipLaunchKernelGGL((k_gp_dedup_q<GP_SMALL_HS, WAVE, false>), dim3(ncu * 32), dim3(WAVE), 0, GP_Q_ARGS(0));
+    hipLaunchKernelGGL((k_gp_dedup_q<GP_MEDIUM_HS, GP_CHUNK, false>), dim3(ncu * 6), dim3(GP_CHUNK), 0, GP_Q_ARGS(1));
+    hipLaunchKernelGGL((k_gp_dedup_q<GP_HS, GP_CHUNK, true>), dim3(ncu * 3), dim3(GP_CHUNK), 0, GP_Q_ARGS(2));
+#undef GP_Q_ARGS
+    if ((st = check_launch(ctx, "pair table"))) return st;
+    ctx->gp_pending = true;
+    ctx->gp_on = true;
+    ctx->gp_pcap = pcap;
+    return APD_OK;
+}
+
+// the async table's pair count (one read-back, after the prepare phase's kernels), its cost buffer,
+// and the synchronous rebuild when a bound was exceeded
+static int finish_global_pairs(apd_ctx *ctx, int nw) {
+    if (!ctx->gp_pending) return APD_OK;
+    ctx->gp_pending = false;
+    const size_t HW = (size_t)ctx->args.HW;
+    const size_t U = HW > (size_t)ctx->weak_count ? HW - (size_t)ctx->weak_count : 1;
+    const int *ctr = (const int *)ctx->gp_cls.p + GP_CLASSES * (U + 1);
+    int h[8] = {};
+    HIP_OK(ctx, hipMemcpyAsync(h, ctr, 8 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
+    const int npairs = h[5];
+    if (h[4] != 0 || npairs < 0 || (size_t)npairs > ctx->gp_pcap) {
+        if (npairs < 0 || (size_t)npairs > ctx->gp_pcap) ctx->gp_cap_factor = 8;
+        const bool rec = ctx->rec_on;
+        int st = build_global_pairs(ctx, nw);
+        if (st) return st;
+        if (!rec) ctx->gp_on = false;  // (the anchor-window records were not built)
+        return check_launch(ctx, "pair table");
+    }
+    if (npairs > 0 && !try_ensure(ctx, ctx->gp_pcost, (size_t)npairs * ((ctx->args.N + 3) & ~3) * sizeof(float))) {
+        ctx->gp_on = false;
+        return APD_OK;
+    }
+    ctx->gp_np = npairs;
+    return APD_OK;
+}
+
 int32_t apd_stage_prepare(apd_ctx *ctx) {
     if (!ctx || !ctx->loaded) return APD_ESTATE;
     (void)hipSetDevice(ctx->device);
@@ -4814,7 +4966,8 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
             // evaluates the candidates itself)
             // (a pair packs x | filtered << 15 | y << 16 into an int: H < 32768 is also apd_set_problem's limit)
             if ((size_t)a.HW < (1u << 25) && a.W < 32768 && a.H < 32768 &&
-                (st = build_global_pairs(ctx, ctx->cnt[2] + ctx->cnt[3])))
+                (st = ctx->gp_async ? build_global_pairs_async(ctx, ctx->cnt[2] + ctx->cnt[3])
+                                    : build_global_pairs(ctx, ctx->cnt[2] + ctx->cnt[3])))
                 return st;
         } else {
             (void)hipEventRecord(ctx->ev[14], s);
@@ -4824,7 +4977,7 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
         // Optional: without room the pair table is dropped (the sweep evaluates the candidates itself).
         ctx->rec_on = false;
         a.arec = nullptr;
-        if (a.use_apd && ctx->gp_on && ctx->gp_np > 0) {
+        if (a.use_apd && ctx->gp_on && (ctx->gp_np > 0 || ctx->gp_pending)) {
             const size_t rb = (size_t)a.HW * (a.sa_any ? 2 : 1) * (a.tex_f16 ? 2 : 4) * sizeof(uint4);
             if (try_ensure(ctx, ctx->arec, rb)) {
                 a.arec = devptr<decltype(a.arec)>(ctx->arec.p);
@@ -4842,6 +4995,7 @@ int32_t apd_stage_prepare(apd_ctx *ctx) {
     if (ctx->overlap) HIP_OK(ctx, hipStreamWaitEvent(s, ctx->ev_side[0], 0));  // join RandomInitialization
     HIP_OK(ctx, hipMemcpyAsync(ctx->sel.p, ctx->sel2.p, (size_t)a.HW * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     (void)hipEventRecord(ctx->ev[3], s);
+    if ((st = finish_global_pairs(ctx, ctx->cnt[2] + ctx->cnt[3]))) return st;
     ctx->prep_timed = true;
     ctx->wcur_fresh = a.wcur != nullptr;
     ctx->prepared = true;
@@ -5250,7 +5404,7 @@ int32_t apd_device_bytes(apd_ctx *ctx, size_t *bytes) {
                             &ctx->rowoff, &ctx->totals, &ctx->near_off, &ctx->dargs, &ctx->evals, &ctx->near_ring, &ctx->near_g,
                             &ctx->wcand, &ctx->arec, &ctx->ga_stage, &ctx->lrs, &ctx->wcur, &ctx->wlist, &ctx->gp_cb, &ctx->gp_cnt,
                             &ctx->gp_cur, &ctx->gp_refs, &ctx->gp_ccnt, &ctx->gp_cbase, &ctx->gp_plist, &ctx->gp_pidx,
-                            &ctx->gp_pcost, &ctx->gp_tmp, &ctx->dpairs};
+                            &ctx->gp_pcost, &ctx->gp_tmp, &ctx->dpairs, &ctx->gp_cls};
     size_t t = 0;
     for (const DevBuf *b : bufs) t += b->bytes;
     *bytes = t;
