@@ -502,10 +502,10 @@ struct FastMod {
 };
 // stage (SPLIT, one GA_STAGE_W-word row per WEAK index wi, so that k_gen_anchors_fit's wave reads its
 // pixel's row in one round trip): [0] the stream position << 6 | the number of points (0: no RANSAC),
-// [1] the pixel, [2 + 2 i] point i (short2, dvalid order) and [3 + 2 i] its depth (the plane's w, which
-// the RANSAC's get3d reads; nothing writes planes between the two kernels): k_gen_anchors_fit runs
-// the RANSAC
-#define GA_STAGE_W 66
+// [1] the pixel, [2 + i] point i (short2, dvalid order): k_gen_anchors_fit runs the RANSAC. (The
+// points' depths gathered here instead -- one dependent load per found point in this latency-bound
+// search -- made it 24 -> 30 ms at C3; the fit kernel's wave gathers them in one round trip.)
+#define GA_STAGE_W 34
 template <bool SPLIT>
 __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restrict__ stage, int wc) {
     const int c = blockIdx.x * BLOCK + threadIdx.x;
@@ -533,9 +533,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
         for (int i = 0; i < 32; ++i) sp[i] = make_short2(-1, -1);
     int odi = -1, nsp = 0;
     auto found = [&](int di, short2 p) {
-        if constexpr (SPLIT)
-            *reinterpret_cast<uint2 *>(row + 2 + 2 * nsp) =
-                make_uint2((uint32_t)(uint16_t)p.x | ((uint32_t)(uint16_t)p.y << 16), __float_as_uint(a.plane[p.x + p.y * W].w));
+        if constexpr (SPLIT) row[2 + nsp] = (uint32_t)(uint16_t)p.x | ((uint32_t)(uint16_t)p.y << 16);
         else sp[di] = p;
         dvalid |= 1u << di;
         nsp++;
@@ -625,11 +623,12 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
     }
     if (nsp <= 3) {
         a.reliable[c] = 0;
-        if constexpr (SPLIT) *reinterpret_cast<uint2 *>(row) = make_uint2(0u, (uint32_t)c);
+        if constexpr (SPLIT) { row[0] = 0u; row[1] = (uint32_t)c; }
         return;
     }
     if constexpr (SPLIT) {
-        *reinterpret_cast<uint2 *>(row) = make_uint2((g.n << 6) | (uint32_t)nsp, (uint32_t)c);
+        row[0] = (g.n << 6) | (uint32_t)nsp;
+        row[1] = (uint32_t)c;
         return;
     } else {
         short2 vp[32];
@@ -722,11 +721,11 @@ __global__ __launch_bounds__(GA_FIT_WAVES * WAVE) void k_gen_anchors_fit(Args a,
     const int wi = __builtin_amdgcn_readfirstlane(blockIdx.x * GA_FIT_WAVES + (int)(threadIdx.x >> 6));
     if (wi >= wc) return;
     const uint32_t *row = stage + (size_t)wi * GA_STAGE_W;
-    // the row in one round trip: lane 0 the header and pixel, lane i + 1 point i and its depth
-    const uint2 rv = (lane <= 32) ? *reinterpret_cast<const uint2 *>(row + 2 * lane) : make_uint2(0u, 0u);
-    const uint32_t hdr = __builtin_amdgcn_readfirstlane(rv.x);
+    // the row in one round trip: lanes 0 and 1 the header and pixel, lane i + 2 point i
+    const uint32_t rv = (lane < GA_STAGE_W) ? row[lane] : 0u;
+    const uint32_t hdr = (uint32_t)__builtin_amdgcn_readfirstlane((int)rv);
     const int vc = (int)(hdr & 63u);
-    const int c = __builtin_amdgcn_readfirstlane((int)rv.y);
+    const int c = __builtin_amdgcn_readlane((int)rv, 1);
     const int W = a.W;
     const int py = c / W, px = c - py * W;
     // the pixel's anchor row (APD.cu:1890-1893: anchor 0 the pixel, the others none until the RANSAC
@@ -737,13 +736,13 @@ __global__ __launch_bounds__(GA_FIT_WAVES * WAVE) void k_gen_anchors_fit(Args a,
     const float depth_diff = a.dmax - a.dmin;
     const APD_C Cam &cam = a.cams[0];
     // lane i: point i (X, Y, Z, packed position)
-    const uint32_t qi = (uint32_t)__shfl((int)rv.x, lane + 1), di = (uint32_t)__shfl((int)rv.y, lane + 1);
+    const uint32_t qi = (uint32_t)__shfl((int)rv, lane + 2);
     float X[3] = {0.0f, 0.0f, 0.0f};
     uint32_t q = 0xFFFFFFFFu;
     if (lane < vc) {
         q = qi;
         const int qx = (int)(int16_t)(q & 0xFFFFu), qy = (int)(int16_t)(q >> 16);
-        get3d(cam, (float)qx, (float)qy, __uint_as_float(di), X);
+        get3d(cam, (float)qx, (float)qy, a.plane[qx + qy * W].w, X);
     }
     const float X0 = X[0], X1 = X[1], X2 = X[2];
     float Cw[3];
