@@ -2241,14 +2241,29 @@ __global__ __launch_bounds__(WV_BLOCK, (WvOcc<F16, SA>::occ)) void k_sweep_weak_
             for (int j = 0; j < 8; ++j) gval[j] = ca[j];
         }
 #else
+        // the candidates' world points (geom_point: depth_from_plane and world_point, view-independent)
+        // once per (pixel, candidate) instead of once per (pixel, view, candidate): with N >= 8 view
+        // lanes per pixel, lane v computes candidate v's and the group's lanes read it by shuffle --
+        // the same statements on the same inputs, so the same bits
+        const bool share_p = geom && N >= 8;
+        float Pv[3] = {0.0f, 0.0f, 0.0f};
+        if (share_p && v < 8) geom_point(a, px, py, L.hyp[v * VM_P + p], Pv);
 #pragma unroll 1
         for (int j = 0; j < 8; ++j) {
             float cj = ca[0];
 #pragma unroll
             for (int k = 1; k < 8; ++k) if (j == k) cj = ca[k];
             float vv = cj;
-            if (geom && w > 0)
-                vv = ((hflag >> j) & 1u) ? fmaf(gf, geom_cost(a, px, py, v + 1, L.hyp[j * VM_P + p]), cj) : fmaf(gf, 3.0f, cj);
+            float P[3];
+            if (share_p) {
+                P[0] = __shfl(Pv[0], G.base + j);
+                P[1] = __shfl(Pv[1], G.base + j);
+                P[2] = __shfl(Pv[2], G.base + j);
+            }
+            if (geom && w > 0) {
+                if (!share_p) geom_point(a, px, py, L.hyp[j * VM_P + p], P);
+                vv = ((hflag >> j) & 1u) ? fmaf(gf, geom_cost_p(a, px, py, v + 1, P), cj) : fmaf(gf, 3.0f, cj);
+            }
 #pragma unroll
             for (int k = 0; k < 8; ++k) if (j == k) gval[k] = vv;
         }
@@ -2974,27 +2989,48 @@ __global__ __launch_bounds__(CHUNK) void k_gp_dedup(Args a, const int *__restric
 // next anchor from an atomic counter; else every gridDim-th. The class's count is read from device
 // memory, and every workgroup leaves the loop when it passes it.
 #define GP_CLASSES 3
-__global__ __launch_bounds__(BLOCK) void k_gp_classes(const int *__restrict__ off, int HW, int cap, int *__restrict__ lists,
-                                                      int *__restrict__ counts) {
+// A large window anchor's references are split into runs of GP_SPLIT, each deduplicated by its own
+// workgroup: one workgroup per anchor left the GPU idle behind the few anchors with 10^5 references
+// (counters: CUs busy 16 % of the kernel's span). A pair whose candidates meet in several runs gets
+// several ids -- labels, as when a table closes -- so k_gp_cost evaluates it a few more times.
+#define GP_SPLIT 4096
+// lists: classes 0 and 1 as anchor positions [cap] each, then class 2 as (anchor, run) pairs [cap2]
+__global__ __launch_bounds__(BLOCK) void k_gp_classes(const int *__restrict__ off, int HW, int cap, int cap2,
+                                                      int *__restrict__ lists, int *__restrict__ counts) {
     const int q = blockIdx.x * BLOCK + threadIdx.x;
     const int lane = threadIdx.x & (WAVE - 1);
     const int n = q < HW ? off[q + 1] - off[q] : 0;
     const int cls = n <= GP_SMALL_N ? 0 : (n <= GP_CHUNK ? 1 : 2);
+    const int runs = cls == 2 ? (n + GP_SPLIT - 1) / GP_SPLIT : 1;
+    int2 *list2 = reinterpret_cast<int2 *>(lists + 2 * (size_t)cap);
 #pragma unroll
     for (int c = 0; c < GP_CLASSES; ++c) {
-        const uint64_t m = __ballot(n > 0 && cls == c);
-        if (!m) continue;
-        const int leader = __builtin_ctzll(m);
+        const bool mine = n > 0 && cls == c;
+        if (!__ballot(mine)) continue;
+        // the wave's entries of class c: an exclusive scan of `runs` over the lanes, one atomic
+        int x = mine ? runs : 0;
+        const int own = x;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
         int base = 0;
-        if (lane == leader) base = atomicAdd(&counts[c], __builtin_popcountll(m));
-        base = __shfl(base, leader);
-        if (n > 0 && cls == c) {
-            const int pos = base + __builtin_popcountll(m & ((1ull << lane) - 1ull));
-            if (pos < cap) lists[(size_t)c * cap + pos] = q;
+        if (lane == WAVE - 1) base = atomicAdd(&counts[c], x);
+        base = __shfl(base, WAVE - 1) + x - own;
+        if (!mine) continue;
+        if (c < 2) {
+            if (base < cap) lists[(size_t)c * cap + base] = q;
             else atomicOr(&counts[GP_CLASSES + 1], 1);  // (overflow: the host rebuilds synchronously)
+        } else {
+            for (int r = 0; r < own; ++r) {
+                if (base + r < cap2) list2[base + r] = make_int2(q, r);
+                else atomicOr(&counts[GP_CLASSES + 1], 1);
+            }
         }
     }
 }
+// DYN (class 2): the list holds (anchor, run) pairs, run r covering references [r GP_SPLIT, (r + 1) GP_SPLIT)
 template <int HS, int CHUNK, bool DYN>
 __global__ __launch_bounds__(CHUNK) void k_gp_dedup_q(Args a, const int *__restrict__ list, const int *__restrict__ count,
                                                       int *__restrict__ next, const int *__restrict__ off,
@@ -3011,8 +3047,18 @@ __global__ __launch_bounds__(CHUNK) void k_gp_dedup_q(Args a, const int *__restr
             __syncthreads();
         }
         if (t >= ntask) break;  // (uniform)
-        const int q = list[t];
-        const int r0 = off[q], n = off[q + 1] - r0;
+        int q, r0, n;
+        if (DYN) {
+            const int2 e = reinterpret_cast<const int2 *>(list)[t];
+            q = e.x;
+            const int b = off[q], m = off[q + 1] - b;
+            r0 = b + e.y * GP_SPLIT;
+            n = min(GP_SPLIT, m - e.y * GP_SPLIT);
+        } else {
+            q = list[t];
+            r0 = off[q];
+            n = off[q + 1] - r0;
+        }
         (void)gp_dedup_task<2, HS, CHUNK>(a, S, q, r0, n, 0, refs, cbw, acnt, plist, pidx, pcap);
     }
 }
@@ -4797,15 +4843,16 @@ static int build_global_pairs_async(apd_ctx *ctx, int nw) {
     ctx->gp_np = 0;
     ctx->gp_pending = false;
     const size_t U = HW > (size_t)ctx->weak_count ? HW - (size_t)ctx->weak_count : 1;  // anchors: STRONG pixels
+    const size_t cap2 = U + 1 + (size_t)nw * 8 / GP_SPLIT + 1;  // class-2 runs: <= anchors + references / GP_SPLIT
     const size_t pcap = std::min<size_t>((size_t)nw * 4 * (size_t)ctx->gp_cap_factor, (size_t)INT32_MAX);
     if (!try_ensure(ctx, ctx->gp_cnt, (HW + 1) * sizeof(int)) || !try_ensure(ctx, ctx->gp_cur, (HW + 1) * sizeof(int)) ||
         !try_ensure(ctx, ctx->gp_refs, (size_t)nw * 8 * sizeof(uint32_t)) ||
         !try_ensure(ctx, ctx->gp_pidx, wc * 64 * sizeof(uint32_t)) || !try_ensure(ctx, ctx->gp_cb, 2 * wc) ||
-        !try_ensure(ctx, ctx->gp_cls, (GP_CLASSES * (U + 1) + 8) * sizeof(int)) ||
+        !try_ensure(ctx, ctx->gp_cls, (2 * (U + 1) + 2 * cap2 + 8) * sizeof(int)) ||
         !try_ensure(ctx, ctx->gp_plist, std::max<size_t>(pcap, 1) * sizeof(int2)))
         return APD_OK;
     int *cnt = (int *)ctx->gp_cnt.p, *cur = (int *)ctx->gp_cur.p;
-    int *lists = (int *)ctx->gp_cls.p, *ctr = lists + GP_CLASSES * (U + 1);  // ctr: [3] class counts, [3] next, [4] overflow, [5] pairs
+    int *lists = (int *)ctx->gp_cls.p, *ctr = lists + 2 * (U + 1) + 2 * cap2;  // ctr: [3] class counts, [3] next, [4] overflow, [5] pairs
     uint32_t *loc = (uint32_t *)ctx->gp_pidx.p;
     HIP_OK(ctx, hipMemsetAsync(cnt, 0, (HW + 1) * sizeof(int), s));
     HIP_OK(ctx, hipMemsetAsync(ctr, 0, 8 * sizeof(int), s));
@@ -4815,7 +4862,8 @@ static int build_global_pairs_async(apd_ctx *ctx, int nw) {
     if ((st = exclusive_scan_int(ctx, cnt, cur, HW + 1))) return st == APD_ENOMEM ? APD_OK : st;
     hipLaunchKernelGGL(k_gp_place, dim3(blocks_for((size_t)nw, BLOCK)), dim3(BLOCK), 0, s, a, (const int *)ctx->wlist.p, nw,
                        (const int *)cur, (const uint8_t *)ctx->gp_cb.p + wc, (const uint32_t *)loc, (uint32_t *)ctx->gp_refs.p);
-    hipLaunchKernelGGL(k_gp_classes, dim3(blocks_for(HW, BLOCK)), dim3(BLOCK), 0, s, (const int *)cur, (int)HW, (int)(U + 1), lists, ctr);
+    hipLaunchKernelGGL(k_gp_classes, dim3(blocks_for(HW, BLOCK)), dim3(BLOCK), 0, s, (const int *)cur, (int)HW, (int)(U + 1),
+                       (int)cap2, lists, ctr);
     const int ncu = ctx->ncu;
 #define GP_Q_ARGS(c)                                                                                                         \
     s, a, (const int *)(lists + (size_t)(c) * (U + 1)), (const int *)(ctr + (c)), ctr + 3, (const int *)cur,                \
@@ -4839,7 +4887,8 @@ static int finish_global_pairs(apd_ctx *ctx, int nw) {
     ctx->gp_pending = false;
     const size_t HW = (size_t)ctx->args.HW;
     const size_t U = HW > (size_t)ctx->weak_count ? HW - (size_t)ctx->weak_count : 1;
-    const int *ctr = (const int *)ctx->gp_cls.p + GP_CLASSES * (U + 1);
+    const size_t cap2 = U + 1 + (size_t)nw * 8 / GP_SPLIT + 1;
+    const int *ctr = (const int *)ctx->gp_cls.p + 2 * (U + 1) + 2 * cap2;
     int h[8] = {};
     HIP_OK(ctx, hipMemcpyAsync(h, ctr, 8 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIP_OK(ctx, hipStreamSynchronize(ctx->stream));
