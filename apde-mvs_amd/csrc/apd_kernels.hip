@@ -792,16 +792,29 @@ __global__ __launch_bounds__(GA_FIT_WAVES * WAVE) void k_gen_anchors_fit(Args a,
     }
     ok = ok && tcnt >= 6;
     const float cd = fabsf(cr.x * Cw[0] + cr.y * Cw[1] + cr.z * Cw[2] + cr.w);
-    // the sequential selection, replayed in iteration order (uniform)
+    // The sequential selection (iteration order: a larger inlier count wins, an equal count a strictly
+    // smaller centre distance) is, over the ok lanes, the largest count; among its lanes the first one,
+    // unless a later one has a smaller distance (`<`: a NaN never wins, and a NaN first one is never
+    // replaced) -- i.e. the earliest lane with the minimum distance, NaN taken as +inf, when the first
+    // one's distance is not NaN. Computed by wave reductions instead of a replay over the lanes.
     const uint64_t okm = __ballot(ok);
-    int best_it = -1, max_count = 3;
-    float min_cost = APD_FLT_MAX;
-    for (uint64_t m = okm; m; m &= m - 1) {
-        const int it = __builtin_ctzll(m);
-        const int tc = __builtin_amdgcn_readlane(tcnt, it);
-        const float ci = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cd), it));
-        if (tc > max_count) { max_count = tc; min_cost = ci; best_it = it; }
-        else if (tc == max_count && ci < min_cost) { min_cost = ci; best_it = it; }
+    int best_it = -1;
+    if (okm) {
+        int mc = ok ? tcnt : -1;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mc = max(mc, __shfl_xor(mc, o));
+        const bool top = ok && tcnt == mc;
+        const uint64_t topm = __ballot(top);
+        const int first = __builtin_ctzll(topm);
+        const float cfirst = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cd), first));
+        if (__builtin_isnan(cfirst)) {
+            best_it = first;
+        } else {
+            float cm = top ? (__builtin_isnan(cd) ? __builtin_inff() : cd) : __builtin_inff();
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) cm = fminf(cm, __shfl_xor(cm, o));
+            best_it = __builtin_ctzll(__ballot(top && !__builtin_isnan(cd) ? cd == cm : (top && cm == __builtin_inff())));
+        }
     }
     if (best_it < 0) {
         if (lane == 0) a.reliable[c] = 0;
