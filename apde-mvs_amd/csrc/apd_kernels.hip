@@ -500,9 +500,6 @@ struct FastMod {
         return (uint32_t)__umul64hi(low, (uint64_t)d);
     }
 };
-#ifndef GA_SEQ_SEARCH
-#define GA_SEQ_SEARCH 0  // 1: the shift-1 search one direction at a time (A/B)
-#endif
 // stage (SPLIT, one GA_STAGE_W-word row per WEAK index wi, so that k_gen_anchors_fit's wave reads its
 // pixel's row in one round trip): [0] the stream position << 6 | the number of points (0: no RANSAC),
 // [1] the pixel, [2 + i] point i (short2, dvalid order): k_gen_anchors_fit runs the RANSAC. (The
@@ -543,94 +540,6 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
     };
     const int rt = a.rotate_time;
     const FastMod fshift((uint32_t)a.anc_shift);
-    if (a.anc_shift == 1 && !GA_SEQ_SEARCH) {
-        // rotate_time >= 3 (main.cpp's rounds 2 and 3): shift = max((int)(tan(angle / 2) * 20), 1) is
-        // 1, every draw's offset is x % 1 = 0, and the 4 attempts of a radius sample the same point --
-        // the same lookup and verdict; the draws only advance the stream position, by 4 (attempt 1
-        // succeeds) or 16 (all fail), and that position is read only after the search (the RANSAC's
-        // stream start), as a sum. So two directions' radius chains -- each a dependent chain of
-        // nearest-STRONG lookups -- run interleaved, their lookups in flight together, and their points
-        // are recorded in direction order: the same points, the same stream position.
-        for (int odx = -1; odx <= 1; ++odx) {
-            for (int ody = -1; ody <= 1; ++ody) {
-                if (odx == 0 && ody == 0) continue;
-                float dx = (float)odx, dy = (float)ody;
-                normalize2(dx, dy);
-                odi++;
-                for (int ri = 0; ri < rt; ri += 2) {
-                    const bool two = ri + 1 < rt;
-                    const float dxA = dx, dyA = dy;
-                    float dxB = dxA * a.anc_cos - dyA * a.anc_sin, dyB = dxA * a.anc_sin + dyA * a.anc_cos;
-                    normalize2(dxB, dyB);
-                    float ddxA = dxA * 20 + (float)0, ddyA = dyA * 20 + (float)0;
-                    normalize2(ddxA, ddyA);
-                    float ddxB = dxB * 20 + (float)0, ddyB = dyB * 20 + (float)0;
-                    normalize2(ddxB, ddyB);
-                    int rA = 2, rB = 2;
-                    bool actA = true, actB = two, gotA = false, gotB = false;
-                    short2 pA = make_short2(-1, -1), pB = make_short2(-1, -1);
-                    while (actA || actB) {
-                        bool mA = false, mB = false;
-                        short2 nA = make_short2(-1, -1), nB = make_short2(-1, -1);
-                        if (actA) {
-                            const float tx = (float)px + dxA * (float)rA, ty = (float)py + dyA * (float)rA;
-                            if (tx < 0 || ty < 0 || tx >= (float)W || ty >= (float)H) {
-                                actA = false;
-                            } else {
-                                const int ax = (int16_t)(int)((float)px + ddxA * (float)rA);
-                                const int ay = (int16_t)(int)((float)py + ddyA * (float)rA);
-                                mA = !(ax < margin || ay < margin || ax >= W - margin || ay >= H - margin);
-                                if (mA) nA = a.nearest[ax + ay * W];
-                            }
-                        }
-                        if (actB) {
-                            const float tx = (float)px + dxB * (float)rB, ty = (float)py + dyB * (float)rB;
-                            if (tx < 0 || ty < 0 || tx >= (float)W || ty >= (float)H) {
-                                actB = false;
-                            } else {
-                                const int ax = (int16_t)(int)((float)px + ddxB * (float)rB);
-                                const int ay = (int16_t)(int)((float)py + ddyB * (float)rB);
-                                mB = !(ax < margin || ay < margin || ax >= W - margin || ay >= H - margin);
-                                if (mB) nB = a.nearest[ax + ay * W];
-                            }
-                        }
-                        if (actA) {
-                            bool ok = mA && !(nA.x == -1 || nA.y == -1);
-                            if (ok) {
-                                float tdx = (float)(nA.x - px), tdy = (float)(nA.y - py);
-                                normalize2(tdx, tdy);
-                                ok = tdx * dxA + tdy * dyA > a.anc_thr;
-                            }
-                            g.n += ok ? 4u : 16u;
-                            if (ok) { gotA = true; pA = nA; actA = false; }
-                            else { rA = min(rA * 2, rA + 25); actA = rA <= APD_MAX_SEARCH_RADIUS; }
-                        }
-                        if (actB) {
-                            bool ok = mB && !(nB.x == -1 || nB.y == -1);
-                            if (ok) {
-                                float tdx = (float)(nB.x - px), tdy = (float)(nB.y - py);
-                                normalize2(tdx, tdy);
-                                ok = tdx * dxB + tdy * dyB > a.anc_thr;
-                            }
-                            g.n += ok ? 4u : 16u;
-                            if (ok) { gotB = true; pB = nB; actB = false; }
-                            else { rB = min(rB * 2, rB + 25); actB = rB <= APD_MAX_SEARCH_RADIUS; }
-                        }
-                    }
-                    if (gotA) found(odi * 4 + ri, pA);
-                    if (gotB) found(odi * 4 + ri + 1, pB);
-                    // the next direction: B rotated (A rotated is B itself)
-                    if (two) {
-                        float rx = dxB * a.anc_cos - dyB * a.anc_sin, ry = dxB * a.anc_sin + dyB * a.anc_cos;
-                        normalize2(rx, ry);
-                        dx = rx; dy = ry;
-                    } else {
-                        dx = dxB; dy = dyB;
-                    }
-                }
-            }
-        }
-    } else
     for (int odx = -1; odx <= 1; ++odx) {
         for (int ody = -1; ody <= 1; ++ody) {
             if (odx == 0 && ody == 0) continue;
