@@ -716,7 +716,10 @@ __device__ __forceinline__ uint32_t rng_draw(const Rng &g, uint32_t d) {
     return j == 0 ? b.x : (j == 1 ? b.y : (j == 2 ? b.z : b.w));
 }
 #define GA_FIT_WAVES 4
-__global__ __launch_bounds__(GA_FIT_WAVES * WAVE) void k_gen_anchors_fit(Args a, const uint32_t *__restrict__ stage, int wc) {
+#ifndef GA_FIT_MINW
+#define GA_FIT_MINW 8  // waves per SIMD the registers are bounded for (short, issue-bound waves: occupancy hides their latency)
+#endif
+__global__ __launch_bounds__(GA_FIT_WAVES * WAVE, GA_FIT_MINW) void k_gen_anchors_fit(Args a, const uint32_t *__restrict__ stage, int wc) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wi = __builtin_amdgcn_readfirstlane(blockIdx.x * GA_FIT_WAVES + (int)(threadIdx.x >> 6));
     if (wi >= wc) return;
