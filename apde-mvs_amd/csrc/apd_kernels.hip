@@ -488,6 +488,23 @@ __device__ __forceinline__ bool point_in_triangle(int ax, int ay, int bx, int by
 __device__ __forceinline__ bool anc_inlier(const Args &a, float d, float depth_diff) {
     return a.anc_dlim_ok ? d < a.anc_dlim : d / depth_diff < a.ransac_thr;
 }
+// GenAnchors' direction test (APD.cu:1936-1939): normalize2(tdx, tdy), then tdx * dx + tdy * dy > thr.
+// Filtered: the same sum with 1 / sqrt from v_rsq_f32 (1 ulp) differs from the IEEE statement's by
+// < 2e-6 for unit (dx, dy) (each product <= 1 in magnitude, a few roundings of 2^-24 relative each), so
+// outside a 1e-4 band around thr (50x that bound) it has the same verdict; inside the band (or for a
+// NaN) the IEEE statement decides. Saves the IEEE sqrt and division on the search's dependent chain.
+#ifndef GA_ANGLE_FILTER
+#define GA_ANGLE_FILTER 1
+#endif
+__device__ __forceinline__ bool ga_angle_ok(float tdx, float tdy, float dx, float dy, float thr) {
+    if (GA_ANGLE_FILTER) {
+        const float r = __builtin_amdgcn_rsqf(tdx * tdx + tdy * tdy);
+        const float va = (tdx * r) * dx + (tdy * r) * dy;
+        if (fabsf(va - thr) > 1e-4f) return va > thr;
+    }
+    normalize2(tdx, tdy);
+    return tdx * dx + tdy * dy > thr;
+}
 // x % d for d in 1..32 without an integer division: with M = floor((2^64 - 1) / d) + 1, the low 64 bits
 // of M * x are frac(x / d) * 2^64 (to within d * 2^-32 < 1/d), whose high part times d is x mod d
 // (Lemire, Kaser, Kurz 2019 for 32-bit x and d)
@@ -506,6 +523,13 @@ struct FastMod {
 // points' depths gathered here instead -- one dependent load per found point in this latency-bound
 // search -- made it 24 -> 30 ms at C3; the fit kernel's wave gathers them in one round trip.)
 #define GA_STAGE_W 34
+#ifndef GA_PHILOX_LDS
+#define GA_PHILOX_LDS 1  // k_gen_anchors_fit: one Philox block per lane, shared through LDS
+#endif
+#ifndef GA_SEARCH_AHEAD
+#define GA_SEARCH_AHEAD 0  // the shift-1 search issues the next radius's lookup before judging this one
+                           // (measured slower at C3: anchors 57.1 -> 61.7 ms, profiles/r6_ab_gen_anchors.txt)
+#endif
 template <bool SPLIT>
 __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restrict__ stage, int wc) {
     const int c = blockIdx.x * BLOCK + threadIdx.x;
@@ -556,23 +580,48 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
                     float ddx = dx * 20 + (float)0, ddy = dy * 20 + (float)0;
                     normalize2(ddx, ddy);
                     // (measured: lookups of four radii issued together, judged in order, made this
-                    // kernel slower at C3, 24.4 -> 32.1 ms: more registers, fewer waves in flight)
-                    for (int radius = 2; radius <= APD_MAX_SEARCH_RADIUS; radius = min(radius * 2, radius + 25)) {
-                        float tx = (float)px + dx * (float)radius, ty = (float)py + dy * (float)radius;
-                        if (tx < 0 || ty < 0 || tx >= (float)W || ty >= (float)H) break;
+                    // kernel slower at C3, 24.4 -> 32.1 ms: more registers, fewer waves in flight.)
+                    // One radius ahead: the next radius's lookup is issued before this one is judged,
+                    // so the gather's latency overlaps the verdict's arithmetic. A radius is live when
+                    // it is <= APD_MAX_SEARCH_RADIUS and its ray point is inside the image (else the
+                    // search ends there, drawing nothing); its lookup only when the probe is inside
+                    // the margin -- the same statements as one radius at a time.
+                    auto probe = [&](int radius, bool &live, short2 &nn) {
+                        const float tx = (float)px + dx * (float)radius, ty = (float)py + dy * (float)radius;
+                        live = radius <= APD_MAX_SEARCH_RADIUS && !(tx < 0 || ty < 0 || tx >= (float)W || ty >= (float)H);
                         const int ax = (int16_t)(int)((float)px + ddx * (float)radius);
                         const int ay = (int16_t)(int)((float)py + ddy * (float)radius);
-                        bool ok = !(ax < margin || ay < margin || ax >= W - margin || ay >= H - margin);
-                        const short2 nn = ok ? a.nearest[ax + ay * W] : make_short2(-1, -1);
-                        ok = ok && !(nn.x == -1 || nn.y == -1);
-                        if (ok) {
-                            float tdx = (float)(nn.x - px), tdy = (float)(nn.y - py);
-                            normalize2(tdx, tdy);
-                            ok = tdx * dx + tdy * dy > a.anc_thr;
-                        }
+                        const bool in = live && !(ax < margin || ay < margin || ax >= W - margin || ay >= H - margin);
+                        nn = in ? a.nearest[ax + ay * W] : make_short2(-1, -1);
+                    };
+#if GA_SEARCH_AHEAD
+                    int radius = 2;
+                    bool live;
+                    short2 nn;
+                    probe(radius, live, nn);
+                    while (live) {
+                        const int rn = min(radius * 2, radius + 25);
+                        bool live_n;
+                        short2 nn_n;
+                        probe(rn, live_n, nn_n);
+                        bool ok = !(nn.x == -1 || nn.y == -1);
+                        if (ok) ok = ga_angle_ok((float)(nn.x - px), (float)(nn.y - py), dx, dy, a.anc_thr);
+                        g.n += ok ? 4u : 16u;
+                        if (ok) { found(di, nn); break; }
+                        radius = rn; live = live_n; nn = nn_n;
+                    }
+#else
+                    for (int radius = 2; radius <= APD_MAX_SEARCH_RADIUS; radius = min(radius * 2, radius + 25)) {
+                        bool live;
+                        short2 nn;
+                        probe(radius, live, nn);
+                        if (!live) break;
+                        bool ok = !(nn.x == -1 || nn.y == -1);
+                        if (ok) ok = ga_angle_ok((float)(nn.x - px), (float)(nn.y - py), dx, dy, a.anc_thr);
                         g.n += ok ? 4u : 16u;
                         if (ok) { found(di, nn); break; }
                     }
+#endif
                 } else
                 for (int radius = 2; radius <= APD_MAX_SEARCH_RADIUS; radius = min(radius * 2, radius + 25)) {
                     float tx = (float)px + dx * (float)radius, ty = (float)py + dy * (float)radius;
@@ -600,10 +649,7 @@ __global__ __launch_bounds__(BLOCK) void k_gen_anchors(Args a, uint32_t *__restr
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
                         if (used < 4 || !in[t] || nn[t].x == -1 || nn[t].y == -1) continue;
-                        float tdx = (float)(nn[t].x - px), tdy = (float)(nn[t].y - py);
-                        normalize2(tdx, tdy);
-                        float ca = tdx * dx + tdy * dy;
-                        if (ca > a.anc_thr) { found(di, nn[t]); used = t + 1; }
+                        if (ga_angle_ok((float)(nn[t].x - px), (float)(nn[t].y - py), dx, dy, a.anc_thr)) { found(di, nn[t]); used = t + 1; }
                     }
 #ifdef APD_ANCHOR_STATS  // measurement build: steps, the attempt that succeeded, wave-level steps
                     if (a.evals) {
@@ -754,6 +800,16 @@ __global__ __launch_bounds__(GA_FIT_WAVES * WAVE, GA_FIT_MINW) void k_gen_anchor
     const Rng g(a.seed_lo, a.seed_hi, (uint32_t)c, ORD_ANCHORS);
     const FastMod fm((uint32_t)vc);
     const uint32_t d0 = (hdr >> 6) + 3u * (uint32_t)lane;
+#if GA_PHILOX_LDS
+    // the 50 iterations' 150 draws lie in Philox blocks n / 4 .. n / 4 + 38: lane j generates block
+    // n / 4 + j once into LDS and every lane reads its three words there (instead of two blocks per lane)
+    __shared__ uint4 sphil[GA_FIT_WAVES][WAVE];
+    const uint32_t nb = (hdr >> 6) >> 2;
+    sphil[threadIdx.x >> 6][lane] = g.block(nb + (uint32_t)lane);
+    __builtin_amdgcn_wave_barrier();  // (LDS operations of one wave complete in order)
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>(&sphil[threadIdx.x >> 6][0]);
+    auto pick = [&](uint32_t d) { return sw[d - 4u * nb]; };  // (d - 4 nb <= 3 + 3 * 63 + 2 < 256)
+#else
     // the three draws d0 .. d0 + 2 lie in Philox blocks d0 / 4 and (d0 + 2) / 4: two blocks, not three
     const uint4 b0 = g.block(d0 >> 2), b1 = g.block((d0 + 2u) >> 2);
     auto pick = [&](uint32_t d) {
@@ -761,6 +817,7 @@ __global__ __launch_bounds__(GA_FIT_WAVES * WAVE, GA_FIT_MINW) void k_gen_anchor
         const uint32_t j = d & 3u;
         return j == 0 ? b.x : (j == 1 ? b.y : (j == 2 ? b.z : b.w));
     };
+#endif
     const int ia = (int)fm.mod(pick(d0));
     const int ib = (int)fm.mod(pick(d0 + 1u));
     const int ic = (int)fm.mod(pick(d0 + 2u));
@@ -781,17 +838,41 @@ __global__ __launch_bounds__(GA_FIT_WAVES * WAVE, GA_FIT_MINW) void k_gen_anchor
     }
     // the points broadcast from LDS (one uniform-address read per point; v_readlane's SGPR results
     // stalled the loop on their read-after-write hazards)
-    __shared__ float4 spts[GA_FIT_WAVES][WAVE];
+    __shared__ float spx[GA_FIT_WAVES][WAVE], spy[GA_FIT_WAVES][WAVE], spz[GA_FIT_WAVES][WAVE];
     __shared__ float swgt[GA_FIT_WAVES][WAVE];
     const int wv = threadIdx.x >> 6;
-    spts[wv][lane] = make_float4(X0, X1, X2, 0.0f);
+    // (coordinates apart, two points per 8-byte read: the point pairs go straight into packed fp32
+    // multiplies and adds; slots past the last point hold NaN, which is never an inlier)
+    const float qnan = __builtin_nanf("");
+    spx[wv][lane] = lane < vc ? X0 : qnan;
+    spy[wv][lane] = lane < vc ? X1 : qnan;
+    spz[wv][lane] = lane < vc ? X2 : qnan;
     __builtin_amdgcn_wave_barrier();  // (LDS operations of one wave complete in order)
+    // (anc_inlier with its uniform choice taken outside the loop: inside, the compiler evaluated both
+    // sides per point -- an IEEE division the common d < anc_dlim side never needs). Per point the same
+    // statement, fabsf(((cr.x * x + cr.y * y) + cr.z * z) + cr.w), two points per packed operation.
     int tcnt = 0;
+    const apd_f2 crx = {cr.x, cr.x}, cry = {cr.y, cr.y}, crz = {cr.z, cr.z}, crw = {cr.w, cr.w};
+    auto pair_d = [&](int k) {
+        const apd_f2 px2 = *reinterpret_cast<const apd_f2 *>(&spx[wv][k]);
+        const apd_f2 py2 = *reinterpret_cast<const apd_f2 *>(&spy[wv][k]);
+        const apd_f2 pz2 = *reinterpret_cast<const apd_f2 *>(&spz[wv][k]);
+        const apd_f2 d = ((crx * px2 + cry * py2) + crz * pz2) + crw;
+        return (apd_f2){fabsf(d.x), fabsf(d.y)};
+    };
+    if (a.anc_dlim_ok) {
+        const float lim = a.anc_dlim;
 #pragma unroll 4
-    for (int k = 0; k < vc; ++k) {
-        const float4 P = spts[wv][k];
-        float d = fabsf(cr.x * P.x + cr.y * P.y + cr.z * P.z + cr.w);
-        if (anc_inlier(a, d, depth_diff)) tcnt++;
+        for (int k = 0; k < vc; k += 2) {
+            const apd_f2 d = pair_d(k);
+            tcnt += (d.x < lim ? 1 : 0) + (d.y < lim ? 1 : 0);
+        }
+    } else {
+#pragma unroll 2
+        for (int k = 0; k < vc; k += 2) {
+            const apd_f2 d = pair_d(k);
+            tcnt += (d.x / depth_diff < a.ransac_thr ? 1 : 0) + (d.y / depth_diff < a.ransac_thr ? 1 : 0);
+        }
     }
     ok = ok && tcnt >= 6;
     const float cd = fabsf(cr.x * Cw[0] + cr.y * Cw[1] + cr.z * Cw[2] + cr.w);
@@ -1580,7 +1661,8 @@ struct WvRefT {
     // once per evaluation: sr / wsum, var_ref -- the same statements (1 / wsum: inv_lut)
     float wsrp[NWIN * VM_P], wvar[NWIN * VM_P];
     int anc[9 * VM_P];           // packed (x, y) of anchors 0..8, -1 = none
-    uint32_t flags[VM_P];        // bits 0-8: hypothesis h present (anchor STRONG); 16-24: window k evaluated
+    uint32_t flags[VM_P];        // bits 0-7: hypothesis h present (anchor STRONG); 12-15: the current plane is
+                                 // hypothesis (bits 12-14) when bit 15; 16-24: window k evaluated
                                  // (anchor present and SA label matches); 25-27: the best anchor
                                  // hypothesis (Weak sweep P2a); 29: the pixel has an SA label (its anchor
                                  // windows are filtered); 31: refine (fit normal != 0)
@@ -2071,6 +2153,9 @@ __device__ __forceinline__ float ncc_new_vm(const Args &a, const WvRefT<F16, NWI
 #ifndef WV_WAVES
 #define WV_WAVES 4  // waves per Weak-sweep workgroup (64 pixels)
 #endif
+#ifndef WV_CUR_MATCH
+#define WV_CUR_MATCH 1  // P1b takes the current plane's costs from P2a when it is an anchor candidate's plane
+#endif
 #ifndef WV_P2_GEOM_BATCH
 // P2a's 8 geometric terms with their gathers batched (1) or one at a time (0): batched was -0.7 % at
 // three workgroups per CU, one at a time is -0.3 % at four (profiles/r5_ab_sa_occ4.txt, r5_ab_kept_lanes.txt)
@@ -2157,7 +2242,34 @@ __global__ __launch_bounds__(WV_BLOCK, (WvOcc<F16, SA>::occ)) void k_sweep_weak_
                     L.hyp[(k - 1) * VM_P + p1] = hp[k];
                 }
             }
-            L.flags[p1] = hflag | (awin << 16) | (use_sa ? (1u << 29) : 0u);
+            // the current plane bitwise equal to STRONG anchor k's (a pixel keeps the anchor hypothesis
+            // it took while neither plane changes): its NCC-New and geometric terms are anchor candidate
+            // k - 1's, which P2a holds -- flags bit 15 + (k - 1) << 12, the first such k (WV_CUR_MATCH)
+            uint32_t cmatch = 0;
+#pragma unroll
+            for (int k = 8; k >= 1; --k)
+                if (WV_CUR_MATCH && ((hflag >> (k - 1)) & 1u) && __float_as_uint(hp[k].x) == __float_as_uint(cur.x) &&
+                    __float_as_uint(hp[k].y) == __float_as_uint(cur.y) && __float_as_uint(hp[k].z) == __float_as_uint(cur.z) &&
+                    __float_as_uint(hp[k].w) == __float_as_uint(cur.w))
+                    cmatch = (1u << 15) | ((uint32_t)(k - 1) << 12);
+            L.flags[p1] = hflag | cmatch | (awin << 16) | (use_sa ? (1u << 29) : 0u);
+            LANE_STAT(0, true);         // (instrumented builds: pixels, and those whose current plane
+            LANE_STAT(2, cmatch != 0);  //  is an anchor candidate's)
+#ifdef APD_PHASE_STAMPS
+            {  // (instrumented builds: the fit plane equal to the current plane / to an anchor candidate's)
+                const float4 ft = a.fit[c1];
+                auto same = [](float4 u, float4 w) {
+                    return __float_as_uint(u.x) == __float_as_uint(w.x) && __float_as_uint(u.y) == __float_as_uint(w.y) &&
+                           __float_as_uint(u.z) == __float_as_uint(w.z) && __float_as_uint(u.w) == __float_as_uint(w.w);
+                };
+                bool fc = false;
+#pragma unroll
+                for (int k = 1; k < 9; ++k) fc = fc || (((hflag >> (k - 1)) & 1u) && same(hp[k], ft));
+                const bool has_fit = !(ft.x == 0 && ft.y == 0 && ft.z == 0);
+                LANE_STAT(4, has_fit && same(ft, cur));
+                LANE_STAT(6, has_fit && fc);
+            }
+#endif
             L.hyp[8 * VM_P + p1] = cur;
             L.pxy[p1] = px1 | (py1 << 16);
             int bx0 = px1, by0 = py1, bx1 = px1, by1 = py1;  // anchors' bounding box (+ the pixel)
@@ -2287,6 +2399,16 @@ __global__ __launch_bounds__(WV_BLOCK, (WvOcc<F16, SA>::occ)) void k_sweep_weak_
 #ifdef APD_PHASE_STAMPS
         if (a.evals && threadIdx.x == 0) atomicAdd(PROF_AT(a.evals, APD_INSTR + 8 + 7), (unsigned long long)(clock64() - tg0_));
 #endif
+        // the current plane is anchor candidate m's: P1b's cost for this view (its NCC-New + geometric
+        // term, 0 for a view without weight) is gval[m], the same statements on the same inputs
+        const uint32_t flp = L.flags[p];
+        if (WV_CUR_MATCH && ((flp >> 15) & 1u)) {
+            const int m = (int)((flp >> 12) & 7u);
+            float gm = gval[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) if (m == k) gm = gval[k];
+            if (G.valid) costL[((direct ? 0 : 8 * N) + v) * VM_P + p] = w > 0 ? gm : 0.0f;
+        }
         float fc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         float wn = 0.0f;
         for (int k = 0; k < N; ++k) {
@@ -2324,9 +2446,10 @@ __global__ __launch_bounds__(WV_BLOCK, (WvOcc<F16, SA>::occ)) void k_sweep_weak_
     PHASE_STAMP(22);  // (instrumented builds: P2a apart from P1b + P1c)
     // ---- P1b: current-plane tasks, lane = pixel, for the views with weight > 0
     const int cur_row = direct ? 0 : 8 * N;
+    const bool cur_shared = WV_CUR_MATCH && pv1 && ((L.flags[p1] >> 15) & 1u);  // (P2a wrote its row)
     for (int v = wave; v < N; v += WV_WAVES) {
         float val = 0.0f;
-        const bool want = pv1 && wts[v * VM_P + p1] > 0;
+        const bool want = pv1 && wts[v * VM_P + p1] > 0 && !cur_shared;
         LANE_STAT(24, want);
         if (__ballot(want)) {
             const float4 pl = L.hyp[8 * VM_P + p1];
@@ -2344,7 +2467,7 @@ __global__ __launch_bounds__(WV_BLOCK, (WvOcc<F16, SA>::occ)) void k_sweep_weak_
                 if (geom) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
             }
         }
-        costL[(cur_row + v) * VM_P + p1] = val;
+        if (!cur_shared) costL[(cur_row + v) * VM_P + p1] = val;
     }
     __syncthreads();
 
@@ -2626,6 +2749,12 @@ __global__ __launch_bounds__(WV_BLOCK, (WvOcc<F16, SA>::occ)) void k_sweep_weak_
 // k_weak_cand_g's workgroups: 8 waves, wave h = anchor candidate h
 #define PK_WAVES 8
 #define PK_BLOCK (PK_WAVES * WAVE)
+#ifndef PK_MINW
+#define PK_MINW 1  // k_weak_cand_g workgroups per CU the registers are bounded for
+#endif
+#ifndef PK_PIPE
+#define PK_PIPE true  // k_weak_cand_g's centre windows software-pipelined by columns
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // Image-wide anchor-window pairs (no SA masks). A WEAK pixel's anchor candidate h (the plane of its
@@ -3176,7 +3305,7 @@ __device__ __forceinline__ float gp_combine(float cc, const float (&sc)[8]) {
 // when anchor 0 carries the label (else center_cost stays 0, APD.cu:493-497) and its taps are
 // filtered by it (APD.cu:526-530); an empty window leaves center_cost 0 (APD.cu:543).
 template <bool F16, bool SA>
-__global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__restrict__ list, int count,
+__global__ __launch_bounds__(PK_BLOCK, PK_MINW) void k_weak_cand_g(Args a, const int *__restrict__ list, int count,
                                                           const uint8_t *__restrict__ cbw, float *__restrict__ out, int wc) {
     using TT = FastTex<F16, true>;  // (FastTexD measured 1.4 % slower per iteration here, profiles/r5_ab_dtex_kernels.txt)
     // (fp16 reference taps when the images are: fp32 measured 6 % slower, profiles/r4_ab_cand_g_fp32_ref.txt)
@@ -3275,7 +3404,7 @@ __global__ __launch_bounds__(PK_BLOCK) void k_weak_cand_g(Args a, const int *__r
         if (__ballot(live)) {
             const bool fast = live && window_rcp_ok(Hm, (float)(ax - 5), (float)(ay - 5));
             float ss = 0.0f, sss = 0.0f, srs = 0.0f;
-            ncc_new_window<F16, 6, 2>(a, &cref[p1], VM_P, tm, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
+            ncc_new_window<F16, 6, 2, PK_PIPE>(a, &cref[p1], VM_P, tm, Hm, ax, ay, live, fast, T, Q, ss, sss, srs);
             if (live) {
                 const float wsum = (float)cws[p1];
                 if (wsum != 0.0f) center_cost = ncc_finalize(csr[p1], csrr[p1], ss, sss, srs, wsum);
@@ -3412,6 +3541,9 @@ __global__ __launch_bounds__(BLOCK) void k_filter(Args a, const int *__restrict_
 // and the peak analysis. Waves skip every task none of their pixels selected (selected_views is
 // spatially coherent), which the lanes = views layout could not.
 // ---------------------------------------------------------------------------------------------
+#ifndef DW_EARLY
+#define DW_EARLY 1  // DepthToWeak: the inner disparity band first; pixels it decides skip the others
+#endif
 #ifndef DW_LDS_BUDGET
 #define DW_LDS_BUDGET 53248  // bytes per workgroup: 3 per CU (8 disparities per chunk at N = 8; 2 per CU with 16 was 7 % slower)
 #endif
@@ -3423,6 +3555,8 @@ struct DwLds {
     float rmean[VM_P], rvar[VM_P];  // reference-window moments (RefWin)
     uint32_t sel[VM_P];
     uint8_t active[VM_P];
+    uint8_t early[VM_P];        // decided WEAK by the inner disparity band (DW_EARLY)
+    int undecided;              // some pixel of the workgroup is not (DW_EARLY)
     int pxy[VM_P];              // px | py << 16
     int vcnt[32];               // active pixels that selected view v
 };
@@ -3508,19 +3642,60 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
     // others' costs are never read), packed 64 to a wave-task, disparity-major, dealt round-robin over
     // the waves in view order -- the 4 waves sample one source image at neighbouring disparities.
     if (wave == 0) { L.rmean[p] = rw.mean; L.rvar[p] = rw.var; }
-    for (int v = wave; v < N; v += VM_WAVES) {
-        const bool on = act && ((sv >> v) & 1u);
-        const uint64_t m = __ballot(on);
-        if (on) vslot[v * VM_P + __popcll(m & ((1ull << lane) - 1ull))] = (uint8_t)p;
-        if (lane == 0) L.vcnt[v] = __popcll(m);
-    }
+    auto build_vslot = [&](bool live) {
+        for (int v = wave; v < N; v += VM_WAVES) {
+            const bool on = live && ((sv >> v) & 1u);
+            const uint64_t m = __ballot(on);
+            if (on) vslot[v * VM_P + __popcll(m & ((1ull << lane) - 1ull))] = (uint8_t)p;
+            if (lane == 0) L.vcnt[v] = __popcll(m);
+        }
+    };
+    build_vslot(act);
+    if (wave == 0) L.early[p] = 0;
     __syncthreads();
     // The peak analysis reads the costs of disparities 1..59 only (and disparity 0 when no peak is found
     // and weak_peak_radius >= 30): disparities 0 and 60 are evaluated only for the curve export.
     const bool ends = a.curve != nullptr || a.peak_radius >= 30;
     const int dlo = ends ? 0 : 1, dhi = ends ? 61 : 60;
-    for (int d0 = dlo; d0 < dhi; d0 += chunk) {
-        const int dc = min(chunk, dhi - d0);
+    // Early decision (no curve export, peak radius R < 30): a pixel is STRONG only if some local
+    // minimum i of its curve with |i - 30| <= R costs <= 0.5 -- otherwise the minimum peak lies
+    // outside the radius, or costs > 0.5, or there is no peak, and P3 says WEAK whatever the other
+    // disparities give. So the band [b0, b1) holding those i and their neighbours (and LocalRefine's
+    // hand-over, disparities 25..35) runs first, and the pixels it decides skip the rest: the same
+    // states, and the same curve values wherever P3 reads them.
+    const bool early = DW_EARLY && !ends;
+    const int b0 = early ? max(dlo, min(25, 29 - a.peak_radius)) : dlo;
+    const int b1 = early ? min(dhi, max(36, 32 + a.peak_radius)) : dhi;
+    bool verdicts = false;  // (workgroup-uniform)
+    for (int sg = 0; sg < 3; ++sg) {
+      const int s0 = sg == 0 ? b0 : (sg == 1 ? dlo : b1);
+      const int s1 = sg == 0 ? b1 : (sg == 1 ? b0 : dhi);
+      if (s0 >= s1) continue;
+      if (sg > 0 && early && !verdicts) {
+          // (once, after the band) the band's verdicts; the undecided pixels' task lists
+          bool keep = false;
+          if (wave == 0 && act) {
+              const float *pcp = &L.pc[p];
+              const int lo = max(2, 30 - a.peak_radius), hi = min(58, 30 + a.peak_radius);
+              for (int i = lo; i <= hi; ++i) {
+                  const float ci = pcp[i * VM_P];
+                  keep = keep || (pcp[(i - 1) * VM_P] > ci && pcp[(i + 1) * VM_P] > ci && ci <= 0.5f);
+              }
+              L.early[p] = !keep;
+          }
+          if (wave == 0) {
+              const bool any_keep = __ballot(keep) != 0ull;
+              if (lane == 0) L.undecided = any_keep;
+          }
+          __syncthreads();
+          if (!L.undecided) break;  // every pixel decided (or inactive)
+          build_vslot(act && !L.early[p]);
+          verdicts = true;
+          __syncthreads();
+      }
+      const int nch = (s1 - s0 + chunk - 1) / chunk, cseg = (s1 - s0 + nch - 1) / nch;  // even chunks
+      for (int d0 = s0; d0 < s1; d0 += cseg) {
+        const int dc = min(cseg, s1 - d0);
         // t / dc for the task decode as a multiply-high: with m = ceil(2^32 / dc), umulhi(t, m) == t / dc
         // for every t < 2^32 / dc (here t < 61 * 64); dc == 1 (m = 2^32) is taken apart
         const uint32_t mdc = dc > 1 ? 0xFFFFFFFFu / (uint32_t)dc + 1u : 0u;
@@ -3639,11 +3814,14 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_depth_to_weak_vm(Args a, 
             if (a.curve && act) a.curve[(size_t)c * 61 + d] = val;
         }
         __syncthreads();
+      }
     }
     // ---- P3: peak analysis (APD.cu:2200-2248)
     if (wave == 0 && pv) {
         int state = APD_UNKNOWN;
-        if (act) {
+        if (act && L.early[p]) {
+            state = APD_WEAK;  // (decided by the band)
+        } else if (act) {
             const float *pc = &L.pc[p];
             int cnt = 0, min_peak = 0;
             float min_cost = 2.0f;

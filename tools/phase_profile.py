@@ -35,7 +35,7 @@ for lo, hi, title in ((8, 12, "k_weak_cand_vm"), (0, 7, "k_sweep_weak_vm")):
         print(f"  (of P2a: geometric terms, thread 0's own time {100.0 * c[15] / max(c[30] or c[10], 1):5.1f} %)")
 t = eng.timing()
 print(f"iteration ms {list(t.iter_ms)[:t.iterations]}")
-for slot, what in ((16, "sweep P1c anchor hypothesis taken"), (20, "sweep P5 refinement tasks"), (22, "sweep P3 fit-plane tasks"), (24, "sweep P1b current-plane tasks"),
+for slot, what in ((0, "sweep P0 pixels"), (2, "sweep P0 current plane = an anchor candidate's"), (4, "sweep P0 fit plane = current plane"), (6, "sweep P0 fit plane = an anchor candidate's"), (16, "sweep P1c anchor hypothesis taken"), (20, "sweep P5 refinement tasks"), (22, "sweep P3 fit-plane tasks"), (24, "sweep P1b current-plane tasks"),
                    (26, "cand pair-window passes"), (28, "cand centre-window tasks")):
     if c[slot]:
         print(f"{what:32s} waves {c[slot]:>12d}  active lanes {c[slot + 1] / (64.0 * c[slot]):6.3f}")
