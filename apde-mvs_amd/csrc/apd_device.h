@@ -442,25 +442,29 @@ struct alignas(16) SaWin {
     uint32_t mlo, mhi;  // visited slots: bit k of (mhi:mlo)
     float sr, srr;      // sum r, sum r*r over the visited slots, in visiting order
 };
-struct RefWin {
-    const float *r;    // 36 values in LDS, column-major (i*6 + j), element k at r[k * stride]
+// RT: the reference taps' storage type in LDS -- float, or _Float16 where the images are exactly
+// fp16-representable (the Strong sweep's taps; every read converts exactly to the same fp32 value)
+template <class RT = float>
+struct RefWinT {
+    const RT *r;       // 36 values in LDS, column-major (i*6 + j), element k at r[k * stride]
     float mean, var;   // sum_ref/36 and sum_ref_ref/36 - mean^2, same op order as the oracle
     const SaWin *sa = nullptr;  // view-major kernels with SA masks: the pixel's SaWin in LDS
 };
+using RefWin = RefWinT<float>;
 // mean / variance of a reference window already in LDS (element k at r[k * RS])
-template <int RS>
-__device__ __forceinline__ RefWin refwin_from_lds(const float *r) {
+template <int RS, class RT = float>
+__device__ __forceinline__ RefWinT<RT> refwin_from_lds(const RT *r) {
     float sr = 0.0f, srr = 0.0f;
 #pragma unroll
     for (int k = 0; k < 36; ++k) {
-        const float x = r[k * RS];
+        const float x = (float)r[k * RS];
         sr += x;
         srr = fmaf(x, x, srr);
     }
     const float inv = 1.0f / 36.0f;
     sr *= inv;
     srr *= inv;
-    RefWin w;
+    RefWinT<RT> w;
     w.r = r;
     w.mean = sr;
     w.var = fmaf(-sr, sr, srr);
@@ -729,8 +733,8 @@ struct FastTexD {
 // The 36 taps of a ComputeBilateralNCCOld window (6x6, step 2) and their moments, for a texel source
 // TT with the FastTex interface (tap / load / finish). Accumulation order = the reference's (i outer,
 // j inner). (Factored out of ncc_old_fast; the Strong sweep measured 3 % faster with this form.)
-template <class TT, int RS>
-__device__ __forceinline__ void ncc_old_taps(const TT &T, const Hom &Hm, int px, int py, const RefWin &rw, float &ss,
+template <class TT, int RS, class RW>
+__device__ __forceinline__ void ncc_old_taps(const TT &T, const Hom &Hm, int px, int py, const RW &rw, float &ss,
                                              float &sss, float &srs) {
         using FT = TT;
         auto column = [&](int i, typename FT::Tap *t) {
@@ -751,7 +755,7 @@ __device__ __forceinline__ void ncc_old_taps(const TT &T, const Hom &Hm, int px,
                 const float v = T.finish(t[j], q[j]);
                 ss += v;
                 // (sss, srs) = (fma(v, v, sss), fma(r, v, srs))
-                const apd_f2 acc = pk_fma((apd_f2){v, rw.r[(i * 6 + j) * RS]}, (apd_f2){v, v}, (apd_f2){sss, srs});
+                const apd_f2 acc = pk_fma((apd_f2){v, (float)rw.r[(i * 6 + j) * RS]}, (apd_f2){v, v}, (apd_f2){sss, srs});
                 sss = acc.x;
                 srs = acc.y;
             }
@@ -796,8 +800,8 @@ __device__ __forceinline__ void ncc_old_taps(const TT &T, const Hom &Hm, int px,
 // 6, software-pipelined as ncc_old_taps), the slots the pixel's SaWin does not visit contributing
 // exact zeros: the partial sums start at +0 and are never -0, so x + (+-0) == x bit-for-bit.
 // Same (X, Y, Z) expressions as project().
-template <class TT, int RS>
-__device__ __forceinline__ void ncc_old_sa_taps(const TT &T, const Hom &Hm, int px, int py, const float *r,
+template <class TT, int RS, class RT>
+__device__ __forceinline__ void ncc_old_sa_taps(const TT &T, const Hom &Hm, int px, int py, const RT *r,
                                                 const SaWin &w, float &ss, float &sss, float &srs) {
     auto group = [&](int g, typename TT::Tap *t) {
 #pragma unroll
@@ -817,7 +821,7 @@ __device__ __forceinline__ void ncc_old_sa_taps(const TT &T, const Hom &Hm, int 
             const uint32_t on = k < 32 ? (w.mlo >> k) & 1u : (w.mhi >> (k - 32)) & 1u;
             const float v = on ? T.finish(t[j], q[j]) : 0.0f;
             ss += v;
-            const apd_f2 acc = pk_fma((apd_f2){v, r[sa_grid(k) * RS]}, (apd_f2){v, v}, (apd_f2){sss, srs});
+            const apd_f2 acc = pk_fma((apd_f2){v, (float)r[sa_grid(k) * RS]}, (apd_f2){v, v}, (apd_f2){sss, srs});
             sss = acc.x;
             srs = acc.y;
         }
@@ -844,9 +848,9 @@ __device__ __forceinline__ void ncc_old_sa_taps(const TT &T, const Hom &Hm, int 
 
 // IEEE-division statement of the ComputeBilateralNCCOld window sum (taken only for windows that
 // window_rcp_ok rejects).
-template <bool F16>
+template <bool F16, class RT = float>
 __device__ __forceinline__ apd_f2 ncc_old_ieee(const APD_G Args *ap, int px, int py, int s, const Hom &Hm,
-                                               const float *r, int rs, float *sss_out) {
+                                               const RT *r, int rs, float *sss_out) {
     const APD_G Args &a = *ap;
     const SrcTex<F16> Q(a, s);
     const float Wm1 = (float)(a.W - 1), Hm1 = (float)(a.H - 1);
@@ -867,7 +871,7 @@ __device__ __forceinline__ apd_f2 ncc_old_ieee(const APD_G Args *ap, int px, int
             const float v = bilerp(Q.fetch(t.idx), t.ax, t.ay);
             ss += v;
             sss = fmaf(v, v, sss);
-            srs = fmaf(r[(i * 6 + j) * rs], v, srs);
+            srs = fmaf((float)r[(i * 6 + j) * rs], v, srs);
         }
     }
     *sss_out = sss;
@@ -887,8 +891,8 @@ __device__ __forceinline__ float ncc_old_finish(float ss, float sss, float srs, 
 // Out-of-line ComputeBilateralNCCOld for the windows ncc_old_fast hands back: the SA quadrant
 // variant, or windows whose taps need the IEEE reciprocal. Everything arrives by value (the
 // homography is recomputed from the plane), so the hot path never spills a homography to the stack.
-template <bool F16>
-__device__ __noinline__ float ncc_old_slow(const APD_G Args *ap, int px, int py, int s, float4 pl, const float *r,
+template <bool F16, class RT = float>
+__device__ __noinline__ float ncc_old_slow(const APD_G Args *ap, int px, int py, int s, float4 pl, const RT *r,
                                            int rs, float mean, float var) {
     const APD_G Args &a = *ap;
     const Hom Hm = homography(a, s, pl);
@@ -900,7 +904,7 @@ __device__ __noinline__ float ncc_old_slow(const APD_G Args *ap, int px, int py,
         if (a.sa[pidx] != 0) return ncc_old_sa<F16>(ap, px, py, s, Hm, a.sa[py * a.W + px]);
     }
     float sss;
-    const apd_f2 rr = ncc_old_ieee<F16>(ap, px, py, s, Hm, r, rs, &sss);
+    const apd_f2 rr = ncc_old_ieee<F16, RT>(ap, px, py, s, Hm, r, rs, &sss);
     return ncc_old_finish(rr.x, sss, rr.y, mean, var);
 }
 
@@ -910,8 +914,8 @@ __device__ __noinline__ float ncc_old_slow(const APD_G Args *ap, int px, int py,
 // is then meaningless (the taps ran on a dummy homography that keeps every address in bounds).
 // RS = LDS stride of the reference window (1: per-pixel contiguous; 64: [k][pixel] layout).
 // (ncc_old_fast_h: the same with the window's homography given, e.g. from precomputed plane_terms)
-template <bool F16, int RS = 1, bool DP = false>
-__device__ __forceinline__ float ncc_old_fast_h(const Args &a, int px, int py, int s, Hom Hm, const RefWin &rw,
+template <bool F16, int RS = 1, bool DP = false, class RW = RefWin>
+__device__ __forceinline__ float ncc_old_fast_h(const Args &a, int px, int py, int s, Hom Hm, const RW &rw,
                                                 bool &slow) {
     // DP: the taps over the pre-differenced texels (FastTexD, F16 problems with a.dpairs)
     using TT = typename std::conditional<DP && F16, FastTexD<(RS > 1)>, FastTex<F16, (RS > 1)>>::type;
@@ -954,10 +958,10 @@ __device__ __forceinline__ float ncc_old_fast_h(const Args &a, int px, int py, i
     ncc_old_taps<TT, RS>(T, Hm, px, py, rw, ss, sss, srs);
     return ncc_old_finish(ss, sss, srs, rw.mean, rw.var);
 }
-template <bool F16, int RS = 1>
-__device__ __forceinline__ float ncc_old_fast(const Args &a, int px, int py, int s, float4 pl, const RefWin &rw,
+template <bool F16, int RS = 1, class RW = RefWin>
+__device__ __forceinline__ float ncc_old_fast(const Args &a, int px, int py, int s, float4 pl, const RW &rw,
                                               bool &slow) {
-    return ncc_old_fast_h<F16, RS>(a, px, py, s, homography(a, s, pl), rw, slow);
+    return ncc_old_fast_h<F16, RS, false, RW>(a, px, py, s, homography(a, s, pl), rw, slow);
 }
 
 

@@ -1138,19 +1138,41 @@ __device__ __forceinline__ float4 candidate(const Cands &C, int k, float4 cur0, 
 #ifndef APD_VM_LDS_PAD
 #define APD_VM_LDS_PAD 0  // experiments: extra LDS bytes per workgroup (fewer workgroups per CU)
 #endif
-// 44 KB at N = 8: three workgroups fit a CU's 160 KB of LDS (the VGPR budget allows three).
-struct VmLds {  // static part; the cost table [9][N][64] and the weights [N][64] (uint8) follow
-    float refw[36 * VM_P];       // [k][p]
+// SS_LDS40 (fp16 problems): the reference taps as fp16 (exact there), the neighbour flags as bits and
+// the view selection's draws regenerated per (pixel, view) lane instead of kept in LDS -- 40.8 KB at
+// N = 10 (48.4 before): four workgroups per CU instead of three (the VGPRs bounded to match).
+#ifndef SS_LDS40
+#define SS_LDS40 1
+#endif
+template <class RT>
+struct VmLdsT {  // static part; the cost table [9][N][64] and the weights [N][64] (uint8) follow
+    RT refw[36 * VM_P];          // [k][p]
     float4 hyp[9 * VM_P];        // [h][p]: 8 propagated + current; P2 overwrites [0..4] with the
                                  // refinement candidates (VM_CAND) once the pixel's reads are done
+#if SS_LDS40
+    uint8_t nvq[4 * VM_P];       // [w][p]: bit r = neighbour d = w + 4r exists (P0's wave w writes its own byte)
+#else
     uint8_t nval[8 * VM_P];      // [d][p]: neighbour d exists (adaptive-checkerboard scan hit)
+#endif
     float4 pnow[VM_P];
     float st[4 * VM_P];          // depth_now, cost_now, cost_init, weight_norm
+#if !SS_LDS40
     float vsu[VS_DRAWS * VM_P];  // [k][p]: the view selection's 15 uniform() draws of the pixel's stream
+#endif
     uint32_t tsel[VM_P];         // views with a sampled weight > 0
     float rmean[VM_P], rvar[VM_P];  // reference-window moments (RefWin) of pixel slot p (P3's packed items)
     int pxy[VM_P];               // packed (x, y) of pixel slot p
 };
+template <bool F16>
+using VmRefT = typename std::conditional<SS_LDS40 && F16, _Float16, float>::type;
+template <class RT>
+__device__ __forceinline__ bool vm_nval(const VmLdsT<RT> &L, int d, int p) {
+#if SS_LDS40
+    return (L.nvq[(d & 3) * VM_P + p] >> (d >> 2)) & 1u;
+#else
+    return L.nval[d * VM_P + p] != 0;
+#endif
+}
 #ifndef SS_P3_CHUNKS
 #define SS_P3_CHUNKS 3  // Strong sweep P3 batches: whole views until at least this many 64-item chunks
 #endif
@@ -1158,8 +1180,9 @@ struct VmLds {  // static part; the cost table [9][N][64] and the weights [N][64
 // per-pixel SaWin table appended to the view-major kernels' dynamic LDS when the problem has SA masks
 static inline size_t sa_lds_bytes(const Args &a) { return a.sa_any ? VM_P * sizeof(SaWin) + 16 : 0; }
 __device__ __forceinline__ void *sa_lds_align(void *p) { return (void *)(((uintptr_t)p + 15) & ~(uintptr_t)15); }     // [k][p], k < 5: refinement candidates (t.w = distance)
-static inline size_t vm_lds_bytes(int N) {
-    return APD_VM_LDS_PAD + sizeof(VmLds) + (size_t)9 * N * VM_P * sizeof(float) + (size_t)N * VM_P;
+static inline size_t vm_lds_bytes(int N, bool f16) {
+    return APD_VM_LDS_PAD + (f16 ? sizeof(VmLdsT<VmRefT<true>>) : sizeof(VmLdsT<VmRefT<false>>)) +
+           (size_t)9 * N * VM_P * sizeof(float) + (size_t)N * VM_P;
 }
 
 // One direction of the adaptive checkerboard (APD.cu:1127-1316): d = 2*dir + far, dir in
@@ -1266,9 +1289,10 @@ template <bool F16, bool SA>
 #ifndef VM_MINW
 #define VM_MINW 3  // waves per SIMD -> VGPR budget 512 / VM_MINW
 #endif
-__global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, const int *__restrict__ list, int count,
+__global__ __launch_bounds__(VM_BLOCK, (SS_LDS40 && F16 && !SA) ? 4 : VM_MINW) void k_sweep_strong_vm(Args a, const int *__restrict__ list, int count,
                                                                   int iter) {
     const int N = a.N, W = a.W, H = a.H;
+    using VmLds = VmLdsT<VmRefT<F16>>;
     VmLds &L = *reinterpret_cast<VmLds *>(apd_dyn_lds);
     float *costL = reinterpret_cast<float *>(&L + 1);                   // [9][N][64], later [5][N][64]
     uint8_t *wts = reinterpret_cast<uint8_t *>(costL + 9 * N * VM_P);    // [N][64] view weights
@@ -1305,18 +1329,25 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const int d = wave + 4 * r;
+#if !SS_LDS40
                 L.nval[d * VM_P + p] = q[r] >= 0;
+#endif
                 if (q[r] >= 0) L.hyp[d * VM_P + p] = hp[r];
             }
+#if SS_LDS40
+            L.nvq[wave * VM_P + p] = (uint8_t)((q[0] >= 0 ? 1u : 0u) | (q[1] >= 0 ? 2u : 0u));
+#endif
             if (wave == 0) { L.hyp[8 * VM_P + p] = hp[2]; L.pxy[p] = px | (py << 16); }
 #pragma unroll
-            for (int kk = 0; kk < 36 / VM_WAVES; ++kk) L.refw[(wave + VM_WAVES * kk) * VM_P + p] = rv[kk];
+            for (int kk = 0; kk < 36 / VM_WAVES; ++kk) L.refw[(wave + VM_WAVES * kk) * VM_P + p] = (VmRefT<F16>)rv[kk];
             if (SA && wave == VM_WAVES - 1) saw[p] = sa_window(a, px, py);
+#if !SS_LDS40
             if (wave == 1 % VM_WAVES) {  // the view selection's draws, once per pixel (not per view lane)
                 Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c, ord_strong(iter));
 #pragma unroll
                 for (int k = 0; k < VS_DRAWS; ++k) L.vsu[k * VM_P + p] = rg.uniform();
             }
+#endif
         }
     }
     __syncthreads();
@@ -1326,7 +1357,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     const bool pv1 = p1 < np;
     int c1 = 0, px1 = 0, py1 = 0;
     if (pv1) { c1 = list[first + p1]; py1 = c1 / W; px1 = c1 - py1 * W; }
-    RefWin rw = refwin_from_lds<VM_P>(&L.refw[p1]);
+    RefWinT<VmRefT<F16>> rw = refwin_from_lds<VM_P>(&L.refw[p1]);
     if (SA) rw.sa = &saw[p1];
     if (wave == 0 && pv1) { L.rmean[p1] = rw.mean; L.rvar[p1] = rw.var; }  // (read after P1's barrier)
     // tasks whose window needs the out-of-line path are collected in `defer` (bit k = k-th task of
@@ -1341,7 +1372,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
     for (int u = wave, k = 0; u < 9 * N; u += VM_WAVES, ++k) {
         const int v = u / 9, h = u - 9 * v, t = h * N + v;
         float val = (h == 0 && v == 0) ? 2.0f : 0.0f;  // float cost_array[8][32] = {2.0f} (APD.cu:1120)
-        const bool fh = h == 8 || L.nval[h * VM_P + p1];
+        const bool fh = h == 8 || vm_nval(L, h, p1);
         if (pv1 && fh) {
             const float4 pl = L.hyp[h * VM_P + p1];
             if (h == 8 && a.wcur) {  // iteration 0: RandomInitialization's NCC-Old of this plane
@@ -1362,7 +1393,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
         defer[w2] &= defer[w2] - 1;
         const int u = wave + k * VM_WAVES, v = u / 9, h = u - 9 * v, t = h * N + v;
         const float4 pl = L.hyp[h * VM_P + p1];
-        float val = ncc_old_slow<F16>(a.self, px1, py1, v + 1, pl, rw.r, VM_P, rw.mean, rw.var);
+        float val = ncc_old_slow<F16, VmRefT<F16>>(a.self, px1, py1, v + 1, pl, rw.r, VM_P, rw.mean, rw.var);
         if (h == 8 && geom_imp) val = fmaf(gf, geom_cost(a, px1, py1, v + 1, pl), val);
         costL[t * VM_P + p1] = val;
     }
@@ -1393,9 +1424,14 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
             const int nb[4] = {c - W, c + W, c - 1, c + 1};
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                if (L.nval[(2 * i) * VM_P + p]) prior += ((a.sel[nb[i]] >> v) & 1u) ? 0.9f : 0.1f;
+                if (vm_nval(L, 2 * i, p)) prior += ((a.sel[nb[i]] >> v) & 1u) ? 0.9f : 0.1f;
         }
+#if SS_LDS40
+        Rng rg(a.seed_lo, a.seed_hi, (uint32_t)c, ord_strong(iter));  // (the pixel's 15 draws, per lane)
+        const int w = view_selection(ca, prior, iter, rg, G, N);
+#else
         const int w = view_selection_u(ca, prior, iter, &L.vsu[p], VM_P, G, N);
+#endif
         const uint32_t tsel = group_bits(w > 0, G);
         if (G.valid) {
             wts[v * VM_P + p] = (uint8_t)w;
@@ -1438,7 +1474,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
             float fcm = fc[0];
 #pragma unroll
             for (int k = 1; k < 8; ++k) if (mi == k) fcm = fc[k];
-            if (L.nval[mi * VM_P + p]) {
+            if (vm_nval(L, mi, p)) {
                 const float4 cand = L.hyp[mi * VM_P + p];
                 const float db = depth_from_plane(cam0, cand, px, py);
                 if (db >= a.dmin && db <= a.dmax && fcm < cost_now) {
@@ -1531,7 +1567,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
                     const int px = xy & 0xFFFF, py = xy >> 16;
                     bool slow = false;
                     if (want) {
-                        const RefWin rwq{&L.refw[p], L.rmean[p], L.rvar[p], SA ? &saw[p] : nullptr};
+                        const RefWinT<VmRefT<F16>> rwq{&L.refw[p], L.rmean[p], L.rvar[p], SA ? &saw[p] : nullptr};
                         const float4 tp = VM_CAND(L)[k * VM_P + p];
                         ++issued;
                         float cv = ncc_old_fast<F16, VM_P>(a, px, py, v + 1, tp, rwq, slow);
@@ -1566,7 +1602,7 @@ __global__ __launch_bounds__(VM_BLOCK, VM_MINW) void k_sweep_strong_vm(Args a, c
                             const int xy = L.pxy[p];
                             const int px = xy & 0xFFFF, py = xy >> 16;
                             const float4 tp = VM_CAND(L)[k * VM_P + p];
-                            float cv = ncc_old_slow<F16>(a.self, px, py, v + 1, tp, &L.refw[p], VM_P, L.rmean[p], L.rvar[p]);
+                            float cv = ncc_old_slow<F16, VmRefT<F16>>(a.self, px, py, v + 1, tp, &L.refw[p], VM_P, L.rmean[p], L.rvar[p]);
                             if (geom_imp) cv = fmaf(gf, geom_cost(a, px, py, v + 1, tp), cv);
                             costL[(k * N + v) * VM_P + p] = cv;
                         }
@@ -5287,7 +5323,7 @@ int32_t apd_stage_iteration(apd_ctx *ctx, int32_t iter) {
         Args ak = a;
         ak.evals = evals;
         if (!(ctx->wcur_fresh && iter == 0)) ak.wcur = nullptr;  // RandomInitialization's costs: iteration 0 only
-        LAUNCH_TEX_SA(k_sweep_strong_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), vm_lds_bytes(a.N) + sa_lds_bytes(a), s,
+        LAUNCH_TEX_SA(k_sweep_strong_vm, dim3(blocks_for((size_t)n, VM_P)), dim3(VM_BLOCK), vm_lds_bytes(a.N, ctx->args.tex_f16 != 0) + sa_lds_bytes(a), s,
                       ak, (const int *)list_ptr(ctx, colour), n, iter);
         prof_end(ctx, e0, APD_PROF_STRONG_SWEEP, n);
         if ((st = check_launch(ctx, "k_sweep_strong"))) return st;
