@@ -143,6 +143,59 @@ def test_classify_random_curves_match_restatement(lib):
     assert mism == 0
 
 
+def band_decides_weak(pc, radius):
+    """k_depth_to_weak_vm's inner-band verdict (DW_EARLY): no local minimum i with |i - 30| <= radius
+    (and 2 <= i <= 58) costs <= 0.5, so the pixel is WEAK whatever its other samples are."""
+    for i in range(max(2, 30 - radius), min(58, 30 + radius) + 1):
+        if pc[i - 1] > pc[i] and pc[i + 1] > pc[i] and pc[i] <= 0.5:
+            return False
+    return True
+
+
+def test_inner_band_rule_is_exact(lib):
+    """The rule the GPU's DepthToWeak uses to skip the outer disparities of a pixel: whenever it says
+    WEAK, the reference's classification of the full curve (APD.cu:2200-2249, the oracle) is WEAK --
+    on random curves, on curves built around the band's edges, and whatever the outer samples hold
+    (they are redrawn). The band [min(25, 29 - r), max(36, 32 + r)) holds every sample the rule reads."""
+    rng = np.random.default_rng(11)
+    decided = 0
+    for t in range(6000):
+        r = int(rng.choice([2, 4, 6]))
+        if t % 3 == 0:
+            pc = rng.integers(0, 129, 61) / 64.0
+        elif t % 3 == 1:  # a minimum near the band's edge or just above the 0.5 limit
+            c = 30 + int(rng.choice([-r - 1, -r, r, r + 1]))
+            pc = multi([(c, rng.choice([0.25, 0.5, 33 / 64.0]))] +
+                       [(int(rng.integers(2, 59)), rng.integers(0, 40) / 64.0) for _ in range(rng.integers(0, 3))],
+                       slope=rng.integers(1, 8) / 64.0)
+        else:
+            pc = multi([(int(rng.integers(2, 59)), rng.integers(0, 40) / 64.0) for _ in range(rng.integers(1, 4))],
+                       slope=rng.integers(1, 8) / 64.0)
+        pc = np.round(np.asarray(pc, np.float64) * 64) / 64
+        lo, hi = min(25, 29 - r), max(36, 32 + r)
+        assert lo <= max(2, 30 - r) - 1 and min(58, 30 + r) + 1 < hi
+        if not band_decides_weak(pc, r):
+            continue
+        decided += 1
+        assert oracle_classify(lib, pc, r) == A.WEAK
+        # the verdict does not depend on the samples outside the band
+        pc2 = pc.copy()
+        outer = np.r_[0:lo, hi:61]
+        pc2[outer] = rng.integers(0, 129, outer.size) / 64.0
+        assert oracle_classify(lib, pc2, r) == A.WEAK
+    assert decided > 1000
+    # control: a qualifying minimum at the band's edge (cost 0.5, |i - 30| = r) is not decided, and
+    # the full curve can be STRONG
+    pc = vee(30 + 4, 0.5)
+    assert not band_decides_weak(pc, 4)
+    pc = vee(30 + 4, 0.10)
+    assert not band_decides_weak(pc, 4) and oracle_classify(lib, pc, 4) == A.STRONG
+    # mutation control (a band rule with < 0.5 instead of <= 0.5 would be wrong): an inner minimum of
+    # exactly 0.5 with a far peak 0.28 above it is STRONG by the spread test
+    pc = multi([(30, 0.5), (10, 0.78)])
+    assert oracle_classify(lib, pc, 4) == A.STRONG and not band_decides_weak(pc, 4)
+
+
 def test_classify_matches_exported_curves():
     """--export_curve (APD.cu:2188-2198): every pixel DepthToWeak classified from a curve gets the
     state the numpy restatement gives that exported curve (FIRST_INIT: nothing changes the states
