@@ -2889,6 +2889,12 @@ __global__ __launch_bounds__(BLOCK) void k_gp_count(Args a, const int *__restric
 // its window anchor's segment, and every reference keeps its own (loc[WEAK index * 8 + k - 1]);
 // k_gp_place then writes each reference at segment offset + place -- no second pass of atomics
 // (k_gp_fill, the path APD_GP_FILL=1 keeps)
+#ifndef GP_LOC_BLOCK
+#define GP_LOC_BLOCK 1  // k_gp_count_loc: per-workgroup aggregation of the anchors' counts in LDS
+#endif
+#define GP_LOC_LG 12
+#define GP_LOC_HS (1 << GP_LOC_LG)  // >= 2 x the 8 * BLOCK references a workgroup can hold: load <= 0.5
+static_assert(GP_LOC_HS >= 2 * 8 * BLOCK, "k_gp_count_loc LDS table sizing");
 __global__ __launch_bounds__(BLOCK) void k_gp_count_loc(Args a, const int *__restrict__ list, int count, int *__restrict__ cnt,
                                                         uint8_t *__restrict__ cbw, uint8_t *__restrict__ wmw,
                                                         uint32_t *__restrict__ loc) {
@@ -2918,6 +2924,49 @@ __global__ __launch_bounds__(BLOCK) void k_gp_count_loc(Args a, const int *__res
     int pos[8];
     bool okk[8];
     int hl[8], rk[8];
+#if GP_LOC_BLOCK
+    // The workgroup's references aggregated per window anchor in LDS first (the runs' lengths added
+    // into a per-anchor local count, whose returned value is the run's offset within the workgroup),
+    // then one global atomic per distinct anchor of the workgroup: neighbouring tiles share their
+    // anchors, and same-address global atomics from the whole GPU serialised the per-run version.
+    // Positions stay unique within each anchor's segment (their order is a label, as before).
+    __shared__ int hkey[GP_LOC_HS], hcnt[GP_LOC_HS];  // anchor q + 1 (0: empty); count, then global base
+    for (int t = threadIdx.x; t < GP_LOC_HS; t += BLOCK) { hkey[t] = 0; hcnt[t] = 0; }
+    __syncthreads();
+    int slot[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (valid[k] && wst[k] == APD_STRONG) cb |= 1u << k;
+        okk[k] = valid[k] && (cid == 0 || lab[k] == cid);  // (gp_window_used)
+        if (okk[k]) wm |= 1u << k;
+        int len;
+        gp_run(okk[k], q[k], hl[k], rk[k], len);
+        int sl = 0, lp = 0;
+        if (okk[k] && rk[k] == 0) {
+            const int key = q[k] + 1;
+            sl = (int)(((uint32_t)key * 0x9E3779B1u) >> (32 - GP_LOC_LG));
+            for (;;) {
+                const int cur = hkey[sl];
+                if (cur == key) break;
+                if (cur == 0) {
+                    const int old = atomicCAS(&hkey[sl], 0, key);
+                    if (old == 0 || old == key) break;
+                }
+                sl = (sl + 1) & (GP_LOC_HS - 1);
+            }
+            lp = atomicAdd(&hcnt[sl], len);
+        }
+        slot[k] = __shfl(sl, hl[k]);
+        pos[k] = __shfl(lp, hl[k]) + rk[k];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < GP_LOC_HS; t += BLOCK)
+        if (hkey[t] != 0) hcnt[t] = atomicAdd(&cnt[hkey[t] - 1], hcnt[t]);
+    __syncthreads();
+    uint32_t l[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) l[k] = (uint32_t)(hcnt[slot[k]] + pos[k]);  // (k_gp_place reads used windows only)
+#else
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         if (valid[k] && wst[k] == APD_STRONG) cb |= 1u << k;
@@ -2931,6 +2980,7 @@ __global__ __launch_bounds__(BLOCK) void k_gp_count_loc(Args a, const int *__res
     uint32_t l[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) l[k] = (uint32_t)(__shfl(pos[k], hl[k]) + rk[k]);  // (k_gp_place reads used windows only)
+#endif
     if (act) {
         uint4 *d = reinterpret_cast<uint4 *>(loc + (size_t)wi * 8);
         d[0] = make_uint4(l[0], l[1], l[2], l[3]);
